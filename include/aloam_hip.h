@@ -1,0 +1,224 @@
+/*
+ * aloam_hip.h — C ABI of the MI355X-native A-LOAM per-scan hot path.
+ *
+ * This is the drop-in boundary: plain C types, host pointers + sizes, no torch
+ * or HIP types in any signature. Every entry point replaces an inline hot block
+ * of the reference's three ROS nodes (reference = ucmmesa/Lidar-Visual-Odometry,
+ * an A-LOAM fork; citations are path:line relative to its repo root):
+ *
+ *   aloam_scan_registration  ->  src/scanRegistration.cpp:114-411   (laserCloudHandler body)
+ *   aloam_odometry           ->  src/laserOdometry.cpp:331-641      (main-loop body, incl. 10x Ceres solve)
+ *   aloam_mapping            ->  src/laserMapping.cpp:305-848       (process() body, incl. 10x Ceres solve)
+ *   aloam_factor (+ eval)    ->  src/lidarFactor.hpp:12-172         (LidarEdge/Plane/PlaneNorm/Distance factors)
+ *
+ * Threading: one caller thread per context, synchronous calls,
+ * one HIP stream per context. Several contexts may coexist in one process.
+ *
+ * Errors: 0 = ok, < 0 = error (ALOAM_E_*); aloam_last_error() has the text.
+ * The reference's soft conditions are NOT errors: "less correspondence!"
+ * (laserOdometry.cpp:566-568) still solves, and a too-small map skips the
+ * solve (laserMapping.cpp:554,730-733); both are reported in the result structs.
+ */
+#ifndef ALOAM_HIP_H
+#define ALOAM_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALOAM_ABI_VERSION 1
+
+/* error codes */
+#define ALOAM_OK             0
+#define ALOAM_E_ARG         -1   /* bad argument (NULL pointer, negative size)            */
+#define ALOAM_E_CAPACITY    -2   /* input larger than the capacity given at create time   */
+#define ALOAM_E_HIP         -3   /* HIP runtime error                                      */
+#define ALOAM_E_SCAN_LINES  -4   /* scan_line not in {16,32,64} and generic rule not opted in
+                                    (reference aborts: scanRegistration.cpp:201-205,472-476) */
+#define ALOAM_E_STATE       -5   /* call out of order (e.g. odometry before any features)  */
+#define ALOAM_E_NODEVICE    -6   /* no HIP device / extension unusable                     */
+
+/* flags for aloam_scan_registration */
+#define ALOAM_INPUT_DEVICE   1   /* xyzr points at device memory (already resident in HBM) */
+
+/* Launch parameters (launch/aloam_velodyne_*.launch) and the reference's
+ * hard-coded constants, which are kept overridable for tests. */
+typedef struct aloam_params {
+    int   scan_line;                /* scanRegistration.cpp:466 "scan_line" (16/32/64)              */
+    float minimum_range;            /* scanRegistration.cpp:468 "minimum_range"                     */
+    int   mapping_skip_frame;       /* laserOdometry.cpp:274   "mapping_skip_frame"                 */
+    float mapping_line_resolution;  /* laserMapping.cpp:902    "mapping_line_resolution"            */
+    float mapping_plane_resolution; /* laserMapping.cpp:903    "mapping_plane_resolution"           */
+    int   input_is_dense;           /* PointCloud2 is_dense: 1 => removeNaNFromPointCloud is a copy */
+    int   generic_scan_lines;       /* opt-in linear elevation->line rule for other line counts    */
+    float generic_min_elev_deg;     /*   lowest beam elevation (deg) for the generic rule          */
+    float generic_max_elev_deg;     /*   highest beam elevation (deg)                              */
+    int   odom_rounds;              /* laserOdometry.cpp:364  (10 in this fork)                    */
+    int   map_rounds;               /* laserMapping.cpp:562   (10 in this fork)                    */
+    int   max_solver_iterations;    /* laserOdometry.cpp:573 / laserMapping.cpp:715 (4)            */
+    int   max_scan_points;          /* capacity: raw points per scan                               */
+    int   max_map_points;           /* capacity: points of corner+surf map                         */
+} aloam_params;
+
+/* A point cloud in caller-owned host memory: n points of float4 (x,y,z,intensity)
+ * = pcl::PointXYZI without its padding (include/aloam_velodyne/common.h:43). */
+typedef struct aloam_cloud {
+    float* pts;   /* n*4 floats                                   */
+    int    n;     /* [out] number of points written               */
+    int    cap;   /* [in]  capacity of pts in points              */
+} aloam_cloud;
+
+/* Outputs of scanRegistration (the five topics, scanRegistration.cpp:413-441). */
+typedef struct aloam_features {
+    aloam_cloud full;        /* /velodyne_cloud_2       (laserCloud, line-ordered)      */
+    aloam_cloud sharp;       /* /laser_cloud_sharp                                      */
+    aloam_cloud less_sharp;  /* /laser_cloud_less_sharp                                 */
+    aloam_cloud flat;        /* /laser_cloud_flat                                       */
+    aloam_cloud less_flat;   /* /laser_cloud_less_flat  (per-line VoxelGrid 0.2 m)      */
+    int*   sharp_idx;        /* optional (may be NULL): index into full of each sharp  */
+    int*   less_sharp_idx;   /* optional: index into full of each less_sharp           */
+    int*   flat_idx;         /* optional: index into full of each flat                 */
+    float* curvature;        /* optional: full.n floats; entries outside [5,n-5) are 0 */
+} aloam_features;
+
+/* Ceres-equivalent solve summary of one outer round. */
+typedef struct aloam_lm_summary {
+    int    iterations;         /* LM iterations executed (<= max_solver_iterations)  */
+    int    successful_steps;
+    int    termination;        /* 0 max-iter, 1 function tol, 2 param tol, 3 gradient tol, 4 no residuals, 5 invalid steps */
+    int    num_residual_blocks;
+    double initial_cost;
+    double final_cost;
+} aloam_lm_summary;
+
+#define ALOAM_MAX_ROUNDS 16
+
+/* laserOdometry result (/laser_odom_to_init, laserOdometry.cpp:588-598). */
+typedef struct aloam_odom_result {
+    double q_w_curr[4];        /* x,y,z,w  (Eigen coeff order)                        */
+    double t_w_curr[3];
+    double q_last_curr[4];     /* para_q (laserOdometry.cpp:131)                       */
+    double t_last_curr[3];     /* para_t                                               */
+    int    optimized;          /* 0 on the initialising frame (laserOdometry.cpp:355)  */
+    int    rounds;
+    int    corner_correspondence[ALOAM_MAX_ROUNDS];
+    int    plane_correspondence[ALOAM_MAX_ROUNDS];
+    aloam_lm_summary lm[ALOAM_MAX_ROUNDS];
+    int    publish_to_mapping;  /* frameCount % skipFrameNum == 0 (laserOdometry.cpp:643) */
+} aloam_odom_result;
+
+/* laserMapping result (/aft_mapped_to_init, laserMapping.cpp:854-865). */
+typedef struct aloam_map_result {
+    double q_w_curr[4];
+    double t_w_curr[3];
+    int    optimized;           /* 0 if the map was too small (laserMapping.cpp:554)   */
+    int    map_corner_num;      /* laserCloudCornerFromMapNum                          */
+    int    map_surf_num;        /* laserCloudSurfFromMapNum                            */
+    int    corner_stack_num;
+    int    surf_stack_num;
+    int    rounds;
+    int    corner_num[ALOAM_MAX_ROUNDS];
+    int    surf_num[ALOAM_MAX_ROUNDS];
+    aloam_lm_summary lm[ALOAM_MAX_ROUNDS];
+    int    map_total_points;    /* all cubes, corner + surf                            */
+} aloam_map_result;
+
+/* One residual block of lidarFactor.hpp, flattened.
+ *  type 0 LidarEdgeFactor      (lidarFactor.hpp:12-55):  cp, a = last_point_a, b = last_point_b
+ *  type 1 LidarPlaneFactor     (lidarFactor.hpp:57-104): cp, a = last_point_j, b = ljm_norm (unit)
+ *  type 2 LidarPlaneNormFactor (lidarFactor.hpp:106-138): cp, a = plane_unit_norm, b[0] = negative_OA_dot_norm
+ *  type 3 LidarDistanceFactor  (lidarFactor.hpp:141-172): cp, a = closed_point
+ * s (interpolation ratio) is 1 on the whole hot path (DISTORTION 0, laserOdometry.cpp:67). */
+typedef struct aloam_factor {
+    int    type;
+    int    pad;
+    double cp[3];
+    double a[3];
+    double b[3];
+} aloam_factor;
+
+/* ---- context ---------------------------------------------------------------------- */
+typedef struct aloam_ctx aloam_ctx;
+
+void        aloam_default_params(aloam_params* p, int scan_line);
+aloam_ctx*  aloam_create(const aloam_params* p, int device);
+void        aloam_destroy(aloam_ctx* ctx);
+const char* aloam_last_error(const aloam_ctx* ctx);
+int         aloam_abi_version(void);
+
+/* ---- stage 1: scanRegistration (scanRegistration.cpp:114-411) ---------------------- */
+/* xyzr: n points of float4 (x,y,z,reflectance) = KITTI .bin / PointCloud2 of PointXYZ(I).
+ * The features stay resident in the context for aloam_odometry(); fetch them with
+ * aloam_get_features(). */
+int aloam_scan_registration(aloam_ctx* ctx, const float* xyzr, int n, int flags);
+int aloam_feature_counts(aloam_ctx* ctx, int counts[5]); /* full, sharp, less_sharp, flat, less_flat */
+int aloam_get_features(aloam_ctx* ctx, aloam_features* out);
+
+/* ---- stage 2: laserOdometry (laserOdometry.cpp:331-641) ---------------------------- */
+/* Consumes the features produced by the last aloam_scan_registration(). */
+int aloam_odometry(aloam_ctx* ctx, aloam_odom_result* out);
+/* Teacher-forcing input: load features from host clouds (float4 x,y,z,intensity),
+ * replacing the ones aloam_scan_registration() left in the context. */
+int aloam_set_features(aloam_ctx* ctx,
+                       const float* sharp, int n_sharp, const float* less_sharp, int n_less_sharp,
+                       const float* flat, int n_flat, const float* less_flat, int n_less_flat);
+/* Overwrite the odometry state (warm start para_q/para_t, pose, last clouds). */
+int aloam_set_odom_state(aloam_ctx* ctx, const double q_last_curr[4], const double t_last_curr[3],
+                         const double q_w_curr[4], const double t_w_curr[3],
+                         const float* corner_last, int n_corner, const float* surf_last, int n_surf);
+
+/* ---- stage 3: laserMapping (laserMapping.cpp:305-848) ------------------------------ */
+/* Consumes laserOdometry's corner_last / surf_last / pose of the same frame. */
+int aloam_mapping(aloam_ctx* ctx, aloam_map_result* out);
+/* Teacher-forcing input for mapping (corner_last, surf_last in the scan frame). */
+int aloam_set_mapping_input(aloam_ctx* ctx, const float* corner_last, int n_corner,
+                            const float* surf_last, int n_surf,
+                            const double q_wodom_curr[4], const double t_wodom_curr[3]);
+/* Map clouds: which = 0 surround (/laser_cloud_surround, laserMapping.cpp:806-821),
+ * 1 whole map (/laser_cloud_map, :823-836). */
+int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out);
+/* /velodyne_cloud_registered (laserMapping.cpp:838-848): last full cloud in the map frame. */
+int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out);
+
+/* ---- whole per-scan pipeline: scanRegistration -> laserOdometry -> laserMapping ----- */
+/* map_out may be NULL; mapping then runs only when do_mapping != 0. */
+int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags,
+                       aloam_odom_result* odom_out, aloam_map_result* map_out);
+
+/* ---- lower-level entry points (tests, tools) -------------------------------------- */
+/* Residuals (3 per factor; plane types fill 1) and the tangent-space Jacobian
+ * (3x6 per factor, row-major; columns = 3 rotation (left-multiplicative quaternion
+ * tangent of EigenQuaternionParameterization) + 3 translation), Huber(0.1)-corrected
+ * when robust != 0, plus the normal equations neq[28] = 21 upper JtJ + 6 Jtr + cost. */
+int aloam_eval_factors(aloam_ctx* ctx, const aloam_factor* f, int n, const double x[7], int robust,
+                       double* residuals, double* jacobians, double neq[28]);
+/* One Ceres-equivalent Solve (LM, Huber 0.1, EigenQuaternionParameterization,
+ * max_solver_iterations) over x = (qx,qy,qz,qw,tx,ty,tz), in place. */
+int aloam_lm_solve(aloam_ctx* ctx, const aloam_factor* f, int n, double x[7], aloam_lm_summary* s);
+/* PCL VoxelGrid (downsample_all_data, x,y,z,intensity centroids) on one cloud. */
+int aloam_voxel_grid(aloam_ctx* ctx, const float* pts, int n, float leaf, aloam_cloud* out);
+/* Exact k-NN (k <= 8) of each query in a point set by float L2 on x,y,z, sorted by distance,
+ * ties by index; idx = -1 / d2 = +inf when fewer than k points exist within radius
+ * (radius <= 0: unbounded). */
+int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int nq, int k,
+              float radius, int* idx, float* d2);
+
+/* Timing of the last pipeline call, measured with HIP events on the context's stream. */
+typedef struct aloam_timing {
+    float scan_registration_ms;
+    float odometry_ms;
+    float mapping_ms;
+    float odom_search_ms;     /* sum over rounds of the odometry correspondence-search kernel */
+    float map_search_ms;      /* sum over rounds of the mapping correspondence-search kernel  */
+    int   odom_search_launches;
+    int   map_search_launches;
+    double map_search_bytes;  /* algorithmic bytes of the mapping searches     */
+    double odom_search_bytes;
+} aloam_timing;
+int aloam_set_profiling(aloam_ctx* ctx, int enable);
+int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALOAM_HIP_H */

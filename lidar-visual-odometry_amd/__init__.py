@@ -1,0 +1,241 @@
+"""MI355X-native A-LOAM per-scan hot path (host mirror of the reference's three nodes).
+
+The compute lives in ``csrc/`` (hand-written HIP for gfx950) behind the C ABI declared in
+``include/aloam_hip.h`` and built as ``csrc/libaloam_hip.so``. This module is a thin ctypes
+host over that ABI with the reference's call surface:
+
+  * ``Context.scan_registration(points)``  ~ ``laserCloudHandler``   (src/scanRegistration.cpp:114)
+  * ``Context.odometry()``                  ~ laserOdometry main loop (src/laserOdometry.cpp:311)
+  * ``Context.mapping()``                   ~ laserMapping ``process`` (src/laserMapping.cpp:231)
+
+There is no CPU fallback: creating a ``Context`` without the HIP library or without a GPU
+raises. The CPU restatement in ``oracle/`` is test infrastructure and is never imported here.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as abi  # noqa: F401
+from . import synth  # noqa: F401
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "libaloam_hip.so")
+_lib = None
+
+
+class ALOAMError(RuntimeError):
+    pass
+
+
+def _declare(L):
+    vp = C.c_void_p
+    F, I, D = C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)
+    L.aloam_abi_version.restype = C.c_int
+    L.aloam_default_params.argtypes = [C.POINTER(abi.Params), C.c_int]
+    L.aloam_create.restype = vp
+    L.aloam_create.argtypes = [C.POINTER(abi.Params), C.c_int]
+    L.aloam_destroy.argtypes = [vp]
+    L.aloam_last_error.restype = C.c_char_p
+    L.aloam_last_error.argtypes = [vp]
+    L.aloam_scan_registration.argtypes = [vp, C.c_void_p, C.c_int, C.c_int]
+    L.aloam_feature_counts.argtypes = [vp, I]
+    L.aloam_get_features.argtypes = [vp, C.POINTER(abi.Features)]
+    L.aloam_odometry.argtypes = [vp, C.POINTER(abi.OdomResult)]
+    L.aloam_set_features.argtypes = [vp] + [F, C.c_int] * 4
+    L.aloam_set_odom_state.argtypes = [vp, D, D, D, D, F, C.c_int, F, C.c_int]
+    L.aloam_mapping.argtypes = [vp, C.POINTER(abi.MapResult)]
+    L.aloam_set_mapping_input.argtypes = [vp, F, C.c_int, F, C.c_int, D, D]
+    L.aloam_get_map_cloud.argtypes = [vp, C.c_int, C.POINTER(abi.Cloud)]
+    L.aloam_get_registered_cloud.argtypes = [vp, C.POINTER(abi.Cloud)]
+    L.aloam_process_scan.argtypes = [vp, C.c_void_p, C.c_int, C.c_int, C.POINTER(abi.OdomResult), C.POINTER(abi.MapResult)]
+    L.aloam_eval_factors.argtypes = [vp, C.c_void_p, C.c_int, D, C.c_int, D, D, D]
+    L.aloam_lm_solve.argtypes = [vp, C.c_void_p, C.c_int, D, C.POINTER(abi.LMSummary)]
+    L.aloam_voxel_grid.argtypes = [vp, F, C.c_int, C.c_float, C.POINTER(abi.Cloud)]
+    L.aloam_knn.argtypes = [vp, F, C.c_int, F, C.c_int, C.c_int, C.c_float, I, F]
+    L.aloam_set_profiling.argtypes = [vp, C.c_int]
+    L.aloam_get_timing.argtypes = [vp, C.POINTER(abi.Timing)]
+    for name in ("aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
+                 "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
+                 "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
+                 "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing"):
+        getattr(L, name).restype = C.c_int
+    return L
+
+
+def lib():
+    """Load csrc/libaloam_hip.so (built in-tree by __graft_entry__.build()). Raises if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ALOAMError(f"HIP extension not built: {LIB_PATH} (run __graft_entry__.build())")
+        _lib = _declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+EXPORTED_SYMBOLS = [
+    "aloam_abi_version", "aloam_default_params", "aloam_create", "aloam_destroy", "aloam_last_error",
+    "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
+    "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
+    "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
+    "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing",
+]
+
+
+class Context:
+    """One aloam_ctx: the state of scanRegistration + laserOdometry + laserMapping on one GPU."""
+
+    def __init__(self, params=None, device=0):
+        self.p = params if params is not None else abi.default_params(64)
+        L = lib()
+        self.h = L.aloam_create(C.byref(self.p), int(device))
+        if not self.h:
+            raise ALOAMError("aloam_create failed (no HIP device?)")
+        self._fail_on(L.aloam_last_error(self.h), creating=True)
+
+    def _fail_on(self, msg, creating=False):
+        if creating and msg:
+            m = msg.decode()
+            if m:
+                self.close()
+                raise ALOAMError(m)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ALOAMError(f"rc={rc}: {lib().aloam_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().aloam_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- stage 1 ----
+    def scan_registration(self, pts, device_ptr=None):
+        if device_ptr is not None:
+            self._check(lib().aloam_scan_registration(self.h, C.c_void_p(device_ptr), int(pts), abi.ALOAM_INPUT_DEVICE))
+            return
+        pts = np.ascontiguousarray(pts, np.float32)
+        self._check(lib().aloam_scan_registration(self.h, pts.ctypes.data_as(C.c_void_p), len(pts), 0))
+
+    def feature_counts(self):
+        cnt = (C.c_int * 5)()
+        self._check(lib().aloam_feature_counts(self.h, cnt))
+        return list(cnt)
+
+    def features(self):
+        n = self.feature_counts()
+        names = ["full", "sharp", "less_sharp", "flat", "less_flat"]
+        f = abi.Features()
+        bufs = {}
+        for name, k in zip(names, n):
+            c, b = abi.make_cloud(k)
+            setattr(f, name, c)
+            bufs[name] = b
+        idx = {k: np.zeros(max(n[i], 1), np.int32) for k, i in (("sharp_idx", 1), ("less_sharp_idx", 2), ("flat_idx", 3))}
+        curv = np.zeros(max(n[0], 1), np.float32)
+        f.sharp_idx, f.less_sharp_idx, f.flat_idx = (abi.iptr(idx[k]) for k in ("sharp_idx", "less_sharp_idx", "flat_idx"))
+        f.curvature = abi.fptr(curv)
+        self._check(lib().aloam_get_features(self.h, C.byref(f)))
+        out = {name: bufs[name][:k].copy() for name, k in zip(names, n)}
+        out["sharp_idx"] = idx["sharp_idx"][:n[1]].copy()
+        out["less_sharp_idx"] = idx["less_sharp_idx"][:n[2]].copy()
+        out["flat_idx"] = idx["flat_idx"][:n[3]].copy()
+        out["curvature"] = curv[:n[0]].copy()
+        return out
+
+    # ---- stage 2 ----
+    def set_features(self, sharp, less_sharp, flat, less_flat):
+        arrs = [np.ascontiguousarray(a, np.float32).reshape(-1, 4) for a in (sharp, less_sharp, flat, less_flat)]
+        args = []
+        for a in arrs:
+            args += [abi.fptr(a), len(a)]
+        self._check(lib().aloam_set_features(self.h, *args))
+
+    def set_odom_state(self, q, t, qw, tw, corner_last, surf_last):
+        q, t, qw, tw = (np.ascontiguousarray(v, np.float64) for v in (q, t, qw, tw))
+        cl = np.ascontiguousarray(corner_last, np.float32).reshape(-1, 4)
+        sl = np.ascontiguousarray(surf_last, np.float32).reshape(-1, 4)
+        self._check(lib().aloam_set_odom_state(self.h, abi.dptr(q), abi.dptr(t), abi.dptr(qw), abi.dptr(tw),
+                                               abi.fptr(cl), len(cl), abi.fptr(sl), len(sl)))
+
+    def odometry(self):
+        r = abi.OdomResult()
+        self._check(lib().aloam_odometry(self.h, C.byref(r)))
+        return abi.odom_to_dict(r)
+
+    # ---- stage 3 ----
+    def set_mapping_input(self, corner, surf, q, t):
+        cl = np.ascontiguousarray(corner, np.float32).reshape(-1, 4)
+        sl = np.ascontiguousarray(surf, np.float32).reshape(-1, 4)
+        q, t = np.ascontiguousarray(q, np.float64), np.ascontiguousarray(t, np.float64)
+        self._check(lib().aloam_set_mapping_input(self.h, abi.fptr(cl), len(cl), abi.fptr(sl), len(sl), abi.dptr(q), abi.dptr(t)))
+
+    def mapping(self):
+        r = abi.MapResult()
+        self._check(lib().aloam_mapping(self.h, C.byref(r)))
+        return abi.map_to_dict(r)
+
+    def map_cloud(self, which, cap=4_000_000):
+        c, b = abi.make_cloud(cap)
+        self._check(lib().aloam_get_map_cloud(self.h, which, C.byref(c)))
+        return b[:min(c.n, cap)].copy()
+
+    def registered_cloud(self, cap=400_000):
+        c, b = abi.make_cloud(cap)
+        self._check(lib().aloam_get_registered_cloud(self.h, C.byref(c)))
+        return b[:min(c.n, cap)].copy()
+
+    # ---- whole pipeline ----
+    def process_scan(self, pts=None, device_ptr=None, n=None):
+        o, m = abi.OdomResult(), abi.MapResult()
+        if device_ptr is not None:
+            self._check(lib().aloam_process_scan(self.h, C.c_void_p(device_ptr), int(n), abi.ALOAM_INPUT_DEVICE, C.byref(o), C.byref(m)))
+        else:
+            pts = np.ascontiguousarray(pts, np.float32)
+            self._check(lib().aloam_process_scan(self.h, pts.ctypes.data_as(C.c_void_p), len(pts), 0, C.byref(o), C.byref(m)))
+        return abi.odom_to_dict(o), abi.map_to_dict(m)
+
+    # ---- low level ----
+    def eval_factors(self, factors, x, robust=True):
+        f = np.ascontiguousarray(factors, abi.FACTOR_DTYPE)
+        n = len(f)
+        x = np.ascontiguousarray(x, np.float64)
+        res, jac, neq = np.zeros(3 * n), np.zeros(3 * n * 6), np.zeros(28)
+        self._check(lib().aloam_eval_factors(self.h, f.ctypes.data_as(C.c_void_p), n, abi.dptr(x), int(robust),
+                                             abi.dptr(res), abi.dptr(jac), abi.dptr(neq)))
+        return res.reshape(n, 3), jac.reshape(n, 3, 6), neq
+
+    def lm_solve(self, factors, x):
+        f = np.ascontiguousarray(factors, abi.FACTOR_DTYPE)
+        x = np.array(x, np.float64)
+        s = abi.LMSummary()
+        self._check(lib().aloam_lm_solve(self.h, f.ctypes.data_as(C.c_void_p), len(f), abi.dptr(x), C.byref(s)))
+        return x, (s.iterations, s.successful_steps, s.termination, s.num_residual_blocks, s.initial_cost, s.final_cost)
+
+    def voxel_grid(self, pts, leaf):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 4)
+        c, b = abi.make_cloud(len(pts))
+        self._check(lib().aloam_voxel_grid(self.h, abi.fptr(pts), len(pts), leaf, C.byref(c)))
+        return b[:c.n].copy()
+
+    def knn(self, pts, queries, k, radius=0.0):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 4)
+        q = np.ascontiguousarray(queries, np.float32).reshape(-1, 4)
+        idx = np.zeros((len(q), k), np.int32)
+        d2 = np.zeros((len(q), k), np.float32)
+        self._check(lib().aloam_knn(self.h, abi.fptr(pts), len(pts), abi.fptr(q), len(q), k, radius, abi.iptr(idx), abi.fptr(d2)))
+        return idx, d2
+
+    def set_profiling(self, on):
+        self._check(lib().aloam_set_profiling(self.h, int(on)))
+
+    def timing(self):
+        t = abi.Timing()
+        self._check(lib().aloam_get_timing(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in abi.Timing._fields_}

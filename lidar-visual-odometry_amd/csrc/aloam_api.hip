@@ -1,0 +1,631 @@
+// aloam_api.hip — the C ABI of include/aloam_hip.h: context, stage orchestration, host I/O.
+//
+// Host <-> device traffic per scan (pipeline path, aloam_process_scan):
+//   H2D  the raw sweep (skipped with ALOAM_INPUT_DEVICE)
+//   D2H  ScanMeta counts after scanRegistration (sizes the odometry launches)
+//   D2H  OdomState + per-round counters after laserOdometry
+//   D2H  MapState + map sizes after laserMapping
+// Everything else (clouds, grids, factors, LM state, the map) stays resident in HBM.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstddef>
+#include <cstring>
+#include <new>
+
+#include "aloam_device.hpp"
+#include "aloam_internal.hpp"
+
+namespace aloam {
+
+void* dalloc(Ctx& C, size_t bytes) {
+    void* p = nullptr;
+    bytes = std::max<size_t>(bytes, 16);
+    HIPCHK(hipMalloc(&p, bytes));
+    HIPCHK(hipMemset(p, 0, bytes));
+    C.bufs.push_back({p, bytes});
+    return p;
+}
+
+void prof_mark(Ctx& C, int idx) {
+    if (C.profiling && C.ev_ready) HIPCHK(hipEventRecord(C.ev[idx], C.stream));
+}
+
+__global__ void k_set2(int* dst, int a, int b) { dst[0] = a; dst[1] = b; }
+void set_counts2(Ctx& C, int* dst, int a, int b) { k_set2<<<1, 1, 0, C.stream>>>(dst, a, b); }
+
+static thread_local std::string g_create_err;
+
+static void init_map_state(MapState& m) {
+    std::memset(&m, 0, sizeof(m));
+    m.parameters[3] = 1.0;
+    m.q_wmap_wodom[3] = 1.0;
+    m.q_wodom[3] = 1.0;
+    m.cenW = 10; m.cenH = 10; m.cenD = 5;   // laserMapping.cpp:74-76
+}
+
+static void allocate(Ctx& C) {
+    const aloam_params& P = C.P;
+    const int N = std::max(P.max_scan_points, 1024);
+    C.cap_in = N;
+    const int nb = (N + 255) / 256;
+    C.d_in = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_cl = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_sid = (int*)dalloc(C, sizeof(int) * N);
+    C.d_ori = (float*)dalloc(C, sizeof(float) * N);
+    C.d_blk = (int*)dalloc(C, sizeof(int) * (nb + 4096));
+    C.d_hist = (int*)dalloc(C, sizeof(int) * (size_t)MAXL * nb);
+    C.d_cloud = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_curv = (float*)dalloc(C, sizeof(float) * N);
+    C.d_scratch_xyz = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_scratch_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)N);
+    C.d_scratch_i = (int*)dalloc(C, sizeof(int) * 3 * (size_t)N);
+    C.d_line_sharp = (int*)dalloc(C, sizeof(int) * MAXL * LINE_SHARP_CAP);
+    C.d_line_lsharp = (int*)dalloc(C, sizeof(int) * MAXL * LINE_LSHARP_CAP);
+    C.d_line_flat = (int*)dalloc(C, sizeof(int) * MAXL * LINE_FLAT_CAP);
+    C.d_line_cnt = (int*)dalloc(C, sizeof(int) * MAXL * 4);
+    C.d_line_lf = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_meta = (ScanMeta*)dalloc(C, sizeof(ScanMeta));
+    const int capS = MAXL * LINE_SHARP_CAP, capLS = MAXL * LINE_LSHARP_CAP, capF = MAXL * LINE_FLAT_CAP;
+    C.d_sharp = (float4*)dalloc(C, sizeof(float4) * capS);
+    C.d_flat = (float4*)dalloc(C, sizeof(float4) * capF);
+    // less-sharp / less-flat ping-pong with the odometry's "last" clouds
+    C.d_lsharp = (float4*)dalloc(C, sizeof(float4) * capLS);
+    C.d_corner_last = (float4*)dalloc(C, sizeof(float4) * capLS);
+    C.d_lflat = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_surf_last = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_sharp_idx = (int*)dalloc(C, sizeof(int) * capS);
+    C.d_lsharp_idx = (int*)dalloc(C, sizeof(int) * capLS);
+    C.d_flat_idx = (int*)dalloc(C, sizeof(int) * capF);
+    // odometry
+    C.d_odom = (OdomState*)dalloc(C, sizeof(OdomState));
+    std::memset(&C.h_odom, 0, sizeof(C.h_odom));
+    C.h_odom.para[3] = 1.0;
+    C.h_odom.q_w[3] = 1.0;
+    HIPCHK(hipMemcpy(C.d_odom, &C.h_odom, sizeof(OdomState), hipMemcpyHostToDevice));
+    grid_alloc(C, C.g_corner_last, capLS, 2.0f * 5.0f * 1.025f);
+    grid_alloc(C, C.g_surf_last, N, 2.0f * 5.0f * 1.025f);
+    C.cap_factors = capLS + N;
+    C.d_factors = (aloam_factor*)dalloc(C, sizeof(aloam_factor) * C.cap_factors);
+    C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);
+    C.d_lm = (LMState*)dalloc(C, sizeof(LMState));
+    C.d_partials = (double*)dalloc(C, sizeof(double) * 512 * 32);
+    C.d_lm_sum = (aloam_lm_summary*)dalloc(C, sizeof(aloam_lm_summary) * 2 * ALOAM_MAX_ROUNDS);
+    C.d_round_cnt = (int*)dalloc(C, sizeof(int) * 4 * ALOAM_MAX_ROUNDS);
+    C.d_last_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_cand = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2);
+    // mapping
+    const int M = std::max(P.max_map_points, 1024);
+    C.cap_map = M;
+    C.d_map = (MapState*)dalloc(C, sizeof(MapState));
+    init_map_state(C.h_map);
+    HIPCHK(hipMemcpy(C.d_map, &C.h_map, sizeof(MapState), hipMemcpyHostToDevice));
+    C.d_mc = (float4*)dalloc(C, sizeof(float4) * M);
+    C.d_ms = (float4*)dalloc(C, sizeof(float4) * M);
+    C.d_mc2 = (float4*)dalloc(C, sizeof(float4) * M);
+    C.d_ms2 = (float4*)dalloc(C, sizeof(float4) * M);
+    C.d_mc_cube = (int*)dalloc(C, sizeof(int) * M);
+    C.d_ms_cube = (int*)dalloc(C, sizeof(int) * M);
+    C.d_mc2_cube = (int*)dalloc(C, sizeof(int) * M);
+    C.d_ms2_cube = (int*)dalloc(C, sizeof(int) * M);
+    C.d_map_tmp = (float4*)dalloc(C, sizeof(float4) * M);
+    C.d_seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 4 * (size_t)M);
+    C.d_map_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_cube_cnt = (int*)dalloc(C, sizeof(int) * 2 * 7 * (CUBE_N + 1));
+    C.d_cube_valid = (unsigned char*)dalloc(C, CUBE_N);
+    grid_alloc(C, C.g_map_corner, M, 2.0f * 1.0f * 1.025f);
+    grid_alloc(C, C.g_map_surf, M, 2.0f * 1.0f * 1.025f);
+    C.d_map_corner_in = (float4*)dalloc(C, sizeof(float4) * capLS);
+    C.d_map_surf_in = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_map_full_in = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_map_in_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_cstack = (float4*)dalloc(C, sizeof(float4) * capLS);
+    C.d_sstack = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_stack_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_registered = (float4*)dalloc(C, sizeof(float4) * N);
+    // voxel / sort scratch
+    C.cap_voxel = std::max(N, capLS) + 64;
+    C.d_vkeys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)C.cap_voxel);
+    C.d_vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
+    C.d_vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    C.d_vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
+    C.sort_tmp_bytes = voxel_sort_tmp_bytes(C.cap_voxel) + 1024;
+    C.d_sort_tmp = dalloc(C, C.sort_tmp_bytes);
+    C.d_ins_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_voxel);
+    C.d_ins_val = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    C.d_ins_val2 = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
+    C.ev_ready = true;
+}
+
+static void sync(Ctx& C) { HIPCHK(hipStreamSynchronize(C.stream)); }
+
+static float ev_ms(Ctx& C, int a, int b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, C.ev[a], C.ev[b]) != hipSuccess) return 0.f;
+    return ms;
+}
+
+static void read_meta(Ctx& C) {
+    HIPCHK(hipMemcpyAsync(&C.h_meta, C.d_meta, sizeof(ScanMeta), hipMemcpyDeviceToHost, C.stream));
+    sync(C);
+    C.n_full = C.h_meta.counts[0];
+    C.n_sharp = C.h_meta.counts[1];
+    C.n_lsharp = C.h_meta.counts[2];
+    C.n_flat = C.h_meta.counts[3];
+    C.n_lflat = C.h_meta.counts[4];
+}
+
+static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
+    if (n < 0 || (n > 0 && !xyzr)) throw ApiError{ALOAM_E_ARG, "bad input"};
+    if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "scan larger than max_scan_points"};
+    const int L = C.P.scan_line;
+    if (!(L == 16 || L == 32 || L == 64) && !C.P.generic_scan_lines)
+        throw ApiError{ALOAM_E_SCAN_LINES, "wrong scan number"};
+    if (L > MAXL || L <= 0) throw ApiError{ALOAM_E_SCAN_LINES, "scan_line above the device maximum (128)"};
+    const float4* in = (const float4*)xyzr;
+    if (!(flags & ALOAM_INPUT_DEVICE) && n > 0) {
+        HIPCHK(hipMemcpyAsync(C.d_in, xyzr, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
+        in = C.d_in;
+    }
+    prof_mark(C, 0);
+    scan_registration_launch(C, in, n);
+    prof_mark(C, 1);
+    read_meta(C);
+    if (C.profiling) C.timing.scan_registration_ms = ev_ms(C, 0, 1);
+    C.have_features = true;
+    C.features_from_host = false;
+}
+
+static void do_odometry(Ctx& C, aloam_odom_result* R) {
+    if (!C.have_features) throw ApiError{ALOAM_E_STATE, "odometry before any features"};
+    aloam_odom_result r{};
+    hipStream_t st = C.stream;
+    prof_mark(C, 2);
+    const int rounds = std::min(C.P.odom_rounds, ALOAM_MAX_ROUNDS);
+    if (!C.odom_inited) {
+        C.odom_inited = true;       // laserOdometry.cpp:355-358
+    } else {
+        r.optimized = 1;
+        r.rounds = rounds;
+        HIPCHK(hipMemsetAsync(C.d_round_cnt, 0, sizeof(int) * 2 * ALOAM_MAX_ROUNDS, st));
+        const int nslots = C.n_sharp + C.n_flat;
+        if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
+        for (int it = 0; it < rounds; it++) {
+            prof_mark(C, 6 + 2 * it);
+            odom_round_search(C, it);
+            prof_mark(C, 7 + 2 * it);
+            lm_run(C, C.d_factors, nslots, C.d_odom->para, it, nullptr);
+        }
+        odom_compose(C);
+    }
+    // the current less-sharp / less-flat become the last clouds (:627-641)
+    std::swap(C.d_lsharp, C.d_corner_last);
+    std::swap(C.d_lflat, C.d_surf_last);
+    C.n_corner_last = C.n_lsharp;
+    C.n_surf_last = C.n_lflat;
+    set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);
+    grid_build(C, C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
+    grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
+    const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
+    r.publish_to_mapping = (C.odom_frame_count % skip == 0);
+    if (r.publish_to_mapping) C.odom_frame_count = 0;
+    C.odom_frame_count++;
+    if (r.publish_to_mapping) {   // /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3, pose
+        if (C.n_corner_last) HIPCHK(hipMemcpyAsync(C.d_map_corner_in, C.d_corner_last, sizeof(float4) * C.n_corner_last, hipMemcpyDeviceToDevice, st));
+        if (C.n_surf_last) HIPCHK(hipMemcpyAsync(C.d_map_surf_in, C.d_surf_last, sizeof(float4) * C.n_surf_last, hipMemcpyDeviceToDevice, st));
+        if (C.n_full && !C.features_from_host) HIPCHK(hipMemcpyAsync(C.d_map_full_in, C.d_cloud, sizeof(float4) * C.n_full, hipMemcpyDeviceToDevice, st));
+        C.n_map_corner_in = C.n_corner_last;
+        C.n_map_surf_in = C.n_surf_last;
+        C.n_map_full_in = C.features_from_host ? 0 : C.n_full;
+        set_counts2(C, C.d_map_in_n, C.n_map_corner_in, C.n_map_surf_in);
+        C.have_map_input = true;
+    }
+    prof_mark(C, 3);
+    // results
+    int cnt[2 * ALOAM_MAX_ROUNDS];
+    HIPCHK(hipMemcpyAsync(&C.h_odom, C.d_odom, sizeof(OdomState), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(cnt, C.d_round_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(r.lm, C.d_lm_sum, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS, hipMemcpyDeviceToHost, st));
+    sync(C);
+    if (!r.optimized) std::memset(r.lm, 0, sizeof(r.lm));
+    for (int i = 0; i < r.rounds; i++) { r.corner_correspondence[i] = cnt[2 * i]; r.plane_correspondence[i] = cnt[2 * i + 1]; }
+    for (int k = 0; k < 4; k++) { r.q_w_curr[k] = C.h_odom.q_w[k]; r.q_last_curr[k] = C.h_odom.para[k]; }
+    for (int k = 0; k < 3; k++) { r.t_w_curr[k] = C.h_odom.t_w[k]; r.t_last_curr[k] = C.h_odom.para[4 + k]; }
+    if (r.publish_to_mapping) {
+        for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = r.q_w_curr[k];
+        for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = r.t_w_curr[k];
+        // the odometry pose is handed to the mapping state on device
+        HIPCHK(hipMemcpyAsync((char*)C.d_map + offsetof(MapState, q_wodom), C.h_map.q_wodom, sizeof(double) * 7,
+                              hipMemcpyHostToDevice, st));
+    }
+    if (C.profiling) {
+        C.timing.odometry_ms = ev_ms(C, 2, 3);
+        float s = 0;
+        for (int i = 0; i < r.rounds; i++) s += ev_ms(C, 6 + 2 * i, 7 + 2 * i);
+        C.timing.odom_search_ms = s;
+        C.timing.odom_search_launches = r.rounds;
+    }
+    if (R) *R = r;
+}
+
+static void do_mapping(Ctx& C, aloam_map_result* R) {
+    if (!C.have_map_input) throw ApiError{ALOAM_E_STATE, "mapping before odometry output"};
+    aloam_map_result r{};
+    hipStream_t st = C.stream;
+    if (C.profiling) HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long) * 2, st));
+    prof_mark(C, 4);
+    map_frame_launch(C, &r);
+    prof_mark(C, 5);
+    int cnt[2 * ALOAM_MAX_ROUNDS];
+    int mapn[2];
+    unsigned long long cand[2] = {0, 0};
+    int stackn[2];
+    HIPCHK(hipMemcpyAsync(&C.h_map, C.d_map, sizeof(MapState), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(cnt, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(r.lm, C.d_lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(mapn, C.d_map_n, sizeof(mapn), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(stackn, C.d_stack_n, sizeof(stackn), hipMemcpyDeviceToHost, st));
+    if (C.profiling) HIPCHK(hipMemcpyAsync(cand, C.d_cand, sizeof(cand), hipMemcpyDeviceToHost, st));
+    sync(C);
+    C.n_mc = mapn[0];
+    C.n_ms = mapn[1];
+    C.n_registered = C.n_map_full_in;
+    r.optimized = C.h_map.optimize;
+    r.rounds = r.optimized ? std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS) : 0;
+    if (!r.optimized) std::memset(r.lm, 0, sizeof(r.lm));
+    for (int i = 0; i < r.rounds; i++) { r.corner_num[i] = cnt[2 * i]; r.surf_num[i] = cnt[2 * i + 1]; }
+    r.map_corner_num = C.h_map.n_corner_map;
+    r.map_surf_num = C.h_map.n_surf_map;
+    r.corner_stack_num = stackn[0];
+    r.surf_stack_num = stackn[1];
+    r.map_total_points = C.n_mc + C.n_ms;
+    for (int k = 0; k < 7; k++) (k < 4 ? r.q_w_curr[k] : r.t_w_curr[k - 4]) = C.h_map.parameters[k];
+    C.have_map_input = false;
+    C.map_frame_count++;
+    if (C.profiling) {
+        C.timing.mapping_ms = ev_ms(C, 4, 5);
+        float s = 0;
+        for (int i = 0; i < r.rounds; i++) s += ev_ms(C, 6 + 2 * (ALOAM_MAX_ROUNDS + i), 7 + 2 * (ALOAM_MAX_ROUNDS + i));
+        C.timing.map_search_ms = s;
+        C.timing.map_search_launches = r.rounds;
+        // B = sum_q [16 + 16 |C(q)|] + 8 k Q  (k = 5 neighbour slots of 4 B + d2)
+        const double Q = (double)(stackn[0] + stackn[1]) * r.rounds;
+        C.timing.map_search_bytes = 16.0 * Q + 16.0 * (double)cand[0] + 8.0 * 5.0 * Q;
+    }
+    if (R) *R = r;
+}
+
+}  // namespace aloam
+
+using namespace aloam;
+
+#define API_BEGIN(ctx)                                    \
+    if (!(ctx)) return ALOAM_E_ARG;                       \
+    Ctx& C = *(Ctx*)(ctx);                                \
+    try {                                                 \
+        HIPCHK(hipSetDevice(C.device));
+#define API_END                                           \
+        return ALOAM_OK;                                  \
+    } catch (const ApiError& e) {                         \
+        C.err = e.msg;                                    \
+        return e.code;                                    \
+    } catch (const HipError& e) {                         \
+        C.err = e.msg;                                    \
+        return ALOAM_E_HIP;                               \
+    } catch (const std::bad_alloc&) {                     \
+        C.err = "host allocation failed";                 \
+        return ALOAM_E_CAPACITY;                          \
+    }
+
+struct aloam_ctx {};   // opaque handle: the pointer is an aloam::Ctx*
+
+extern "C" {
+
+int aloam_abi_version(void) { return ALOAM_ABI_VERSION; }
+
+void aloam_default_params(aloam_params* p, int scan_line) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->scan_line = scan_line;
+    p->minimum_range = scan_line == 64 ? 5.0f : 0.3f;
+    p->mapping_skip_frame = 1;
+    p->mapping_line_resolution = scan_line == 64 ? 0.4f : 0.2f;
+    p->mapping_plane_resolution = scan_line == 64 ? 0.8f : 0.4f;
+    p->input_is_dense = 1;
+    p->generic_scan_lines = (scan_line == 16 || scan_line == 32 || scan_line == 64) ? 0 : 1;
+    p->generic_min_elev_deg = -25.f;
+    p->generic_max_elev_deg = 15.f;
+    p->odom_rounds = 10;
+    p->map_rounds = 10;
+    p->max_solver_iterations = 4;
+    p->max_scan_points = 400000;
+    p->max_map_points = 4000000;
+}
+
+aloam_ctx* aloam_create(const aloam_params* p, int device) {
+    if (!p) { g_create_err = "null params"; return nullptr; }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) { g_create_err = "no HIP device"; return nullptr; }
+    if (device < 0 || device >= n) { g_create_err = "bad device index"; return nullptr; }
+    Ctx* C = new (std::nothrow) Ctx();
+    if (!C) { g_create_err = "host allocation failed"; return nullptr; }
+    C->P = *p;
+    C->device = device;
+    try {
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
+        allocate(*C);
+    } catch (const HipError& e) {
+        g_create_err = e.msg;
+        for (auto& b : C->bufs) (void)hipFree(b.p);
+        delete C;
+        return nullptr;
+    }
+    g_create_err.clear();
+    return (aloam_ctx*)C;
+}
+
+void aloam_destroy(aloam_ctx* ctx) {
+    if (!ctx) return;
+    Ctx* C = (Ctx*)ctx;
+    (void)hipSetDevice(C->device);
+    if (C->stream) (void)hipStreamSynchronize(C->stream);
+    if (C->ev_ready) for (int i = 0; i < Ctx::NEV; i++) (void)hipEventDestroy(C->ev[i]);
+    for (auto& b : C->bufs) (void)hipFree(b.p);
+    if (C->stream) (void)hipStreamDestroy(C->stream);
+    delete C;
+}
+
+const char* aloam_last_error(const aloam_ctx* ctx) {
+    if (!ctx) return g_create_err.c_str();
+    return ((const Ctx*)ctx)->err.c_str();
+}
+
+int aloam_scan_registration(aloam_ctx* ctx, const float* xyzr, int n, int flags) {
+    API_BEGIN(ctx)
+    do_scan_registration(C, xyzr, n, flags);
+    API_END
+}
+
+int aloam_feature_counts(aloam_ctx* ctx, int counts[5]) {
+    API_BEGIN(ctx)
+    if (!counts) throw ApiError{ALOAM_E_ARG, "null counts"};
+    counts[0] = C.n_full; counts[1] = C.n_sharp; counts[2] = C.n_lsharp; counts[3] = C.n_flat; counts[4] = C.n_lflat;
+    API_END
+}
+
+static void d2h_cloud(Ctx& C, const float4* src, int n, aloam_cloud* c) {
+    if (!c) return;
+    c->n = n;
+    if (c->pts && n > 0) HIPCHK(hipMemcpyAsync(c->pts, src, sizeof(float4) * std::min(n, c->cap), hipMemcpyDeviceToHost, C.stream));
+}
+
+int aloam_get_features(aloam_ctx* ctx, aloam_features* o) {
+    API_BEGIN(ctx)
+    if (!o) throw ApiError{ALOAM_E_ARG, "null features"};
+    if (!C.have_features) throw ApiError{ALOAM_E_STATE, "no features yet"};
+    const bool swapped = false;
+    (void)swapped;
+    d2h_cloud(C, C.d_cloud, C.features_from_host ? 0 : C.n_full, &o->full);
+    d2h_cloud(C, C.d_sharp, C.n_sharp, &o->sharp);
+    d2h_cloud(C, C.d_lsharp, C.n_lsharp, &o->less_sharp);
+    d2h_cloud(C, C.d_flat, C.n_flat, &o->flat);
+    d2h_cloud(C, C.d_lflat, C.n_lflat, &o->less_flat);
+    if (o->sharp_idx && C.n_sharp) HIPCHK(hipMemcpyAsync(o->sharp_idx, C.d_sharp_idx, sizeof(int) * C.n_sharp, hipMemcpyDeviceToHost, C.stream));
+    if (o->less_sharp_idx && C.n_lsharp) HIPCHK(hipMemcpyAsync(o->less_sharp_idx, C.d_lsharp_idx, sizeof(int) * C.n_lsharp, hipMemcpyDeviceToHost, C.stream));
+    if (o->flat_idx && C.n_flat) HIPCHK(hipMemcpyAsync(o->flat_idx, C.d_flat_idx, sizeof(int) * C.n_flat, hipMemcpyDeviceToHost, C.stream));
+    if (o->curvature && C.n_full) HIPCHK(hipMemcpyAsync(o->curvature, C.d_curv, sizeof(float) * C.n_full, hipMemcpyDeviceToHost, C.stream));
+    sync(C);
+    API_END
+}
+
+int aloam_set_features(aloam_ctx* ctx, const float* sharp, int ns, const float* less_sharp, int nls,
+                       const float* flat, int nf, const float* less_flat, int nlf) {
+    API_BEGIN(ctx)
+    if (ns < 0 || nls < 0 || nf < 0 || nlf < 0) throw ApiError{ALOAM_E_ARG, "negative size"};
+    if (ns > MAXL * LINE_SHARP_CAP || nls > MAXL * LINE_LSHARP_CAP || nf > MAXL * LINE_FLAT_CAP || nlf > C.cap_in)
+        throw ApiError{ALOAM_E_CAPACITY, "feature cloud too large"};
+    auto up = [&](float4* d, const float* h, int n) {
+        if (n > 0) HIPCHK(hipMemcpyAsync(d, h, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
+    };
+    up(C.d_sharp, sharp, ns); up(C.d_lsharp, less_sharp, nls); up(C.d_flat, flat, nf); up(C.d_lflat, less_flat, nlf);
+    sync(C);
+    C.n_sharp = ns; C.n_lsharp = nls; C.n_flat = nf; C.n_lflat = nlf; C.n_full = 0;
+    C.have_features = true;
+    C.features_from_host = true;
+    API_END
+}
+
+int aloam_set_odom_state(aloam_ctx* ctx, const double q[4], const double t[3], const double qw[4], const double tw[3],
+                         const float* corner_last, int nc, const float* surf_last, int ns) {
+    API_BEGIN(ctx)
+    if (!q || !t || !qw || !tw || nc < 0 || ns < 0) throw ApiError{ALOAM_E_ARG, "bad odom state"};
+    if (nc > MAXL * LINE_LSHARP_CAP || ns > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "last cloud too large"};
+    for (int k = 0; k < 4; k++) { C.h_odom.para[k] = q[k]; C.h_odom.q_w[k] = qw[k]; }
+    for (int k = 0; k < 3; k++) { C.h_odom.para[4 + k] = t[k]; C.h_odom.t_w[k] = tw[k]; }
+    HIPCHK(hipMemcpyAsync(C.d_odom, &C.h_odom, sizeof(OdomState), hipMemcpyHostToDevice, C.stream));
+    if (nc > 0) HIPCHK(hipMemcpyAsync(C.d_corner_last, corner_last, sizeof(float4) * nc, hipMemcpyHostToDevice, C.stream));
+    if (ns > 0) HIPCHK(hipMemcpyAsync(C.d_surf_last, surf_last, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
+    C.n_corner_last = nc; C.n_surf_last = ns;
+    set_counts2(C, C.d_last_n, nc, ns);
+    grid_build(C, C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(nc, 1), nullptr, nullptr);
+    grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(ns, 1), nullptr, nullptr);
+    sync(C);
+    C.odom_inited = true;
+    API_END
+}
+
+int aloam_odometry(aloam_ctx* ctx, aloam_odom_result* out) {
+    API_BEGIN(ctx)
+    do_odometry(C, out);
+    API_END
+}
+
+int aloam_set_mapping_input(aloam_ctx* ctx, const float* corner, int nc, const float* surf, int ns, const double q[4], const double t[3]) {
+    API_BEGIN(ctx)
+    if (nc < 0 || ns < 0 || !q || !t) throw ApiError{ALOAM_E_ARG, "bad mapping input"};
+    if (nc > MAXL * LINE_LSHARP_CAP || ns > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
+    if (nc > 0) HIPCHK(hipMemcpyAsync(C.d_map_corner_in, corner, sizeof(float4) * nc, hipMemcpyHostToDevice, C.stream));
+    if (ns > 0) HIPCHK(hipMemcpyAsync(C.d_map_surf_in, surf, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
+    C.n_map_corner_in = nc; C.n_map_surf_in = ns; C.n_map_full_in = 0;
+    set_counts2(C, C.d_map_in_n, nc, ns);
+    for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = q[k];
+    for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = t[k];
+    HIPCHK(hipMemcpyAsync((char*)C.d_map + offsetof(MapState, q_wodom), C.h_map.q_wodom, sizeof(double) * 7, hipMemcpyHostToDevice, C.stream));
+    sync(C);
+    C.have_map_input = true;
+    API_END
+}
+
+int aloam_mapping(aloam_ctx* ctx, aloam_map_result* out) {
+    API_BEGIN(ctx)
+    do_mapping(C, out);
+    API_END
+}
+
+int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out) {
+    API_BEGIN(ctx)
+    if (!out) throw ApiError{ALOAM_E_ARG, "null cloud"};
+    // map arrays are sorted by cube id; the surround cloud is the surrounding cubes' points
+    std::vector<int> cube_c(C.n_mc), cube_s(C.n_ms);
+    std::vector<float4> pc(C.n_mc), ps(C.n_ms);
+    if (C.n_mc) {
+        HIPCHK(hipMemcpyAsync(pc.data(), C.d_mc, sizeof(float4) * C.n_mc, hipMemcpyDeviceToHost, C.stream));
+        HIPCHK(hipMemcpyAsync(cube_c.data(), C.d_mc_cube, sizeof(int) * C.n_mc, hipMemcpyDeviceToHost, C.stream));
+    }
+    if (C.n_ms) {
+        HIPCHK(hipMemcpyAsync(ps.data(), C.d_ms, sizeof(float4) * C.n_ms, hipMemcpyDeviceToHost, C.stream));
+        HIPCHK(hipMemcpyAsync(cube_s.data(), C.d_ms_cube, sizeof(int) * C.n_ms, hipMemcpyDeviceToHost, C.stream));
+    }
+    sync(C);
+    // reference order: for each cube (surround list order or all cubes in index order): corner then surf
+    std::vector<int> cubes;
+    if (which == 0) for (int i = 0; i < C.h_map.valid_num; i++) cubes.push_back(C.h_map.valid_ind[i]);
+    else for (int i = 0; i < CUBE_N; i++) cubes.push_back(i);
+    std::vector<int> oc(CUBE_N + 1, 0), os(CUBE_N + 1, 0);
+    for (int c : cube_c) oc[c + 1]++;
+    for (int c : cube_s) os[c + 1]++;
+    for (int i = 0; i < CUBE_N; i++) { oc[i + 1] += oc[i]; os[i + 1] += os[i]; }
+    int n = 0;
+    float4* dst = (float4*)out->pts;
+    for (int c : cubes) {
+        for (int i = oc[c]; i < oc[c + 1]; i++) { if (dst && n < out->cap) dst[n] = pc[i]; n++; }
+        for (int i = os[c]; i < os[c + 1]; i++) { if (dst && n < out->cap) dst[n] = ps[i]; n++; }
+    }
+    out->n = n;
+    API_END
+}
+
+int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out) {
+    API_BEGIN(ctx)
+    d2h_cloud(C, C.d_registered, C.n_registered, out);
+    sync(C);
+    API_END
+}
+
+int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags, aloam_odom_result* o, aloam_map_result* m) {
+    API_BEGIN(ctx)
+    do_scan_registration(C, xyzr, n, flags);
+    aloam_odom_result od{};
+    do_odometry(C, &od);
+    if (o) *o = od;
+    if (od.publish_to_mapping) do_mapping(C, m);
+    else if (m) std::memset(m, 0, sizeof(*m));
+    API_END
+}
+
+int aloam_eval_factors(aloam_ctx* ctx, const aloam_factor* f, int n, const double x[7], int robust,
+                       double* residuals, double* jacobians, double neq[28]) {
+    API_BEGIN(ctx)
+    if (n < 0 || (n > 0 && !f) || !x) throw ApiError{ALOAM_E_ARG, "bad factors"};
+    if (n > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "too many factors"};
+    double* d_x = (double*)C.d_partials;       // scratch: x[7] + neq[28] + residuals + jac via voxel buffers
+    double* d_neq = d_x + 8;
+    double* d_res = (double*)C.d_vkeys;        // 3n doubles
+    double* d_jac = (double*)C.d_seg_keys;     // 18n doubles
+    if ((size_t)3 * n > 2 * (size_t)C.cap_voxel) throw ApiError{ALOAM_E_CAPACITY, "too many factors"};
+    if (n) HIPCHK(hipMemcpyAsync(C.d_factors, f, sizeof(aloam_factor) * n, hipMemcpyHostToDevice, C.stream));
+    HIPCHK(hipMemcpyAsync(d_x, x, sizeof(double) * 7, hipMemcpyHostToDevice, C.stream));
+    lm_eval_only(C, C.d_factors, n, d_x, robust, d_res, d_jac, d_neq);
+    if (residuals && n) HIPCHK(hipMemcpyAsync(residuals, d_res, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, C.stream));
+    if (jacobians && n) HIPCHK(hipMemcpyAsync(jacobians, d_jac, sizeof(double) * 18 * n, hipMemcpyDeviceToHost, C.stream));
+    if (neq) HIPCHK(hipMemcpyAsync(neq, d_neq, sizeof(double) * 28, hipMemcpyDeviceToHost, C.stream));
+    sync(C);
+    API_END
+}
+
+int aloam_lm_solve(aloam_ctx* ctx, const aloam_factor* f, int n, double x[7], aloam_lm_summary* s) {
+    API_BEGIN(ctx)
+    if (n < 0 || (n > 0 && !f) || !x) throw ApiError{ALOAM_E_ARG, "bad factors"};
+    if (n > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "too many factors"};
+    double* d_x = (double*)C.d_nbr;   // 7 doubles of scratch
+    if (n) HIPCHK(hipMemcpyAsync(C.d_factors, f, sizeof(aloam_factor) * n, hipMemcpyHostToDevice, C.stream));
+    HIPCHK(hipMemcpyAsync(d_x, x, sizeof(double) * 7, hipMemcpyHostToDevice, C.stream));
+    lm_run(C, C.d_factors, n, d_x, 2 * ALOAM_MAX_ROUNDS - 1, nullptr);
+    aloam_lm_summary sum{};
+    HIPCHK(hipMemcpyAsync(x, d_x, sizeof(double) * 7, hipMemcpyDeviceToHost, C.stream));
+    HIPCHK(hipMemcpyAsync(&sum, C.d_lm_sum + 2 * ALOAM_MAX_ROUNDS - 1, sizeof(sum), hipMemcpyDeviceToHost, C.stream));
+    sync(C);
+    if (s) *s = sum;
+    API_END
+}
+
+int aloam_voxel_grid(aloam_ctx* ctx, const float* pts, int n, float leaf, aloam_cloud* out) {
+    API_BEGIN(ctx)
+    if (n < 0 || (n > 0 && !pts) || !out || !(leaf > 0)) throw ApiError{ALOAM_E_ARG, "bad voxel input"};
+    if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "too many points"};
+    if (n) HIPCHK(hipMemcpyAsync(C.d_in, pts, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
+    set_counts2(C, C.d_map_in_n, n, 0);
+    voxel_grid_sorted(C, C.d_in, C.d_map_in_n, n, leaf, C.d_cl, C.d_stack_n);
+    int nout = 0;
+    HIPCHK(hipMemcpyAsync(&nout, C.d_stack_n, sizeof(int), hipMemcpyDeviceToHost, C.stream));
+    sync(C);
+    d2h_cloud(C, C.d_cl, nout, out);
+    sync(C);
+    C.have_map_input = false;
+    API_END
+}
+
+int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int nq, int k, float radius, int* idx, float* d2) {
+    API_BEGIN(ctx)
+    if (n < 0 || nq < 0 || k < 1 || k > 8 || !(radius > 0) || !idx || !d2) throw ApiError{ALOAM_E_ARG, "bad knn args (radius must be > 0, 1 <= k <= 8)"};
+    if (n > C.cap_in || nq > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "too many points"};
+    if (n) HIPCHK(hipMemcpyAsync(C.d_in, pts, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
+    if (nq) HIPCHK(hipMemcpyAsync(C.d_cl, queries, sizeof(float4) * nq, hipMemcpyHostToDevice, C.stream));
+    set_counts2(C, C.d_map_in_n, n, 0);
+    Grid g = C.g_surf_last;      // borrow the odometry surf grid's storage with the requested radius
+    g.min_cell = 2.0f * radius * 1.025f;
+    grid_build(C, g, C.d_in, C.d_map_in_n, std::max(n, 1), nullptr, nullptr);
+    int* d_idx = (int*)C.d_scratch_i;
+    float* d_d2 = (float*)(C.d_scratch_i + (size_t)nq * k);
+    if ((size_t)nq * k * 2 > 3 * (size_t)C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "too many queries"};
+    knn_launch(C, g, C.d_cl, nq, k, radius, d_idx, d_d2);
+    if (nq) {
+        HIPCHK(hipMemcpyAsync(idx, d_idx, sizeof(int) * nq * k, hipMemcpyDeviceToHost, C.stream));
+        HIPCHK(hipMemcpyAsync(d2, d_d2, sizeof(float) * nq * k, hipMemcpyDeviceToHost, C.stream));
+    }
+    sync(C);
+    // the odometry surf grid was overwritten: rebuild it for the current last cloud
+    grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
+    sync(C);
+    C.have_map_input = false;
+    API_END
+}
+
+int aloam_set_profiling(aloam_ctx* ctx, int enable) {
+    API_BEGIN(ctx)
+    C.profiling = enable != 0;
+    std::memset(&C.timing, 0, sizeof(C.timing));
+    API_END
+}
+
+int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t) {
+    API_BEGIN(ctx)
+    if (!t) throw ApiError{ALOAM_E_ARG, "null timing"};
+    *t = C.timing;
+    API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,205 @@
+// aloam_internal.hpp — context layout and kernel-launch entry points shared by the .hip files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/aloam_hip.h"
+
+namespace aloam {
+
+constexpr int MAXL = 128;            // scan lines supported on device
+constexpr int LINE_SHARP_CAP = 12;   // 2 per segment x 6   (scanRegistration.cpp:301)
+constexpr int LINE_LSHARP_CAP = 120; // 20 per segment x 6  (:307)
+constexpr int LINE_FLAT_CAP = 24;    // 4 per segment x 6   (:359)
+constexpr int LINE_LDS_CAP = 4096;   // points per line kept in LDS (larger lines use global scratch)
+constexpr int CUBE_W = 21, CUBE_H = 21, CUBE_D = 11, CUBE_N = 21 * 21 * 11;  // laserMapping.cpp:74-82
+constexpr int GRID_MAX_CELLS = 1 << 22;
+
+// ---- device-resident bookkeeping of scanRegistration ----
+struct ScanMeta {
+    int n_in, n_cl, jstar, cloud_size;
+    int counts[5];                 // full, sharp, less_sharp, flat, less_flat
+    int line_off[MAXL + 1];
+};
+
+// ---- dense uniform grid over a point set (kd-tree-free radius search) ----
+struct GridDesc {
+    unsigned bb[6];                // ordered-encoded bbox: min xyz, max xyz
+    float ox, oy, oz, cell, inv_cell;
+    int dx, dy, dz, ncells, n;
+};
+struct Grid {
+    GridDesc* desc = nullptr;      // device
+    int* cell_count = nullptr;     // GRID_MAX_CELLS (all zero between builds)
+    int* cell_start = nullptr;     // GRID_MAX_CELLS + 1
+    int* blk = nullptr;            // scan scratch
+    float4* pts = nullptr;         // points sorted by cell
+    int* idx = nullptr;            // original index of each sorted point
+    int* pcell = nullptr;          // cell of each input point
+    int cap = 0;
+    float min_cell = 1.f;
+};
+
+// ---- Ceres-equivalent LM state (device) ----
+struct LMState {
+    double x[7], cand[7];
+    double A[21], g[6];            // current (unscaled) JtJ upper triangle, gradient Jt r
+    double cost, initial_cost;
+    double scale[6], diag[6];
+    double radius, decrease_factor, x_norm, mcc, step_norm;
+    int reuse_diag, iteration, done, termination, successful, nres;
+    unsigned ticket;
+};
+
+struct OdomState {                 // laserOdometry.cpp:123-137
+    double para[7];                // q_last_curr (x,y,z,w), t_last_curr
+    double q_w[4], t_w[3];
+};
+struct MapState {                  // laserMapping.cpp:58-120
+    double parameters[7];          // q_w_curr, t_w_curr
+    double q_wmap_wodom[4], t_wmap_wodom[3];
+    double q_wodom[4], t_wodom[3];
+    int cenW, cenH, cenD;
+    int shift[3];                  // cube shift applied this frame
+    int cI, cJ, cK;
+    int valid_num;
+    int valid_ind[125];
+    int optimize;                  // map corner > 10 && surf > 50
+    int n_corner_map, n_surf_map;  // FromMap sizes
+    int n_corner_stack, n_surf_stack;
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Ctx {
+    aloam_params P;
+    int device = 0;
+    std::string err;
+    hipStream_t stream = nullptr;
+    bool profiling = false;
+    aloam_timing timing{};
+    std::vector<DevBuf> bufs;
+
+    // ---- scanRegistration ----
+    int cap_in = 0;
+    float4* d_in = nullptr;        // raw points staging
+    float4* d_cl = nullptr;        // after NaN / range filter
+    int* d_sid = nullptr;          // scanID per filtered point (-1 = dropped)
+    float* d_ori = nullptr;        // raw -atan2f per filtered point
+    int* d_blk = nullptr;          // block scratch
+    int* d_hist = nullptr;         // line x block histogram
+    float4* d_cloud = nullptr;     // laserCloud (line ordered, intensity)
+    float* d_curv = nullptr;
+    float4* d_scratch_xyz = nullptr;   // per-line scratch for lines above the LDS cap
+    unsigned long long* d_scratch_keys = nullptr;
+    int* d_scratch_i = nullptr;
+    int* d_line_sharp = nullptr;   // [MAXL][12]
+    int* d_line_lsharp = nullptr;  // [MAXL][120]
+    int* d_line_flat = nullptr;    // [MAXL][24]
+    int* d_line_cnt = nullptr;     // [MAXL][4] sharp, lsharp, flat, lessflat
+    float4* d_line_lf = nullptr;   // per-line less-flat centroids at line offsets
+    ScanMeta* d_meta = nullptr;
+    ScanMeta h_meta{};
+    // scanRegistration outputs (the "current" features)
+    float4 *d_sharp = nullptr, *d_lsharp = nullptr, *d_flat = nullptr, *d_lflat = nullptr;
+    int *d_sharp_idx = nullptr, *d_lsharp_idx = nullptr, *d_flat_idx = nullptr;
+    int n_full = 0, n_sharp = 0, n_lsharp = 0, n_flat = 0, n_lflat = 0;
+    bool have_features = false;
+    bool features_from_host = false;
+
+    // ---- laserOdometry ----
+    bool odom_inited = false;
+    int odom_frame_count = 0;
+    OdomState* d_odom = nullptr;
+    OdomState h_odom{};
+    float4 *d_corner_last = nullptr, *d_surf_last = nullptr;
+    int n_corner_last = 0, n_surf_last = 0;
+    Grid g_corner_last, g_surf_last;
+    aloam_factor* d_factors = nullptr;
+    int cap_factors = 0;
+    LMState* d_lm = nullptr;
+    double* d_partials = nullptr;
+    aloam_lm_summary* d_lm_sum = nullptr;   // [ALOAM_MAX_ROUNDS]
+    int* d_round_cnt = nullptr;             // [ALOAM_MAX_ROUNDS][2] correspondences per round
+
+    // ---- laserMapping ----
+    MapState* d_map = nullptr;
+    MapState h_map{};
+    int cap_map = 0;
+    float4* d_mc = nullptr; int* d_mc_cube = nullptr;    // corner map, sorted by cube
+    float4* d_ms = nullptr; int* d_ms_cube = nullptr;    // surf map
+    float4* d_mc2 = nullptr; int* d_mc2_cube = nullptr;  // double buffers
+    float4* d_ms2 = nullptr; int* d_ms2_cube = nullptr;
+    int n_mc = 0, n_ms = 0;                              // host-known sizes (synced per frame)
+    int* d_map_n = nullptr;                              // device sizes [2]
+    int* d_cube_cnt = nullptr;                           // [2][CUBE_N + 1]
+    int* d_cube_off = nullptr;                           // [2][CUBE_N + 1]
+    unsigned char* d_cube_valid = nullptr;               // [CUBE_N]
+    Grid g_map_corner, g_map_surf;
+    float4 *d_map_corner_in = nullptr, *d_map_surf_in = nullptr, *d_map_full_in = nullptr;
+    int n_map_corner_in = 0, n_map_surf_in = 0, n_map_full_in = 0;
+    float4 *d_cstack = nullptr, *d_sstack = nullptr;
+    int* d_stack_n = nullptr;                            // [2]
+    int* d_nbr = nullptr;                                // [queries][5] neighbour slots
+    float4* d_registered = nullptr;
+    int n_registered = 0;
+    bool have_map_input = false;
+    int map_frame_count = 0;
+    // voxel-grid scratch (rocprim)
+    void* d_sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
+    unsigned long long *d_vkeys = nullptr, *d_vkeys2 = nullptr;
+    int *d_vvals = nullptr, *d_vvals2 = nullptr;
+    int cap_voxel = 0;
+    // insertion scratch
+    float4* d_ins_pts = nullptr; int* d_ins_val = nullptr; int* d_ins_val2 = nullptr;
+    float4* d_map_tmp = nullptr;                         // per-cube filter output (map capacity)
+    unsigned long long* d_seg_keys = nullptr;            // per-cube filter key scratch (4 x map capacity)
+    int* d_map_in_n = nullptr;                           // [2] corner / surf input counts (device)
+    int* d_last_n = nullptr;                             // [2] corner_last / surf_last counts (device)
+    unsigned long long* d_cand = nullptr;                // [2] candidate counters (profiling)
+
+    // profiling events: [0..1] scan, [2..3] odom, [4..5] map, search pairs after that
+    static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS;
+    hipEvent_t ev[NEV];
+    bool ev_ready = false;
+};
+
+// error helpers
+#define HIPCHK(x)                                                                        \
+    do {                                                                                 \
+        hipError_t _e = (x);                                                             \
+        if (_e != hipSuccess) {                                                          \
+            throw HipError(std::string(#x) + ": " + hipGetErrorString(_e));              \
+        }                                                                                \
+    } while (0)
+struct HipError {
+    std::string msg;
+    explicit HipError(std::string m) : msg(std::move(m)) {}
+};
+struct ApiError {
+    int code;
+    std::string msg;
+};
+
+// ---- launch entry points (defined in the k_*.hip files) ----
+void scan_registration_launch(Ctx& C, const float4* in, int n);
+void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of, const unsigned char* cube_valid);
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell);
+void odom_round_search(Ctx& C, int round);
+void set_counts2(Ctx& C, int* dst, int a, int b);
+void odom_compose(Ctx& C);
+void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* d_nslots);
+void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq);
+void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2);
+size_t voxel_sort_tmp_bytes(int cap);
+void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout);
+void map_frame_launch(Ctx& C, aloam_map_result* R);
+void* dalloc(Ctx& C, size_t bytes);
+
+}  // namespace aloam

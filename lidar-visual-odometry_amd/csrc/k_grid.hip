@@ -1,0 +1,292 @@
+// k_grid.hip — dense uniform grid index + exact radius k-NN (replaces pcl::KdTreeFLANN).
+//
+// The reference accepts a neighbour only inside a fixed radius: 1-NN with d^2 < 25 in odometry
+// (src/laserOdometry.cpp:386-389,470-473) and 5-NN with d^2[4] < 1 in mapping
+// (src/laserMapping.cpp:582-584,648-650). So an exact radius-r k-NN over a grid with cells of edge
+// >= 2r returns FLANN's answer: a query's r-ball overlaps at most 2 cells per axis (8 cells), chosen
+// by which half of its cell it lies in. Distances are fp32 ((dx^2 + dy^2) + dz^2) like FLANN's
+// L2_Simple<float>; equal distances are ordered by point index.
+//
+// Build = counting sort by cell: bbox (ordered-int atomics) -> per-cell counts -> exclusive scan ->
+// scatter (atomic decrement, which leaves the count array zeroed for the next build).
+#include "aloam_device.hpp"
+#include "aloam_internal.hpp"
+
+namespace aloam {
+
+constexpr int GB = 256;
+
+__device__ inline void grid_params(const unsigned bb[6], float min_cell, GridDesc* d) {
+    float mn[3], mx[3];
+    for (int a = 0; a < 3; a++) { mn[a] = ord2f(bb[a]); mx[a] = ord2f(bb[3 + a]); }
+    float cell = min_cell;
+    int dims[3];
+    for (int it = 0; it < 64; it++) {
+        long long prod = 1;
+        for (int a = 0; a < 3; a++) {
+            float ext = mx[a] - mn[a];
+            if (!(ext >= 0.f)) ext = 0.f;
+            dims[a] = (int)(ext / cell) + 2;
+            prod *= dims[a];
+        }
+        if (prod <= GRID_MAX_CELLS) break;
+        cell *= 1.25f;
+    }
+    d->ox = mn[0]; d->oy = mn[1]; d->oz = mn[2];
+    d->cell = cell; d->inv_cell = 1.0f / cell;
+    d->dx = dims[0]; d->dy = dims[1]; d->dz = dims[2];
+    d->ncells = dims[0] * dims[1] * dims[2];
+}
+
+__device__ inline int cell_coord(float v, float o, float inv) { return (int)floorf((v - o) * inv); }
+
+__global__ void k_grid_init(GridDesc* d) {
+    if (threadIdx.x < 6) d->bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    if (threadIdx.x == 0) { d->n = 0; d->ncells = 0; }
+}
+
+__device__ inline bool grid_include(int i, const int* cube_of, const unsigned char* cube_valid) {
+    if (!cube_of) return true;
+    int c = cube_of[i];
+    return c >= 0 && cube_valid[c];
+}
+
+__global__ void k_grid_bbox(const float4* __restrict__ pts, const int* d_n, const int* cube_of,
+                            const unsigned char* cube_valid, GridDesc* d) {
+    __shared__ unsigned sh[6];
+    if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    const int n = *d_n;
+    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    int cnt = 0;
+    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
+        if (!grid_include(i, cube_of, cube_valid)) continue;
+        float4 p = pts[i];
+        unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
+        for (int a = 0; a < 3; a++) { mn[a] = min(mn[a], v[a]); mx[a] = max(mx[a], v[a]); }
+        cnt++;
+    }
+    for (int a = 0; a < 3; a++) {
+        unsigned long long lo = wave_min_u64(mn[a]), hi = wave_max_u64(mx[a]);
+        if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
+    }
+    cnt = wave_sum_i(cnt);
+    if (lane_id() == 0 && cnt) atomicAdd(&d->n, cnt);
+    __syncthreads();
+    if (threadIdx.x < 3) { atomicMin(&d->bb[threadIdx.x], sh[threadIdx.x]); atomicMax(&d->bb[3 + threadIdx.x], sh[3 + threadIdx.x]); }
+}
+
+__global__ void k_grid_count(const float4* __restrict__ pts, const int* d_n, const int* cube_of,
+                             const unsigned char* cube_valid, GridDesc* d, float min_cell, int* cell_count, int* pcell) {
+    __shared__ GridDesc gd;
+    if (threadIdx.x == 0) {
+        unsigned bb[6];
+        for (int a = 0; a < 6; a++) bb[a] = d->bb[a];
+        gd.n = d->n;
+        grid_params(bb, min_cell, &gd);
+        if (blockIdx.x == 0) {
+            d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
+            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells;
+        }
+    }
+    __syncthreads();
+    const int n = *d_n;
+    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
+        if (!grid_include(i, cube_of, cube_valid)) { pcell[i] = -1; continue; }
+        float4 p = pts[i];
+        int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
+        int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
+        int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
+        int c = (cz * gd.dy + cy) * gd.dx + cx;
+        pcell[i] = c;
+        atomicAdd(&cell_count[c], 1);
+    }
+}
+
+// three-phase exclusive scan of cell_count[0, ncells) into cell_start
+constexpr int SCAN_CHUNK = 4096;
+__global__ void k_grid_scan1(const int* __restrict__ cnt, const GridDesc* d, int* blk) {
+    __shared__ int sh[GB / WAVE];
+    const int nc = d->ncells;
+    const int base = blockIdx.x * SCAN_CHUNK;
+    int s = 0;
+    if (base < nc)
+        for (int i = base + threadIdx.x; i < min(base + SCAN_CHUNK, nc); i += GB) s += cnt[i];
+    s = wave_sum_i(s);
+    if (lane_id() == 0) sh[threadIdx.x / WAVE] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < GB / WAVE; w++) t += sh[w]; blk[blockIdx.x] = t; }
+}
+__global__ void k_grid_scan2(int* blk, const GridDesc* d) {
+    __shared__ int sh[1024];
+    const int nb = (d->ncells + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    // nb <= GRID_MAX_CELLS / SCAN_CHUNK = 1024
+    int v = threadIdx.x < nb ? blk[threadIdx.x] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += t;
+        __syncthreads();
+    }
+    if (threadIdx.x < nb) blk[threadIdx.x] = sh[threadIdx.x] - v;
+}
+__global__ void k_grid_scan3(const int* __restrict__ cnt, const GridDesc* d, const int* blk, int* start) {
+    __shared__ int sh[SCAN_CHUNK];
+    const int nc = d->ncells;
+    const int base = blockIdx.x * SCAN_CHUNK;
+    if (base >= nc) return;
+    const int len = min(SCAN_CHUNK, nc - base);
+    // each thread scans 16 consecutive entries serially, then a block scan of the thread sums
+    const int per = SCAN_CHUNK / GB;
+    int loc[SCAN_CHUNK / GB];
+    int s = 0;
+    for (int k = 0; k < per; k++) {
+        int i = threadIdx.x * per + k;
+        int v = i < len ? cnt[base + i] : 0;
+        loc[k] = s;
+        s += v;
+    }
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < GB; o <<= 1) {
+        int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += t;
+        __syncthreads();
+    }
+    const int off = blk[blockIdx.x] + sh[threadIdx.x] - s;
+    for (int k = 0; k < per; k++) {
+        int i = threadIdx.x * per + k;
+        if (i < len) start[base + i] = off + loc[k];
+    }
+    if (base + len == nc && threadIdx.x == GB - 1) start[nc] = off + s;
+}
+
+__global__ void k_grid_scatter(const float4* __restrict__ pts, const int* d_n, const int* __restrict__ pcell,
+                               const int* __restrict__ start, int* cell_count, float4* __restrict__ spts, int* __restrict__ sidx) {
+    const int n = *d_n;
+    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
+        int c = pcell[i];
+        if (c < 0) continue;
+        int pos = start[c] + atomicSub(&cell_count[c], 1) - 1;
+        spts[pos] = pts[i];
+        sidx[pos] = i;
+    }
+}
+
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell) {
+    g.cap = cap;
+    g.min_cell = min_cell;
+    g.desc = (GridDesc*)dalloc(C, sizeof(GridDesc));
+    g.cell_count = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
+    g.cell_start = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
+    g.blk = (int*)dalloc(C, sizeof(int) * 1024);
+    g.pts = (float4*)dalloc(C, sizeof(float4) * cap);
+    g.idx = (int*)dalloc(C, sizeof(int) * cap);
+    g.pcell = (int*)dalloc(C, sizeof(int) * cap);
+}
+
+void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of,
+                const unsigned char* cube_valid) {
+    hipStream_t st = C.stream;
+    const int nb = std::max(1, std::min(1024, (cap_n + GB - 1) / GB));
+    k_grid_init<<<1, 64, 0, st>>>(g.desc);
+    k_grid_bbox<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc);
+    k_grid_count<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc, g.min_cell, g.cell_count, g.pcell);
+    const int nsb = GRID_MAX_CELLS / SCAN_CHUNK;
+    k_grid_scan1<<<nsb, GB, 0, st>>>(g.cell_count, g.desc, g.blk);
+    k_grid_scan2<<<1, 1024, 0, st>>>(g.blk, g.desc);
+    k_grid_scan3<<<nsb, GB, 0, st>>>(g.cell_count, g.desc, g.blk, g.cell_start);
+    k_grid_scatter<<<nb, GB, 0, st>>>(pts, d_n, g.pcell, g.cell_start, g.cell_count, g.pts, g.idx);
+    HIPCHK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// k-NN of one query by one wave: 8 cells, per-lane sorted top-K, K-round wave merge.
+template <int K>
+__device__ inline int wave_knn(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
+                               const int* __restrict__ sidx, float qx, float qy, float qz, float r2,
+                               int* out_pos, float* out_d2, int* out_idx) {
+    const int lane = lane_id();
+    float bd[K];
+    int bi[K], bp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    float fx = (qx - gd.ox) * gd.inv_cell, fy = (qy - gd.oy) * gd.inv_cell, fz = (qz - gd.oz) * gd.inv_cell;
+    int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+    int x0 = (fx - cx < 0.5f) ? cx - 1 : cx, y0 = (fy - cy < 0.5f) ? cy - 1 : cy, z0 = (fz - cz < 0.5f) ? cz - 1 : cz;
+    for (int c8 = 0; c8 < 8; c8++) {
+        int x = x0 + (c8 & 1), y = y0 + ((c8 >> 1) & 1), z = z0 + (c8 >> 2);
+        if (x < 0 || y < 0 || z < 0 || x >= gd.dx || y >= gd.dy || z >= gd.dz) continue;
+        int c = (z * gd.dy + y) * gd.dx + x;
+        int b = start[c], e = start[c + 1];
+        for (int p = b + lane; p < e; p += WAVE) {
+            float4 v = spts[p];
+            float d2 = sqdist(v.x, v.y, v.z, qx, qy, qz);
+            if (!(d2 < r2)) continue;
+            int id = sidx[p];
+            if (d2 < bd[K - 1] || (d2 == bd[K - 1] && id < bi[K - 1])) {
+                // sorted insertion
+                float nd = d2; int ni = id, np = p;
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                    if (lt) {
+                        float td = bd[k]; int ti = bi[k], tp = bp[k];
+                        bd[k] = nd; bi[k] = ni; bp[k] = np;
+                        nd = td; ni = ti; np = tp;
+                    }
+                }
+            }
+        }
+    }
+    // merge: K rounds of wave argmin over the lanes' heads
+    int head = 0, found = 0;
+    for (int k = 0; k < K; k++) {
+        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
+#pragma unroll
+        for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
+        unsigned long long key = (hp < 0) ? ~0ull : dist_key(hd, hi);
+        unsigned long long mn = wave_min_u64(key);
+        if (mn == ~0ull) break;
+        if (key == mn) head++;
+        int win_pos = __shfl(hp, __ffsll((long long)__ballot(key == mn)) - 1, WAVE);
+        if (lane == 0) {
+            out_pos[k] = win_pos;
+            out_d2[k] = __uint_as_float((unsigned)(mn >> 32));
+            out_idx[k] = (int)(mn & 0xffffffffu);
+        }
+        found++;
+    }
+    return found;
+}
+
+template <int K>
+__global__ void k_knn(const GridDesc* __restrict__ gdp, const int* __restrict__ start, const float4* __restrict__ spts,
+                      const int* __restrict__ sidx, const float4* __restrict__ q, int nq, int k, float r2, int* idx, float* d2) {
+    const int wq = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    if (wq >= nq) return;
+    const GridDesc gd = *gdp;
+    int pos[K], oi[K];
+    float od[K];
+    for (int j = 0; j < K; j++) { pos[j] = -1; oi[j] = -1; od[j] = INFINITY; }
+    float4 qq = q[wq];
+    int f = wave_knn<K>(gd, start, spts, sidx, qq.x, qq.y, qq.z, r2, pos, od, oi);
+    if (lane_id() == 0)
+        for (int j = 0; j < k; j++) {
+            idx[wq * k + j] = j < f ? oi[j] : -1;
+            d2[wq * k + j] = j < f ? od[j] : INFINITY;
+        }
+}
+
+void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2) {
+    const int threads = 256, per_block = threads / WAVE;
+    const int nbk = (nq + per_block - 1) / per_block;
+    const float r2 = radius * radius;
+    if (nbk > 0) k_knn<8><<<nbk, threads, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2);
+    HIPCHK(hipGetLastError());
+}
+
+}  // namespace aloam

@@ -1,0 +1,362 @@
+// k_lm.hip — lidarFactor residuals + analytic SE(3) Jacobians + Ceres-1.12-equivalent LM on gfx950.
+//
+// One LM "pass" = one launch over all factor slots at one parameter vector: every workgroup
+// reduces its slots' Huber-corrected normal equations (21 upper JtJ + 6 Jtr + cost + count) with
+// wave shuffles, publishes them write-through, and the LAST workgroup to arrive (agent-scope
+// ticket) sums the per-workgroup partials in workgroup order — deterministic for a fixed grid —
+// and runs the trust-region logic of ceres::TrustRegionMinimizer + LevenbergMarquardtStrategy:
+//   pass 0:  evaluate at x, Jacobi column scaling, gradient check, first LM step -> candidate
+//   pass k:  evaluate cost + JtJ at the candidate (speculatively), parameter / function tolerance,
+//            gain-ratio accept (keep the candidate's JtJ) or reject, next LM step
+// so the 4 iterations of a Solve (laserOdometry.cpp:573, laserMapping.cpp:715) take 5 launches
+// and no host round trip. Semantics: SURVEY Appendix B. The normal equations replace DENSE_QR's
+// Householder solve of [J; D] (same minimiser, rounding-level difference).
+#include "aloam_device.hpp"
+#include "aloam_internal.hpp"
+
+namespace aloam {
+
+constexpr int LB = 256;          // threads per LM workgroup
+constexpr int NACC = 29;         // 21 JtJ + 6 Jtr + cost + residual-block count
+constexpr int LM_MAX_BLOCKS = 512;
+
+// residual and 6-column tangent Jacobian of one factor at (q, t). Returns #residuals (0 = invalid).
+__device__ inline int eval_factor(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
+    if (f.type < 0) return 0;
+    const dvec3 cp{f.cp[0], f.cp[1], f.cp[2]};
+    dvec3 pr, lp;
+    if (f.type == 0 || f.type == 1) {
+        dquat ql = qslerp_identity(1.0, q);          // lidarFactor.hpp:29,81 (s = 1)
+        pr = qrot(ql, cp);
+        lp = {pr.x + 1.0 * t[0], pr.y + 1.0 * t[1], pr.z + 1.0 * t[2]};
+    } else {
+        pr = qrot(q, cp);                            // lidarFactor.hpp:120,154
+        lp = {pr.x + t[0], pr.y + t[1], pr.z + t[2]};
+    }
+    if (f.type == 0) {                               // LidarEdgeFactor (lidarFactor.hpp:19-43)
+        const dvec3 a{f.a[0], f.a[1], f.a[2]}, b{f.b[0], f.b[1], f.b[2]};
+        const dvec3 u{lp.x - a.x, lp.y - a.y, lp.z - a.z}, v{lp.x - b.x, lp.y - b.y, lp.z - b.z};
+        const dvec3 nu = dcross(u, v);
+        const dvec3 w{a.x - b.x, a.y - b.y, a.z - b.z};
+        const double n = sqrt(w.x * w.x + w.y * w.y + w.z * w.z);
+        r[0] = nu.x / n; r[1] = nu.y / n; r[2] = nu.z / n;
+        // d nu = dlp x w ; dlp/d(theta_k) = -2 (pr x e_k) ; dlp/dt_k = e_k
+        for (int k = 0; k < 3; k++) {
+            dvec3 e{k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
+            dvec3 pe = dcross(pr, e);
+            dvec3 dlp{-2.0 * pe.x, -2.0 * pe.y, -2.0 * pe.z};
+            dvec3 cr = dcross(dlp, w), ct = dcross(e, w);
+            J[0][k] = cr.x / n; J[1][k] = cr.y / n; J[2][k] = cr.z / n;
+            J[0][3 + k] = ct.x / n; J[1][3 + k] = ct.y / n; J[2][3 + k] = ct.z / n;
+        }
+        return 3;
+    }
+    if (f.type == 1 || f.type == 2) {
+        dvec3 nrm;
+        if (f.type == 1) {                           // LidarPlaneFactor (lidarFactor.hpp:69-90)
+            nrm = {f.b[0], f.b[1], f.b[2]};
+            r[0] = (lp.x - f.a[0]) * nrm.x + (lp.y - f.a[1]) * nrm.y + (lp.z - f.a[2]) * nrm.z;
+        } else {                                     // LidarPlaneNormFactor (lidarFactor.hpp:113-125)
+            nrm = {f.a[0], f.a[1], f.a[2]};
+            r[0] = nrm.x * lp.x + nrm.y * lp.y + nrm.z * lp.z + f.b[0];
+        }
+        dvec3 np = dcross(nrm, pr);                  // dr/dtheta = -2 (n x pr)
+        J[0][0] = -2.0 * np.x; J[0][1] = -2.0 * np.y; J[0][2] = -2.0 * np.z;
+        J[0][3] = nrm.x; J[0][4] = nrm.y; J[0][5] = nrm.z;
+        return 1;
+    }
+    // LidarDistanceFactor (lidarFactor.hpp:147-161)
+    r[0] = lp.x - f.a[0]; r[1] = lp.y - f.a[1]; r[2] = lp.z - f.a[2];
+    for (int k = 0; k < 3; k++) {
+        dvec3 e{k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
+        dvec3 pe = dcross(pr, e);
+        J[0][k] = -2.0 * pe.x; J[1][k] = -2.0 * pe.y; J[2][k] = -2.0 * pe.z;
+        for (int i = 0; i < 3; i++) J[i][3 + k] = (i == k) ? 1.0 : 0.0;
+    }
+    return 3;
+}
+
+// ceres::HuberLoss(0.1) + Corrector (rho'' <= 0 => plain sqrt(rho') scaling)
+__device__ inline double huber_scale(double s, double* rho0) {
+    const double a = 0.1, b = a * a;
+    if (s > b) {
+        const double r = sqrt(s);
+        *rho0 = 2.0 * a * r - b;
+        return sqrt(fmax(2.2250738585072014e-308, a / r));
+    }
+    *rho0 = s;
+    return 1.0;
+}
+
+__device__ inline void accumulate(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
+    double r[3], J[3][6];
+    const int m = eval_factor(f, q, t, r, J);
+    if (!m) return;
+    double sq = 0;
+    for (int i = 0; i < m; i++) sq += r[i] * r[i];
+    double rho0;
+    const double sc = huber_scale(sq, &rho0);
+    acc[27] += 0.5 * rho0;
+    acc[28] += 1.0;
+    for (int i = 0; i < m; i++) {
+        double Ji[6];
+        for (int c = 0; c < 6; c++) Ji[c] = J[i][c] * sc;
+        const double ri = r[i] * sc;
+        int k = 0;
+        for (int a = 0; a < 6; a++)
+            for (int b = a; b < 6; b++) acc[k++] += Ji[a] * Ji[b];
+        for (int a = 0; a < 6; a++) acc[21 + a] += Ji[a] * ri;
+    }
+}
+
+// ---- host-side-free LM math (thread 0 of the last workgroup) -------------------------------
+__device__ inline void plus7(const double* x, const double* d, double* out) {
+    const double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    dquat q{x[0], x[1], x[2], x[3]};
+    if (nd > 0.0) {
+        const double sdd = sin(nd) / nd;
+        dquat dq{sdd * d[0], sdd * d[1], sdd * d[2], cos(nd)};
+        dquat r = qmul(dq, q);
+        out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+    } else { out[0] = q.x; out[1] = q.y; out[2] = q.z; out[3] = q.w; }
+    for (int i = 0; i < 3; i++) out[4 + i] = x[4 + i] + d[3 + i];
+}
+__device__ inline double norm7(const double* a) { double s = 0; for (int i = 0; i < 7; i++) s += a[i] * a[i]; return sqrt(s); }
+__device__ inline double grad_max_norm(const double* x, const double* g) {
+    double ng[6], xp[7];
+    for (int i = 0; i < 6; i++) ng[i] = -g[i];
+    plus7(x, ng, xp);
+    double m = 0;
+    for (int i = 0; i < 7; i++) m = fmax(m, fabs(x[i] - xp[i]));
+    return m;
+}
+__device__ inline double Aget(const double* A, int a, int b) {   // upper-triangle packed
+    if (a > b) { int t = a; a = b; b = t; }
+    return A[a * 6 - a * (a - 1) / 2 + (b - a)];
+}
+__device__ inline bool chol_solve6(double M[6][6], const double* rhs, double* y) {
+    double L[6][6] = {};
+    for (int j = 0; j < 6; j++) {
+        double s = M[j][j];
+        for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+        if (!(s > 0.0)) return false;
+        L[j][j] = sqrt(s);
+        for (int i = j + 1; i < 6; i++) {
+            double v = M[i][j];
+            for (int k = 0; k < j; k++) v -= L[i][k] * L[j][k];
+            L[i][j] = v / L[j][j];
+        }
+    }
+    double z[6];
+    for (int i = 0; i < 6; i++) { double v = rhs[i]; for (int k = 0; k < i; k++) v -= L[i][k] * z[k]; z[i] = v / L[i][i]; }
+    for (int i = 5; i >= 0; i--) { double v = z[i]; for (int k = i + 1; k < 6; k++) v -= L[k][i] * y[k]; y[i] = v / L[i][i]; }
+    for (int i = 0; i < 6; i++) if (!isfinite(y[i])) return false;
+    return true;
+}
+
+__device__ void lm_finish(LMState* st, aloam_lm_summary* out, int term) {
+    st->done = 1;
+    st->termination = term;
+    if (out) {
+        out->iterations = st->iteration;
+        out->successful_steps = st->successful;
+        out->termination = term;
+        out->num_residual_blocks = st->nres;
+        out->initial_cost = st->initial_cost;
+        out->final_cost = st->cost;
+    }
+}
+
+// LevenbergMarquardtStrategy::ComputeStep + model cost change; loops over invalid steps.
+__device__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
+    while (true) {
+        if (st->iteration >= max_iter) { lm_finish(st, out, 0); return; }
+        st->iteration++;
+        double As[6][6], gs[6];
+        for (int a = 0; a < 6; a++) {
+            gs[a] = st->scale[a] * st->g[a];
+            for (int b = 0; b < 6; b++) As[a][b] = st->scale[a] * Aget(st->A, a, b) * st->scale[b];
+        }
+        if (!st->reuse_diag)
+            for (int a = 0; a < 6; a++) st->diag[a] = fmin(fmax(As[a][a], 1e-6), 1e32);
+        double M[6][6];
+        for (int a = 0; a < 6; a++) {
+            for (int b = 0; b < 6; b++) M[a][b] = As[a][b];
+            const double D = sqrt(st->diag[a] / st->radius);
+            M[a][a] += D * D;
+        }
+        double y[6];
+        const bool ok = chol_solve6(M, gs, y);
+        st->reuse_diag = 1;
+        double step[6], mcc = -1.0;
+        if (ok) {
+            for (int a = 0; a < 6; a++) step[a] = -y[a];
+            double sg = 0, sAs = 0;
+            for (int a = 0; a < 6; a++) {
+                sg += step[a] * gs[a];
+                double t = 0;
+                for (int b = 0; b < 6; b++) t += As[a][b] * step[b];
+                sAs += step[a] * t;
+            }
+            mcc = -(sg + 0.5 * sAs);
+        }
+        if (!ok || mcc < 0.0) {            // invalid step: StepIsInvalid() == StepRejected(0)
+            st->radius = st->radius / st->decrease_factor;
+            st->decrease_factor *= 2.0;
+            st->reuse_diag = 1;
+            continue;
+        }
+        double delta[6];
+        for (int a = 0; a < 6; a++) delta[a] = step[a] * st->scale[a];
+        plus7(st->x, delta, st->cand);
+        double dx[7];
+        for (int i = 0; i < 7; i++) dx[i] = st->x[i] - st->cand[i];
+        st->step_norm = norm7(dx);
+        st->mcc = mcc;
+        return;
+    }
+}
+
+__device__ void lm_tail(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+    if (pass == 0) {
+        for (int i = 0; i < 7; i++) st->x[i] = xp[i];
+        st->nres = (int)tot[28];
+        st->iteration = 0; st->successful = 0; st->done = 0;
+        st->cost = tot[27]; st->initial_cost = tot[27];
+        if (st->nres == 0) { st->cost = 0; lm_finish(st, out, 4); return; }
+        for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        for (int a = 0; a < 6; a++) st->scale[a] = 1.0 / (1.0 + sqrt(Aget(st->A, a, a)));
+        st->x_norm = norm7(st->x);
+        st->radius = 1e4; st->decrease_factor = 2.0; st->reuse_diag = 0;
+        if (grad_max_norm(st->x, st->g) <= 1e-10) { lm_finish(st, out, 3); return; }
+        lm_next_step(st, out, max_iter);
+        return;
+    }
+    const double new_cost = tot[27];
+    if (st->step_norm <= 1e-8 * (st->x_norm + 1e-8)) { lm_finish(st, out, 2); return; }
+    const double cost_change = st->cost - new_cost;
+    if (fabs(cost_change) <= 1e-6 * st->cost) { lm_finish(st, out, 1); return; }
+    const double rel = cost_change / st->mcc;
+    if (rel > 1e-3) {
+        for (int i = 0; i < 7; i++) { st->x[i] = st->cand[i]; xp[i] = st->cand[i]; }
+        st->x_norm = norm7(st->x);
+        for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        st->cost = new_cost;
+        st->successful++;
+        const double t = 2.0 * rel - 1.0;
+        st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - t * t * t);
+        st->radius = fmin(1e16, st->radius);
+        st->decrease_factor = 2.0;
+        st->reuse_diag = 0;
+        if (grad_max_norm(st->x, st->g) <= 1e-10) { lm_finish(st, out, 3); return; }
+    } else {
+        st->radius = st->radius / st->decrease_factor;
+        st->decrease_factor *= 2.0;
+        st->reuse_diag = 1;
+    }
+    lm_next_step(st, out, max_iter);
+}
+
+__global__ void __launch_bounds__(LB) k_lm_pass(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
+                                                double* partials, aloam_lm_summary* out, int pass, int max_iter,
+                                                const int* gate) {
+    __shared__ double sh[LB / WAVE][NACC];
+    __shared__ double tot[NACC];
+    __shared__ int last;
+    if (gate && *gate == 0) return;                  // mapping skipped (laserMapping.cpp:554)
+    if (pass > 0 && st->done) return;
+    const double* xs = pass == 0 ? xp : st->cand;
+    const dquat q{xs[0], xs[1], xs[2], xs[3]};
+    const double t[3] = {xs[4], xs[5], xs[6]};
+    double acc[NACC];
+#pragma unroll
+    for (int i = 0; i < NACC; i++) acc[i] = 0;
+    for (int i = blockIdx.x * LB + threadIdx.x; i < nslots; i += gridDim.x * LB) accumulate(f[i], q, t, acc);
+    const int w = threadIdx.x / WAVE;
+#pragma unroll
+    for (int i = 0; i < NACC; i++) {
+        double v = wave_sum_d(acc[i]);
+        if (lane_id() == 0) sh[w][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NACC) {
+        double s = 0;
+        for (int ww = 0; ww < LB / WAVE; ww++) s += sh[ww][threadIdx.x];
+        __hip_atomic_store((unsigned long long*)&partials[blockIdx.x * NACC + threadIdx.x], __double_as_longlong(s),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned prev = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x < NACC) {
+        double s = 0;
+        for (int b = 0; b < (int)gridDim.x; b++)
+            s += __longlong_as_double(__hip_atomic_load((unsigned long long*)&partials[b * NACC + threadIdx.x],
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        tot[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st->ticket = 0;
+        lm_tail(st, tot, pass, xp, out, max_iter);
+    }
+}
+
+static int lm_blocks(int nslots) { return std::max(1, std::min(LM_MAX_BLOCKS, (nslots + LB - 1) / LB)); }
+
+// one Ceres Solve: max_iter + 1 passes; `gate` (device int, may be null) disables the solve
+void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate) {
+    const int nb = lm_blocks(nslots);
+    aloam_lm_summary* out = C.d_lm_sum + round;
+    for (int pass = 0; pass <= C.P.max_solver_iterations; pass++)
+        k_lm_pass<<<nb, LB, 0, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_partials, out, pass, C.P.max_solver_iterations, gate);
+    HIPCHK(hipGetLastError());
+}
+
+// ---- test entry: per-factor residuals / Jacobians and the normal equations ----
+__global__ void k_eval_factors(const aloam_factor* __restrict__ f, int n, const double* x, int robust, double* res,
+                               double* jac, double* neq) {
+    __shared__ double sh[LB / WAVE][NACC];
+    const dquat q{x[0], x[1], x[2], x[3]};
+    const double t[3] = {x[4], x[5], x[6]};
+    double acc[NACC];
+    for (int i = 0; i < NACC; i++) acc[i] = 0;
+    for (int i = threadIdx.x; i < n; i += LB) {
+        double r[3] = {0, 0, 0}, J[3][6] = {};
+        const int m = eval_factor(f[i], q, t, r, J);
+        double sc = 1.0, rho0 = 0, sq = 0;
+        for (int k = 0; k < m; k++) sq += r[k] * r[k];
+        if (robust) sc = huber_scale(sq, &rho0); else rho0 = sq;
+        double Js[3][6], rs[3];
+        for (int k = 0; k < 3; k++) {
+            rs[k] = k < m ? r[k] * sc : 0.0;
+            res[i * 3 + k] = rs[k];
+            for (int c = 0; c < 6; c++) { Js[k][c] = k < m ? J[k][c] * sc : 0.0; jac[(i * 3 + k) * 6 + c] = Js[k][c]; }
+        }
+        if (!m) continue;
+        acc[27] += 0.5 * rho0;
+        for (int k = 0; k < m; k++) {
+            int kk = 0;
+            for (int a = 0; a < 6; a++) for (int b = a; b < 6; b++) acc[kk++] += Js[k][a] * Js[k][b];
+            for (int a = 0; a < 6; a++) acc[21 + a] += Js[k][a] * rs[k];
+        }
+    }
+    const int w = threadIdx.x / WAVE;
+    for (int i = 0; i < NACC; i++) { double v = wave_sum_d(acc[i]); if (lane_id() == 0) sh[w][i] = v; }
+    __syncthreads();
+    if (threadIdx.x < 28) { double s = 0; for (int ww = 0; ww < LB / WAVE; ww++) s += sh[ww][threadIdx.x]; neq[threadIdx.x] = s; }
+}
+
+void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq) {
+    k_eval_factors<<<1, LB, 0, C.stream>>>(d_f, n, d_x, robust, d_res, d_jac, d_neq);
+    HIPCHK(hipGetLastError());
+}
+
+}  // namespace aloam

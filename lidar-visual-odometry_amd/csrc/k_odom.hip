@@ -1,0 +1,192 @@
+// k_odom.hip — laserOdometry correspondence search on gfx950 (src/laserOdometry.cpp:380-561).
+//
+// One wave per feature point (sharp points, then flat points):
+//   1. TransformToStart (:154-172, DISTORTION 0 => s = 1) in double, stored as float
+//   2. exact 1-NN in the last less-sharp / less-flat cloud within d^2 < 25 (grid, k_grid.hip)
+//   3. the reference's scan-line window search, forward then backward from the closest point,
+//      64 candidates per step: break index by ballot, first-occurrence minimum by a 64-bit
+//      (d^2, order) wave-min, strict '<' against the running minimum (init 25) exactly like :400-441
+//   4. LidarEdgeFactor / LidarPlaneFactor residual block written to the point's factor slot
+#include "aloam_device.hpp"
+#include "aloam_internal.hpp"
+
+namespace aloam {
+
+// wave_knn<1> lives in k_grid.hip; a local copy keeps this file self-contained.
+__device__ inline int wave_nn1(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
+                               const int* __restrict__ sidx, float qx, float qy, float qz, float r2, int* out_idx, float* out_d2) {
+    unsigned long long best = ~0ull;
+    float fx = (qx - gd.ox) * gd.inv_cell, fy = (qy - gd.oy) * gd.inv_cell, fz = (qz - gd.oz) * gd.inv_cell;
+    int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+    int x0 = (fx - cx < 0.5f) ? cx - 1 : cx, y0 = (fy - cy < 0.5f) ? cy - 1 : cy, z0 = (fz - cz < 0.5f) ? cz - 1 : cz;
+    for (int c8 = 0; c8 < 8; c8++) {
+        int x = x0 + (c8 & 1), y = y0 + ((c8 >> 1) & 1), z = z0 + (c8 >> 2);
+        if (x < 0 || y < 0 || z < 0 || x >= gd.dx || y >= gd.dy || z >= gd.dz) continue;
+        int c = (z * gd.dy + y) * gd.dx + x;
+        int b = start[c], e = start[c + 1];
+        for (int p = b + lane_id(); p < e; p += WAVE) {
+            float4 v = spts[p];
+            float d2 = sqdist(v.x, v.y, v.z, qx, qy, qz);
+            if (d2 < r2) {
+                unsigned long long k = dist_key(d2, sidx[p]);
+                best = k < best ? k : best;
+            }
+        }
+    }
+    best = wave_min_u64(best);
+    if (best == ~0ull) return 0;
+    *out_idx = (int)(best & 0xffffffffu);
+    *out_d2 = __uint_as_float((unsigned)(best >> 32));
+    return 1;
+}
+
+__device__ inline int line_of(float intensity) { return int(intensity); }
+
+// forward/backward scan-line search of laserOdometry.cpp:400-441 (corner) / :483-532 (surf)
+// mode 0 = corner (one candidate set), 1 = surf (two sets).
+template <int MODE>
+__device__ inline void window_search(const float4* __restrict__ cl, int n, int closest, int cid, float sx, float sy, float sz,
+                                     int* ind2, int* ind3) {
+    const int lane = lane_id();
+    float best2 = 25.0f, best3 = 25.0f;
+    int i2 = -1, i3 = -1;
+    // ---- forward (increasing index) ----
+    for (int base = closest + 1; base < n; base += WAVE) {
+        const int j = base + lane;
+        const bool in = j < n;
+        float4 p = in ? cl[j] : make_float4(0, 0, 0, 0);
+        const int line = line_of(p.w);
+        const bool brk = in && (line > (cid + 2.5));
+        const unsigned long long bm = __ballot(brk);
+        const int first_brk = bm ? base + (__ffsll((long long)bm) - 1) : 0x7fffffff;
+        const bool live = in && j < first_brk;
+        const float d = sqdist(p.x, p.y, p.z, sx, sy, sz);
+        bool c2, c3;
+        if (MODE == 0) { c2 = live && !(line <= cid); c3 = false; }
+        else { c2 = live && line <= cid; c3 = live && line > cid; }
+        unsigned long long k2 = c2 ? dist_key(d, j) : ~0ull, k3 = c3 ? dist_key(d, j) : ~0ull;
+        k2 = wave_min_u64(k2);
+        if (k2 != ~0ull) { float dm = __uint_as_float((unsigned)(k2 >> 32)); if (dm < best2) { best2 = dm; i2 = (int)(k2 & 0xffffffffu); } }
+        if (MODE == 1) {
+            k3 = wave_min_u64(k3);
+            if (k3 != ~0ull) { float dm = __uint_as_float((unsigned)(k3 >> 32)); if (dm < best3) { best3 = dm; i3 = (int)(k3 & 0xffffffffu); } }
+        }
+        if (bm) break;
+    }
+    // ---- backward (decreasing index): first occurrence = largest index among equal distances ----
+    for (int base = closest - 1; base >= 0; base -= WAVE) {
+        const int j = base - lane;
+        const bool in = j >= 0;
+        float4 p = in ? cl[j] : make_float4(0, 0, 0, 0);
+        const int line = line_of(p.w);
+        const bool brk = in && (line < (cid - 2.5));
+        const unsigned long long bm = __ballot(brk);
+        const int first_brk = bm ? base - (__ffsll((long long)bm) - 1) : -1;
+        const bool live = in && j > first_brk;
+        const float d = sqdist(p.x, p.y, p.z, sx, sy, sz);
+        bool c2, c3;
+        if (MODE == 0) { c2 = live && !(line >= cid); c3 = false; }
+        else { c2 = live && line >= cid; c3 = live && line < cid; }
+        const unsigned ord = 0x7fffffffu - (unsigned)j;
+        unsigned long long k2 = c2 ? dist_key(d, (int)ord) : ~0ull, k3 = c3 ? dist_key(d, (int)ord) : ~0ull;
+        k2 = wave_min_u64(k2);
+        if (k2 != ~0ull) { float dm = __uint_as_float((unsigned)(k2 >> 32)); if (dm < best2) { best2 = dm; i2 = (int)(0x7fffffffu - (unsigned)(k2 & 0xffffffffu)); } }
+        if (MODE == 1) {
+            k3 = wave_min_u64(k3);
+            if (k3 != ~0ull) { float dm = __uint_as_float((unsigned)(k3 >> 32)); if (dm < best3) { best3 = dm; i3 = (int)(0x7fffffffu - (unsigned)(k3 & 0xffffffffu)); } }
+        }
+        if (bm) break;
+    }
+    *ind2 = i2;
+    *ind3 = i3;
+}
+
+__global__ void __launch_bounds__(256) k_odom_search(
+    const float4* __restrict__ sharp, int n_sharp, const float4* __restrict__ flat, int n_flat,
+    const float4* __restrict__ corner_last, int n_cl, const float4* __restrict__ surf_last, int n_sl,
+    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
+    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
+    const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt) {
+    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int lane = lane_id();
+    if (qi >= n_sharp + n_flat) return;
+    const bool is_corner = qi < n_sharp;
+    const float4 pi = is_corner ? sharp[qi] : flat[qi - n_sharp];
+    // TransformToStart (:154-172)
+    const dquat q{odom->para[0], odom->para[1], odom->para[2], odom->para[3]};
+    const dquat ql = qslerp_identity(1.0, q);
+    const dvec3 r = qrot(ql, {pi.x, pi.y, pi.z});
+    const float sx = (float)(r.x + 1.0 * odom->para[4]);
+    const float sy = (float)(r.y + 1.0 * odom->para[5]);
+    const float sz = (float)(r.z + 1.0 * odom->para[6]);
+    aloam_factor f;
+    f.type = -1; f.pad = 0;
+    f.cp[0] = pi.x; f.cp[1] = pi.y; f.cp[2] = pi.z;
+    const float4* cl = is_corner ? corner_last : surf_last;
+    const int n = is_corner ? n_cl : n_sl;
+    int closest = -1;
+    float d2 = 0.f;
+    int found;
+    if (is_corner) found = n > 0 ? wave_nn1(*gdc, cs_c, sp_c, si_c, sx, sy, sz, 25.0f, &closest, &d2) : 0;
+    else found = n > 0 ? wave_nn1(*gds, cs_s, sp_s, si_s, sx, sy, sz, 25.0f, &closest, &d2) : 0;
+    if (found) {
+        const int cid = line_of(cl[closest].w);
+        int i2, i3;
+        if (is_corner) {
+            window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+            if (i2 >= 0) {
+                const float4 a = cl[closest], b = cl[i2];
+                f.type = 0;
+                f.a[0] = a.x; f.a[1] = a.y; f.a[2] = a.z;
+                f.b[0] = b.x; f.b[1] = b.y; f.b[2] = b.z;
+            }
+        } else {
+            window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+            if (i2 >= 0 && i3 >= 0) {
+                const float4 pj = cl[closest], pl = cl[i2], pm = cl[i3];
+                // LidarPlaneFactor ctor (lidarFactor.hpp:64-65)
+                dvec3 jj{pj.x, pj.y, pj.z}, ll{pl.x, pl.y, pl.z}, mm{pm.x, pm.y, pm.z};
+                dvec3 nn = dcross({jj.x - ll.x, jj.y - ll.y, jj.z - ll.z}, {jj.x - mm.x, jj.y - mm.y, jj.z - mm.z});
+                double z = nn.x * nn.x + nn.y * nn.y + nn.z * nn.z;
+                if (z > 0) { double s = sqrt(z); nn = {nn.x / s, nn.y / s, nn.z / s}; }
+                f.type = 1;
+                f.a[0] = jj.x; f.a[1] = jj.y; f.a[2] = jj.z;
+                f.b[0] = nn.x; f.b[1] = nn.y; f.b[2] = nn.z;
+            }
+        }
+    }
+    if (lane == 0) {
+        out[qi] = f;
+        if (f.type >= 0) atomicAdd(&round_cnt[is_corner ? 0 : 1], 1);
+    }
+}
+
+// t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582)
+__global__ void k_odom_compose(OdomState* o) {
+    dquat qw{o->q_w[0], o->q_w[1], o->q_w[2], o->q_w[3]};
+    dquat ql{o->para[0], o->para[1], o->para[2], o->para[3]};
+    dvec3 r = qrot(qw, {o->para[4], o->para[5], o->para[6]});
+    o->t_w[0] = o->t_w[0] + r.x; o->t_w[1] = o->t_w[1] + r.y; o->t_w[2] = o->t_w[2] + r.z;
+    dquat n = qmul(qw, ql);
+    o->q_w[0] = n.x; o->q_w[1] = n.y; o->q_w[2] = n.z; o->q_w[3] = n.w;
+}
+
+void odom_round_search(Ctx& C, int round) {
+    const int nq = C.n_sharp + C.n_flat;
+    if (nq == 0) return;
+    const int threads = 256;
+    const int nb = (nq * WAVE + threads - 1) / threads;
+    k_odom_search<<<nb, threads, 0, C.stream>>>(
+        C.d_sharp, C.n_sharp, C.d_flat, C.n_flat, C.d_corner_last, C.n_corner_last, C.d_surf_last, C.n_surf_last,
+        C.g_corner_last.desc, C.g_corner_last.cell_start, C.g_corner_last.pts, C.g_corner_last.idx,
+        C.g_surf_last.desc, C.g_surf_last.cell_start, C.g_surf_last.pts, C.g_surf_last.idx,
+        C.d_odom, C.d_factors, C.d_round_cnt + 2 * round);
+    HIPCHK(hipGetLastError());
+}
+
+void odom_compose(Ctx& C) {
+    k_odom_compose<<<1, 1, 0, C.stream>>>(C.d_odom);
+    HIPCHK(hipGetLastError());
+}
+
+}  // namespace aloam

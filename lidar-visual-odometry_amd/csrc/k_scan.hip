@@ -1,0 +1,698 @@
+// k_scan.hip — scanRegistration on gfx950 (src/scanRegistration.cpp:114-411).
+//
+// Pipeline (one stream, no host round trip):
+//   filter_count/filter_scan/filter_scatter  removeNaN + removeClosedPointCloud, order preserved  (:85-112,136-137)
+//   bucket_classify                          elevation -> scanID, azimuth, halfPassed switch index (:141-236)
+//   bucket_scan / bucket_scatter             stable counting sort into laserCloud by scanID        (:238-252)
+//   curvature                                11-point fp32 stencil, reference summation order       (:256-266)
+//   line_features (one workgroup per line)   segment sort, corner / flat greedy selection,
+//                                            less-flat candidates, per-line VoxelGrid(0.2)          (:277-408)
+//   concat                                   line-major concatenation of the five outputs          (:271-274,407)
+// Bit-exactness: libm calls are restated (libm_f32.h atan2f = glibc flt-32; double atan from ocml,
+// last-ulp double differences cannot move a float elevation across a scan boundary except with
+// probability ~2^-29 per point), and -ffp-contract=off keeps every fp32 op separately rounded.
+#include "aloam_device.hpp"
+#include "aloam_internal.hpp"
+#include "libm_f32.h"
+
+namespace aloam {
+
+constexpr int SB = 256;  // threads per block for the per-point kernels
+
+// ------------------------------------------------------------------------------------------
+// block-wide exclusive scan of one int per thread (256 threads)
+__device__ inline int block_excl_scan_256(int v, int* sh, int* total) {
+    const int lane = lane_id(), w = threadIdx.x / WAVE;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        int t = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += t;
+    }
+    if (lane == WAVE - 1) sh[w] = x;
+    __syncthreads();
+    int base = 0;
+    for (int i = 0; i < w; i++) base += sh[i];
+    int tot = 0;
+    for (int i = 0; i < SB / WAVE; i++) tot += sh[i];
+    __syncthreads();
+    if (total) *total = tot;
+    return base + x - v;
+}
+
+__device__ inline bool keep_point(const float4 p, int dense, float thres) {
+    if (!dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return false;
+    // removeClosedPointCloud (:99): float arithmetic, strict <
+    return !(p.x * p.x + p.y * p.y + p.z * p.z < thres * thres);
+}
+
+__global__ void k_filter_count(const float4* __restrict__ in, int n, int dense, float thres, int* blk) {
+    __shared__ int sh[SB / WAVE];
+    int i = blockIdx.x * SB + threadIdx.x;
+    int k = (i < n) && keep_point(in[i], dense, thres);
+    int tot;
+    block_excl_scan_256(k, sh, &tot);
+    if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// single block of 1024: exclusive scan of nb ints in place, total -> *total
+__global__ void k_scan_small(int* a, int nb, int* total) {
+    __shared__ int sh[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < nb; base += 1024) {
+        int i = base + threadIdx.x;
+        int v = i < nb ? a[i] : 0;
+        sh[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += t;
+            __syncthreads();
+        }
+        int incl = sh[threadIdx.x];
+        if (i < nb) a[i] = carry + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+__global__ void k_filter_scatter(const float4* __restrict__ in, int n, int dense, float thres, const int* blk,
+                                 float4* __restrict__ out) {
+    __shared__ int sh[SB / WAVE];
+    int i = blockIdx.x * SB + threadIdx.x;
+    float4 p = i < n ? in[i] : make_float4(0, 0, 0, 0);
+    int k = (i < n) && keep_point(p, dense, thres);
+    int r = block_excl_scan_256(k, sh, nullptr);
+    if (k) out[blk[blockIdx.x] + r] = p;
+}
+
+// ------------------------------------------------------------------------------------------
+// start / end azimuth (:141-153), recomputed identically by every thread that needs it
+struct Oris { float start, end; };
+__device__ inline Oris start_end_ori(const float4* cl, int n) {
+    Oris o;
+    o.start = -lm_atan2f(cl[0].y, cl[0].x);
+    o.end = -lm_atan2f(cl[n - 1].y, cl[n - 1].x) + 2 * M_PI;
+    if (o.end - o.start > 3 * M_PI) o.end -= 2 * M_PI;
+    else if (o.end - o.start < M_PI) o.end += 2 * M_PI;
+    return o;
+}
+
+// scanID of one point (:166-205); -1 = dropped
+__device__ inline int scan_id(float4 p, int N_SCANS, float gmin, float gmax) {
+    float angle = atan((double)p.z / sqrt((double)(p.x * p.x + p.y * p.y))) * 180 / M_PI;
+    int scanID;
+    if (N_SCANS == 16) {
+        scanID = int((angle + 15) / 2 + 0.5);
+        if (scanID > (N_SCANS - 1) || scanID < 0) return -1;
+    } else if (N_SCANS == 32) {
+        scanID = int((angle + 92.0 / 3.0) * 3.0 / 4.0);
+        if (scanID > (N_SCANS - 1) || scanID < 0) return -1;
+    } else if (N_SCANS == 64) {
+        if (angle >= -8.83) scanID = int((2 - angle) * 3.0 + 0.5);
+        else scanID = N_SCANS / 2 + int((-8.83 - angle) * 2.0 + 0.5);
+        if (angle > 2 || angle < -24.33 || scanID > 50 || scanID < 0) return -1;
+    } else {
+        double lo = gmin, hi = gmax;
+        scanID = int((angle - lo) / (hi - lo) * (N_SCANS - 1) + 0.5);
+        if (scanID > (N_SCANS - 1) || scanID < 0) return -1;
+    }
+    return scanID;
+}
+
+// first half of the azimuth unwrap (:209-224): returns adjusted ori, sets *passed
+__device__ inline float ori_branch1(float ori, float startOri, bool* passed) {
+    if (ori < startOri - M_PI / 2) ori += 2 * M_PI;
+    else if (ori > startOri + M_PI * 3 / 2) ori -= 2 * M_PI;
+    *passed = (ori - startOri > M_PI);
+    return ori;
+}
+__device__ inline float ori_branch2(float ori, float endOri) {   // (:225-236)
+    ori += 2 * M_PI;
+    if (ori < endOri - M_PI * 3 / 2) ori += 2 * M_PI;
+    else if (ori > endOri + M_PI / 2) ori -= 2 * M_PI;
+    return ori;
+}
+
+__global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta* meta, int N_SCANS, float gmin, float gmax,
+                                  int* __restrict__ sid, float* __restrict__ ori_out, int* hist, int nb, ScanMeta* meta_w) {
+    __shared__ int h[MAXL];
+    const int n = meta->n_cl;
+    for (int i = threadIdx.x; i < N_SCANS; i += SB) h[i] = 0;
+    __syncthreads();
+    int j = blockIdx.x * SB + threadIdx.x;
+    if (j < n) {
+        float4 p = cl[j];
+        int s = scan_id(p, N_SCANS, gmin, gmax);
+        sid[j] = s;
+        if (s >= 0) {
+            float ori = -lm_atan2f(p.y, p.x);
+            ori_out[j] = ori;
+            Oris o = start_end_ori(cl, n);
+            bool passed;
+            ori_branch1(ori, o.start, &passed);
+            if (passed) atomicMin(&meta_w->jstar, j);
+            atomicAdd(&h[s], 1);
+        }
+    }
+    __syncthreads();
+    if (blockIdx.x < nb)
+        for (int i = threadIdx.x; i < N_SCANS; i += SB) hist[i * nb + blockIdx.x] = h[i];
+}
+
+// single block: exclusive scan of hist (line-major) and the line offsets
+__global__ void k_bucket_scan(int* hist, int nb, int N_SCANS, ScanMeta* meta) {
+    __shared__ int sh[1024];
+    __shared__ int carry;
+    const int total_n = nb * N_SCANS;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < total_n; base += 1024) {
+        int i = base + threadIdx.x;
+        int v = i < total_n ? hist[i] : 0;
+        sh[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += t;
+            __syncthreads();
+        }
+        int incl = sh[threadIdx.x];
+        if (i < total_n) {
+            hist[i] = carry + incl - v;
+            if (i % nb == 0) meta->line_off[i / nb] = carry + incl - v;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        meta->line_off[N_SCANS] = carry;
+        meta->cloud_size = carry;
+    }
+}
+
+__global__ void k_bucket_scatter(const float4* __restrict__ cl, const ScanMeta* meta, const int* __restrict__ sid,
+                                 const float* __restrict__ ori_in, const int* __restrict__ hist, int nb, int N_SCANS,
+                                 float4* __restrict__ cloud) {
+    __shared__ int wcnt[SB / WAVE][MAXL];
+    const int n = meta->n_cl;
+    const int w = threadIdx.x / WAVE, lane = lane_id();
+    for (int i = threadIdx.x; i < (SB / WAVE) * MAXL; i += SB) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    int j = blockIdx.x * SB + threadIdx.x;
+    int s = j < n ? sid[j] : -1;
+    // stable rank within the wave among equal scanIDs (match-any emulation)
+    int rank = 0;
+    unsigned long long active = __ballot(s >= 0);
+    while (active) {
+        int leader = __ffsll((long long)active) - 1;
+        int ls = __shfl(s, leader, WAVE);
+        unsigned long long m = __ballot(s == ls);
+        if (s == ls) rank = __popcll(m & lanemask_lt64());
+        if (lane == leader) wcnt[w][ls] = __popcll(m);
+        active &= ~m;
+    }
+    __syncthreads();
+    if (s >= 0) {
+        int before = 0;
+        for (int ww = 0; ww < w; ww++) before += wcnt[ww][s];
+        float4 p = cl[j];
+        Oris o = start_end_ori(cl, n);
+        float ori = ori_in[j];
+        if (j <= meta->jstar) { bool passed; ori = ori_branch1(ori, o.start, &passed); }
+        else ori = ori_branch2(ori, o.end);
+        float relTime = (ori - o.start) / (o.end - o.start);
+        p.w = s + 0.1 * relTime;   // scanPeriod * relTime in double, stored as float (:239)
+        cloud[hist[s * nb + blockIdx.x] + before + rank] = p;
+    }
+}
+
+// curvature (:256-266) for i in [5, cloudSize - 5); 0 elsewhere
+__global__ void k_curvature(const float4* __restrict__ c, const ScanMeta* meta, float* __restrict__ curv) {
+    const int n = meta->cloud_size;
+    int i = blockIdx.x * SB + threadIdx.x;
+    if (i >= n) return;
+    if (i < 5 || i >= n - 5) { curv[i] = 0.f; return; }
+    const float4* p = c + i;
+    float dX = p[-5].x + p[-4].x + p[-3].x + p[-2].x + p[-1].x - 10 * p[0].x + p[1].x + p[2].x + p[3].x + p[4].x + p[5].x;
+    float dY = p[-5].y + p[-4].y + p[-3].y + p[-2].y + p[-1].y - 10 * p[0].y + p[1].y + p[2].y + p[3].y + p[4].y + p[5].y;
+    float dZ = p[-5].z + p[-4].z + p[-3].z + p[-2].z + p[-1].z - 10 * p[0].z + p[1].z + p[2].z + p[3].z + p[4].z + p[5].z;
+    curv[i] = dX * dX + dY * dY + dZ * dZ;
+}
+
+// ------------------------------------------------------------------------------------------
+// libstdc++ std::sort (introsort) replica on int indices compared by curvature — only used for
+// segments whose curvatures contain exact ties, where the unstable order of the reference's
+// std::sort (:288) decides which of the equal points is picked first.
+struct CurvLess {
+    const float* c;
+    int base;
+    __device__ bool operator()(int a, int b) const { return c[a - base] < c[b - base]; }
+};
+__device__ void dev_unguarded_linear_insert(int* last, CurvLess less) {
+    int val = *last;
+    int* next = last - 1;
+    while (less(val, *next)) { *last = *next; last = next; --next; }
+    *last = val;
+}
+__device__ void dev_insertion_sort(int* first, int* last, CurvLess less) {
+    if (first == last) return;
+    for (int* i = first + 1; i != last; ++i) {
+        if (less(*i, *first)) {
+            int val = *i;
+            for (int* k = i; k != first; --k) *k = *(k - 1);
+            *first = val;
+        } else dev_unguarded_linear_insert(i, less);
+    }
+}
+__device__ void dev_adjust_heap(int* first, long hole, long len, int value, CurvLess less) {
+    const long top = hole;
+    long child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (less(first[child], first[child - 1])) child--;
+        first[hole] = first[child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        first[hole] = first[child - 1];
+        hole = child - 1;
+    }
+    long parent = (hole - 1) / 2;
+    while (hole > top && less(first[parent], value)) { first[hole] = first[parent]; hole = parent; parent = (hole - 1) / 2; }
+    first[hole] = value;
+}
+__device__ void dev_heap_sort(int* first, int* last, CurvLess less) {
+    long len = last - first;
+    if (len >= 2) {
+        long parent = (len - 2) / 2;
+        while (true) { dev_adjust_heap(first, parent, len, first[parent], less); if (parent == 0) break; parent--; }
+    }
+    while (last - first > 1) {
+        --last;
+        int v = *last; *last = *first;
+        dev_adjust_heap(first, 0L, (long)(last - first), v, less);
+    }
+}
+__device__ inline void iswap(int* a, int* b) { int t = *a; *a = *b; *b = t; }
+__device__ void dev_std_sort(int* first, int* last, CurvLess less) {
+    if (first == last) return;
+    long n = last - first;
+    long depth = (63 - __clzll((long long)n)) * 2;
+    // introsort loop with an explicit stack (recursion on the right part)
+    int* stk_f[64]; int* stk_l[64]; long stk_d[64]; int sp = 0;
+    stk_f[sp] = first; stk_l[sp] = last; stk_d[sp] = depth; sp++;
+    while (sp > 0) {
+        sp--;
+        int* f = stk_f[sp]; int* l = stk_l[sp]; long d = stk_d[sp];
+        while (l - f > 16) {
+            if (d == 0) { dev_heap_sort(f, l, less); break; }
+            --d;
+            int* mid = f + (l - f) / 2;
+            int *a = f + 1, *b = mid, *c = l - 1;
+            if (less(*a, *b)) {
+                if (less(*b, *c)) iswap(f, b); else if (less(*a, *c)) iswap(f, c); else iswap(f, a);
+            } else if (less(*a, *c)) iswap(f, a); else if (less(*b, *c)) iswap(f, c); else iswap(f, b);
+            int *lo = f + 1, *hi = l;
+            while (true) {
+                while (less(*lo, *f)) ++lo;
+                --hi;
+                while (less(*f, *hi)) --hi;
+                if (!(lo < hi)) break;
+                iswap(lo, hi);
+                ++lo;
+            }
+            // recurse on [lo, l) first (pushed), continue with [f, lo)
+            // libstdc++ recurses on the right part then loops on the left; order of processing
+            // does not change the result because the two ranges are disjoint.
+            stk_f[sp] = lo; stk_l[sp] = l; stk_d[sp] = d; sp++;
+            l = lo;
+        }
+    }
+    if (n > 16) {
+        dev_insertion_sort(first, first + 16, less);
+        for (int* i = first + 16; i != last; ++i) dev_unguarded_linear_insert(i, less);
+    } else dev_insertion_sort(first, last, less);
+}
+
+// ------------------------------------------------------------------------------------------
+// One workgroup (1024 threads) per scan line: (:277-408)
+constexpr int LT = 1024;
+
+__device__ inline void suppress_neighbours(int ind, const float* X, const float* Y, const float* Z, volatile int8_t* picked) {
+    for (int l = 1; l <= 5; l++) {
+        float dx = X[ind + l] - X[ind + l - 1], dy = Y[ind + l] - Y[ind + l - 1], dz = Z[ind + l] - Z[ind + l - 1];
+        if (dx * dx + dy * dy + dz * dz > 0.05) break;
+        picked[ind + l] = 1;
+    }
+    for (int l = -1; l >= -5; l--) {
+        float dx = X[ind + l] - X[ind + l + 1], dy = Y[ind + l] - Y[ind + l + 1], dz = Z[ind + l] - Z[ind + l + 1];
+        if (dx * dx + dy * dy + dz * dz > 0.05) break;
+        picked[ind + l] = 1;
+    }
+}
+
+__device__ inline void bitonic_sort_u64(unsigned long long* k, int n2) {
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {
+                int i = 2 * t - (t & (stride - 1));
+                int j = i + stride;
+                bool asc = ((i & size) == 0);
+                unsigned long long a = k[i], b = k[j];
+                if ((a > b) == asc) { k[i] = b; k[j] = a; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__ cloud, const float* __restrict__ gcurv,
+                                                      const ScanMeta* meta, int N_SCANS,
+                                                      float4* g_xyz, unsigned long long* g_keys, int* g_i,
+                                                      int* line_sharp, int* line_lsharp, int* line_flat, int* line_cnt,
+                                                      float4* line_lf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    // all LDS is dynamic (Guideline 17: no statics ahead of the dynamic base)
+    struct LineShared { int flag, ncand, nrun, cnt[3]; unsigned bb[6]; int wsum[LT / WAVE]; };
+    LineShared& SH = *(LineShared*)smem_raw;
+    unsigned char* smem = smem_raw + 128;
+    static_assert(sizeof(LineShared) <= 128, "LineShared");
+    int& s_flag = SH.flag; int& s_ncand = SH.ncand; int& s_nrun = SH.nrun;
+    int* s_cnt = SH.cnt; unsigned* s_bb = SH.bb; int* s_wsum = SH.wsum;
+    const int line = blockIdx.x;
+    const int off0 = meta->line_off[line], off1 = meta->line_off[line + 1];
+    const int nl = off1 - off0;
+    const int s = off0 + 5, e = off1 - 6;
+    int* cnt_out = line_cnt + line * 4;
+    if (e - s < 6) {
+        if (threadIdx.x < 4) cnt_out[threadIdx.x] = 0;
+        return;
+    }
+    const bool big = nl > LINE_LDS_CAP;
+    // carve LDS (or global scratch at the line's offset for oversized lines)
+    float *X, *Y, *Z, *Cv;
+    int* S;                 // sorted global indices per segment position
+    volatile int8_t* picked;
+    int8_t* label;
+    unsigned long long* keys;
+    if (!big) {
+        X = (float*)smem;
+        Y = X + LINE_LDS_CAP;
+        Z = Y + LINE_LDS_CAP;
+        Cv = Z + LINE_LDS_CAP;
+        S = (int*)(Cv + LINE_LDS_CAP);
+        keys = (unsigned long long*)(S + LINE_LDS_CAP);
+        picked = (volatile int8_t*)(keys + LINE_LDS_CAP);
+        label = (int8_t*)(picked + LINE_LDS_CAP);
+    } else {
+        float* gx = (float*)g_xyz;     // 4 floats per cloud point of scratch
+        X = gx + off0;
+        Y = gx + (size_t)meta->cloud_size + off0;
+        Z = gx + 2 * (size_t)meta->cloud_size + off0;
+        Cv = gx + 3 * (size_t)meta->cloud_size + off0;
+        S = g_i + off0;
+        keys = g_keys + 2 * (size_t)off0;   // 2x room for the power-of-two padding
+        picked = (volatile int8_t*)(g_i + (size_t)meta->cloud_size + off0);
+        label = (int8_t*)(g_i + 2 * (size_t)meta->cloud_size + off0);
+    }
+    for (int k = threadIdx.x; k < nl; k += LT) {
+        float4 p = cloud[off0 + k];
+        X[k] = p.x; Y[k] = p.y; Z[k] = p.z;
+        Cv[k] = gcurv[off0 + k];
+        picked[k] = 0;
+        label[k] = 0;
+    }
+    if (threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    // ---- segment sorts (:282-289): stable rank sort, libstdc++ replica on exact ties ----
+    for (int j = 0; j < 6; j++) {
+        const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
+        const int m = ep - sp + 1, b0 = sp - off0;
+        if (threadIdx.x == 0) s_flag = 0;
+        __syncthreads();
+        int any_tie = 0;
+        for (int a = threadIdx.x; a < m; a += LT) {
+            const float ca = Cv[b0 + a];
+            int rank = 0, ties = 0;
+            for (int b = 0; b < m; b++) {
+                const float cb = Cv[b0 + b];
+                rank += (cb < ca) || (cb == ca && b < a);
+                ties += (cb == ca);
+            }
+            S[b0 + rank] = sp + a;
+            any_tie |= (ties > 1);
+        }
+        if (any_tie) s_flag = 1;
+        __syncthreads();
+        if (s_flag) {
+            if (threadIdx.x == 0) {
+                for (int a = 0; a < m; a++) S[b0 + a] = sp + a;
+                dev_std_sort(S + b0, S + b0 + m, CurvLess{Cv, off0});
+            }
+            __syncthreads();
+        }
+    }
+    // ---- greedy selection, one wave, segments in order (:291-390) ----
+    if (threadIdx.x < WAVE) {
+        const int lane = threadIdx.x;
+        int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+        for (int j = 0; j < 6; j++) {
+            const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
+            int largest = 0;
+            int cur = ep;
+            while (cur >= sp) {
+                const int k = cur - lane;
+                const bool valid = k >= sp;
+                const int ind = valid ? S[k - off0] : sp;
+                const bool elig = valid && picked[ind - off0] == 0 && (double)Cv[ind - off0] > 0.1;
+                const unsigned long long mk = __ballot(elig);
+                if (!mk) { cur -= WAVE; continue; }
+                const int f = __ffsll((long long)mk) - 1;
+                const int indf = __shfl(ind, f, WAVE);
+                largest++;
+                if (largest > 20) break;
+                if (lane == 0) {
+                    if (largest <= 2) {
+                        label[indf - off0] = 2;
+                        line_sharp[line * LINE_SHARP_CAP + n_sharp] = indf;
+                    } else {
+                        label[indf - off0] = 1;
+                    }
+                    line_lsharp[line * LINE_LSHARP_CAP + n_lsharp] = indf;
+                    picked[indf - off0] = 1;
+                    suppress_neighbours(indf - off0, X, Y, Z, picked);
+                }
+                if (largest <= 2) n_sharp++;
+                n_lsharp++;
+                __threadfence_block();
+                cur = cur - f - 1;
+            }
+            int smallest = 0;
+            cur = sp;
+            while (cur <= ep) {
+                const int k = cur + lane;
+                const bool valid = k <= ep;
+                const int ind = valid ? S[k - off0] : sp;
+                const bool elig = valid && picked[ind - off0] == 0 && (double)Cv[ind - off0] < 0.1;
+                const unsigned long long mk = __ballot(elig);
+                if (!mk) { cur += WAVE; continue; }
+                const int f = __ffsll((long long)mk) - 1;
+                const int indf = __shfl(ind, f, WAVE);
+                if (lane == 0) {
+                    label[indf - off0] = -1;
+                    line_flat[line * LINE_FLAT_CAP + n_flat] = indf;
+                }
+                n_flat++;
+                smallest++;
+                if (smallest >= 4) break;
+                if (lane == 0) {
+                    picked[indf - off0] = 1;
+                    suppress_neighbours(indf - off0, X, Y, Z, picked);
+                }
+                __threadfence_block();
+                cur = cur + f + 1;
+            }
+        }
+        if (lane == 0) { s_cnt[0] = n_sharp; s_cnt[1] = n_lsharp; s_cnt[2] = n_flat; }
+    }
+    __syncthreads();
+    // ---- less-flat candidates: label <= 0 in [s, e-1], cloud order (:392-398) ----
+    // compact into S (reused) by a block-wide scan over chunks of LT
+    if (threadIdx.x == 0) s_ncand = 0;
+    __syncthreads();
+    const int lanei = lane_id(), wi = threadIdx.x / WAVE;
+    for (int base = s; base <= e - 1; base += LT) {
+        const int k = base + threadIdx.x;
+        const int flag = (k <= e - 1) && label[k - off0] <= 0;
+        const unsigned long long mk = __ballot(flag);
+        if (lanei == 0) s_wsum[wi] = __popcll(mk);
+        __syncthreads();
+        int before = s_ncand;
+        for (int ww = 0; ww < wi; ww++) before += s_wsum[ww];
+        if (flag) S[before + __popcll(mk & lanemask_lt64())] = k - off0;
+        __syncthreads();
+        if (threadIdx.x == 0) { int t = 0; for (int ww = 0; ww < LT / WAVE; ww++) t += s_wsum[ww]; s_ncand += t; }
+        __syncthreads();
+    }
+    const int nc = s_ncand;
+    // ---- VoxelGrid(0.2) of the candidates (PCL 1.8 applyFilter), points summed in input order ----
+    if (threadIdx.x < 6) s_bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    {
+        unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+        for (int t = threadIdx.x; t < nc; t += LT) {
+            int k = S[t];
+            unsigned v[3] = {f2ord(X[k]), f2ord(Y[k]), f2ord(Z[k])};
+            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+        }
+        for (int d = 0; d < 3; d++) { atomicMin(&s_bb[d], mn[d]); atomicMax(&s_bb[3 + d], mx[d]); }
+    }
+    __syncthreads();
+    const float inv = 1.0f / 0.2f;
+    float minp[3], maxp[3];
+    for (int d = 0; d < 3; d++) { minp[d] = ord2f(s_bb[d]); maxp[d] = ord2f(s_bb[3 + d]); }
+    long long ddx = (long long)((maxp[0] - minp[0]) * inv) + 1;
+    long long ddy = (long long)((maxp[1] - minp[1]) * inv) + 1;
+    long long ddz = (long long)((maxp[2] - minp[2]) * inv) + 1;
+    const bool overflow = ddx * ddy * ddz > 2147483647LL;
+    int minb[3], divb[3];
+    for (int d = 0; d < 3; d++) {
+        minb[d] = (int)floorf(minp[d] * inv);
+        int maxb = (int)floorf(maxp[d] * inv);
+        divb[d] = maxb - minb[d] + 1;
+    }
+    const int mul1 = divb[0], mul2 = divb[0] * divb[1];
+    int n2 = 1;
+    while (n2 < nc) n2 <<= 1;
+    for (int t = threadIdx.x; t < n2; t += LT) {
+        unsigned long long key = ~0ull;
+        if (t < nc) {
+            int k = S[t];
+            unsigned idx;
+            if (overflow) idx = (unsigned)t;   // PCL copies the input through unchanged
+            else {
+                int i0 = (int)(floorf(X[k] * inv) - (float)minb[0]);
+                int i1 = (int)(floorf(Y[k] * inv) - (float)minb[1]);
+                int i2 = (int)(floorf(Z[k] * inv) - (float)minb[2]);
+                idx = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+            }
+            key = ((unsigned long long)idx << 32) | (unsigned)t;
+        }
+        keys[t] = key;
+    }
+    __syncthreads();
+    bitonic_sort_u64(keys, n2);
+    // run heads -> centroids; run r's head position stored in S[nc + r] region? reuse Cv as int
+    int* heads = (int*)Cv;   // curvature no longer needed
+    if (threadIdx.x == 0) s_nrun = 0;
+    __syncthreads();
+    for (int base = 0; base < nc; base += LT) {
+        const int t = base + threadIdx.x;
+        const int flag = t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32));
+        const unsigned long long mk = __ballot(flag);
+        if (lanei == 0) s_wsum[wi] = __popcll(mk);
+        __syncthreads();
+        int before = s_nrun;
+        for (int ww = 0; ww < wi; ww++) before += s_wsum[ww];
+        if (flag) heads[before + __popcll(mk & lanemask_lt64())] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) { int tt = 0; for (int ww = 0; ww < LT / WAVE; ww++) tt += s_wsum[ww]; s_nrun += tt; }
+        __syncthreads();
+    }
+    const int nrun = s_nrun;
+    for (int r = threadIdx.x; r < nrun; r += LT) {
+        const int h0 = heads[r], h1 = (r + 1 < nrun) ? heads[r + 1] : nc;
+        int k = S[(int)(keys[h0] & 0xffffffffu)];
+        float4 c = cloud[off0 + k];
+        for (int t = h0 + 1; t < h1; t++) {
+            float4 p = cloud[off0 + S[(int)(keys[t] & 0xffffffffu)]];
+            c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
+        }
+        const float cnt = (float)(h1 - h0);
+        line_lf[off0 + r] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+    }
+    if (threadIdx.x == 0) {
+        cnt_out[0] = s_cnt[0]; cnt_out[1] = s_cnt[1]; cnt_out[2] = s_cnt[2]; cnt_out[3] = nrun;
+    }
+}
+
+// concatenate per-line outputs in line order (:304-310,356,407)
+__global__ void k_concat(const float4* __restrict__ cloud, const int* line_sharp, const int* line_lsharp,
+                         const int* line_flat, const int* line_cnt, const float4* line_lf, int N_SCANS, ScanMeta* meta,
+                         float4* sharp, int* sharp_idx, float4* lsharp, int* lsharp_idx, float4* flat, int* flat_idx,
+                         float4* lflat) {
+    const int line = blockIdx.x;
+    int o[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
+    for (int l = 0; l < N_SCANS; l++) {
+        for (int c = 0; c < 4; c++) {
+            int v = line_cnt[l * 4 + c];
+            if (l < line) o[c] += v;
+            tot[c] += v;
+        }
+    }
+    const int* lc = line_cnt + line * 4;
+    for (int t = threadIdx.x; t < lc[0]; t += blockDim.x) {
+        int i = line_sharp[line * LINE_SHARP_CAP + t];
+        sharp[o[0] + t] = cloud[i]; sharp_idx[o[0] + t] = i;
+    }
+    for (int t = threadIdx.x; t < lc[1]; t += blockDim.x) {
+        int i = line_lsharp[line * LINE_LSHARP_CAP + t];
+        lsharp[o[1] + t] = cloud[i]; lsharp_idx[o[1] + t] = i;
+    }
+    for (int t = threadIdx.x; t < lc[2]; t += blockDim.x) {
+        int i = line_flat[line * LINE_FLAT_CAP + t];
+        flat[o[2] + t] = cloud[i]; flat_idx[o[2] + t] = i;
+    }
+    const int off0 = meta->line_off[line];
+    for (int t = threadIdx.x; t < lc[3]; t += blockDim.x) lflat[o[3] + t] = line_lf[off0 + t];
+    if (line == 0 && threadIdx.x == 0) {
+        meta->counts[0] = meta->cloud_size;
+        meta->counts[1] = tot[0]; meta->counts[2] = tot[1]; meta->counts[3] = tot[2]; meta->counts[4] = tot[3];
+    }
+}
+
+__global__ void k_meta_init(ScanMeta* m, int n_in) {
+    m->n_in = n_in;
+    m->jstar = 0x7fffffff;
+    m->cloud_size = 0;
+    for (int i = 0; i < 5; i++) m->counts[i] = 0;
+}
+
+// ------------------------------------------------------------------------------------------
+void scan_registration_launch(Ctx& C, const float4* in, int n) {
+    const aloam_params& P = C.P;
+    const int N_SCANS = P.scan_line;
+    hipStream_t st = C.stream;
+    const int nb = (n + SB - 1) / SB;
+    const float thres = (float)P.minimum_range;
+    k_meta_init<<<1, 1, 0, st>>>(C.d_meta, n);
+    if (n > 0) {
+        k_filter_count<<<nb, SB, 0, st>>>(in, n, P.input_is_dense, thres, C.d_blk);
+        k_scan_small<<<1, 1024, 0, st>>>(C.d_blk, nb, &C.d_meta->n_cl);
+        k_filter_scatter<<<nb, SB, 0, st>>>(in, n, P.input_is_dense, thres, C.d_blk, C.d_cl);
+        k_bucket_classify<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, N_SCANS, P.generic_min_elev_deg, P.generic_max_elev_deg,
+                                             C.d_sid, C.d_ori, C.d_hist, nb, C.d_meta);
+        k_bucket_scan<<<1, 1024, 0, st>>>(C.d_hist, nb, N_SCANS, C.d_meta);
+        k_bucket_scatter<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, C.d_sid, C.d_ori, C.d_hist, nb, N_SCANS, C.d_cloud);
+        k_curvature<<<nb, SB, 0, st>>>(C.d_cloud, C.d_meta, C.d_curv);
+        const size_t lds = 128 + (size_t)LINE_LDS_CAP * (4 * 4 + 4 + 8 + 2);
+        k_line_features<<<N_SCANS, LT, lds, st>>>(C.d_cloud, C.d_curv, C.d_meta, N_SCANS, C.d_scratch_xyz,
+                                                  C.d_scratch_keys, C.d_scratch_i, C.d_line_sharp, C.d_line_lsharp,
+                                                  C.d_line_flat, C.d_line_cnt, C.d_line_lf);
+        k_concat<<<N_SCANS, 256, 0, st>>>(C.d_cloud, C.d_line_sharp, C.d_line_lsharp, C.d_line_flat, C.d_line_cnt,
+                                          C.d_line_lf, N_SCANS, C.d_meta, C.d_sharp, C.d_sharp_idx, C.d_lsharp,
+                                          C.d_lsharp_idx, C.d_flat, C.d_flat_idx, C.d_lflat);
+    }
+    HIPCHK(hipGetLastError());
+}
+
+}  // namespace aloam

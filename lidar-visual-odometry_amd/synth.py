@@ -1,0 +1,108 @@
+"""Seeded synthetic lidar sweeps in the KITTI velodyne .bin layout.
+
+The ray caster is C (tools/synth_scan.c -> tools/libaloam_synth.so, built by
+``__graft_entry__.build()``), so a 100k-point HDL-64 sweep takes tens of milliseconds and is
+bit-identical on this container and on the GPU box.
+
+Configs (BASELINE.json ``configs``):
+  * ``vlp16``  — C1: VLP-16, 1,800 azimuths (~29k points)
+  * ``hdl64``  — C2/C3: HDL-64E elevation table of scanRegistration.cpp:189-192, 2,083 azimuths
+                 (~100-125k points after the 5 m minimum range)
+  * ``l128``   — C4: 128 lines uniform -25..+15 deg, 1,875 azimuths (~240k points)
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "tools", "libaloam_synth.so")
+
+
+class SynthConfig(C.Structure):
+    _fields_ = [("model", C.c_int), ("n_azimuth", C.c_int), ("range_sigma", C.c_double),
+                ("max_range", C.c_double), ("seed", C.c_ulonglong), ("speed", C.c_double),
+                ("yaw_amp_deg", C.c_double)]
+
+
+PRESETS = {
+    "vlp16": dict(model=16, n_azimuth=1800, range_sigma=0.02, max_range=100.0, seed=1, speed=1.0, yaw_amp_deg=2.0),
+    "hdl64": dict(model=64, n_azimuth=2083, range_sigma=0.02, max_range=120.0, seed=2, speed=1.0, yaw_amp_deg=2.0),
+    "l128": dict(model=128, n_azimuth=1875, range_sigma=0.02, max_range=120.0, seed=4, speed=1.0, yaw_amp_deg=2.0),
+}
+SCAN_LINES = {"vlp16": 16, "hdl64": 64, "l128": 128}
+
+_lib = None
+
+
+def build_lib(force=False):
+    src = os.path.join(_HERE, "tools", "synth_scan.c")
+    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+        rc = os.system(f"gcc -O2 -ffp-contract=off -fPIC -shared -o {_LIB} {src} -lm")
+        if rc != 0:
+            raise RuntimeError("building libaloam_synth.so failed")
+    return _LIB
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build_lib()
+        _lib = C.CDLL(_LIB)
+        _lib.synth_generate.restype = C.c_int
+        _lib.synth_generate.argtypes = [C.POINTER(SynthConfig), C.c_int, C.POINTER(C.c_float), C.c_int]
+        _lib.synth_pose.restype = None
+        _lib.synth_pose.argtypes = [C.POINTER(SynthConfig), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        _lib.synth_dense_map.restype = C.c_int
+        _lib.synth_dense_map.argtypes = [C.c_ulonglong, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                                         C.POINTER(C.c_float), C.c_int]
+    return _lib
+
+
+def config(name, **over):
+    d = dict(PRESETS[name])
+    d.update(over)
+    return SynthConfig(**d)
+
+
+def scan(name, frame, **over):
+    """One sweep: float32 array (n, 4) of x, y, z, reflectance in the sensor frame."""
+    lib = _load()
+    cfg = config(name, **over)
+    cap = cfg.model * cfg.n_azimuth
+    out = np.empty((cap, 4), np.float32)
+    n = lib.synth_generate(C.byref(cfg), int(frame), out.ctypes.data_as(C.POINTER(C.c_float)), cap)
+    if n < 0:
+        raise RuntimeError("synth capacity")
+    return out[:n].copy()
+
+
+def sequence(name, n_frames, start=0, **over):
+    return [scan(name, start + k, **over) for k in range(n_frames)]
+
+
+def pose(name, frame, **over):
+    """Ground-truth sensor pose (R 3x3, origin 3) of a frame in the scene frame."""
+    lib = _load()
+    cfg = config(name, **over)
+    R = (C.c_double * 9)()
+    o = (C.c_double * 3)()
+    lib.synth_pose(C.byref(cfg), int(frame), R, o)
+    return np.array(R[:]).reshape(3, 3), np.array(o[:])
+
+
+def dense_map(seed, cx, cy, half=50.0, step=0.15, noise=0.01, max_pts=4_000_000):
+    lib = _load()
+    out = np.empty((max_pts, 4), np.float32)
+    n = lib.synth_dense_map(int(seed), cx, cy, half, step, noise, out.ctypes.data_as(C.POINTER(C.c_float)), max_pts)
+    return out[:n].copy()
+
+
+def write_kitti_bin(path, pts):
+    """KITTI velodyne .bin: float32 x, y, z, r (src/kittiHelper.cpp:25-35)."""
+    np.asarray(pts, np.float32).reshape(-1, 4).tofile(path)
+
+
+def read_kitti_bin(path):
+    return np.fromfile(path, dtype=np.float32).reshape(-1, 4)

@@ -1,0 +1,94 @@
+"""The C-ABI boundary: header <-> shared library <-> ctypes mirror (CPU-only checks)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from lvo_amd_loader import abi, lvo
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "aloam_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(aloam_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_python_symbol_list():
+    assert declared_functions() == sorted(lvo.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(lvo.LIB_PATH), "run __graft_entry__.build() first"
+    out = subprocess.check_output(["nm", "-D", "--defined-only", lvo.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [s for s in declared_functions() if s not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_abi_version():
+    L = lvo.lib()
+    assert L.aloam_abi_version() == 1
+
+
+def test_struct_layouts_match_header():
+    # compile a tiny C program against the header and compare sizeof / offsetof with ctypes
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "aloam_hip.h"
+int main(void){
+ printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(aloam_params), sizeof(aloam_cloud), sizeof(aloam_features),
+        sizeof(aloam_lm_summary), sizeof(aloam_odom_result), sizeof(aloam_map_result), sizeof(aloam_factor), sizeof(aloam_timing));
+ printf("%zu %zu %zu\n", offsetof(aloam_odom_result, lm), offsetof(aloam_map_result, lm), offsetof(aloam_factor, b));
+ return 0;}
+'''
+    tmp = os.path.join(REPO, "tests", "_layout_check.c")
+    exe = tmp[:-2]
+    with open(tmp, "w") as f:
+        f.write(prog)
+    try:
+        subprocess.check_call(["gcc", "-I", os.path.join(REPO, "include"), tmp, "-o", exe])
+        line1, line2 = subprocess.check_output([exe], text=True).split("\n")[:2]
+    finally:
+        for p in (tmp, exe):
+            if os.path.exists(p):
+                os.remove(p)
+    sizes = [int(v) for v in line1.split()]
+    assert sizes == [C.sizeof(t) for t in (abi.Params, abi.Cloud, abi.Features, abi.LMSummary, abi.OdomResult,
+                                            abi.MapResult, abi.Factor, abi.Timing)]
+    offs = [int(v) for v in line2.split()]
+    assert offs == [abi.OdomResult.lm.offset, abi.MapResult.lm.offset, abi.Factor.b.offset]
+
+
+def test_default_params_match_python_mirror():
+    L = lvo.lib()
+    for lines in (16, 32, 64, 128):
+        p = abi.Params()
+        L.aloam_default_params(C.byref(p), lines)
+        q = abi.default_params(lines)
+        for name, _ in abi.Params._fields_:
+            assert getattr(p, name) == pytest.approx(getattr(q, name)), (lines, name)
+
+
+def test_no_cpu_fallback_without_gpu():
+    """Without a HIP device the product path must refuse to run (no silent CPU fallback)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(lvo.ALOAMError):
+        lvo.Context(abi.default_params(64))
+    L = lvo.lib()
+    assert L.aloam_create(C.byref(abi.default_params(64)), 0) is None
+    assert b"device" in L.aloam_last_error(None)
+
+
+def test_null_context_is_an_argument_error():
+    L = lvo.lib()
+    assert L.aloam_odometry(None, None) == abi.ALOAM_E_ARG
+    assert L.aloam_scan_registration(None, None, 0, 0) == abi.ALOAM_E_ARG
