@@ -54,7 +54,7 @@ static void allocate(Ctx& C) {
     C.d_cl = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_sid = (int*)dalloc(C, sizeof(int) * N);
     C.d_ori = (float*)dalloc(C, sizeof(float) * N);
-    C.d_blk = (int*)dalloc(C, sizeof(int) * (nb + 4096));
+    C.d_blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, std::max(P.max_map_points, 1024) / 256 + 1) + 4096));
     C.d_hist = (int*)dalloc(C, sizeof(int) * (size_t)MAXL * nb);
     C.d_cloud = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_curv = (float*)dalloc(C, sizeof(float) * N);
@@ -84,8 +84,8 @@ static void allocate(Ctx& C) {
     C.h_odom.para[3] = 1.0;
     C.h_odom.q_w[3] = 1.0;
     HIPCHK(hipMemcpy(C.d_odom, &C.h_odom, sizeof(OdomState), hipMemcpyHostToDevice));
-    grid_alloc(C, C.g_corner_last, capLS, 2.0f * 5.0f * 1.025f);
-    grid_alloc(C, C.g_surf_last, N, 2.0f * 5.0f * 1.025f);
+    grid_alloc(C, C.g_corner_last, capLS, 2.5f * 1.025f);   // two-phase 1-NN, k_odom.hip
+    grid_alloc(C, C.g_surf_last, N, 2.5f * 1.025f);
     C.cap_factors = capLS + N;
     C.d_factors = (aloam_factor*)dalloc(C, sizeof(aloam_factor) * C.cap_factors);
     C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);
@@ -110,12 +110,12 @@ static void allocate(Ctx& C) {
     C.d_mc2_cube = (int*)dalloc(C, sizeof(int) * M);
     C.d_ms2_cube = (int*)dalloc(C, sizeof(int) * M);
     C.d_map_tmp = (float4*)dalloc(C, sizeof(float4) * M);
-    C.d_seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 4 * (size_t)M);
+    C.d_seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (4 * (size_t)M + 32768));
     C.d_map_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_cube_cnt = (int*)dalloc(C, sizeof(int) * 2 * 7 * (CUBE_N + 1));
     C.d_cube_valid = (unsigned char*)dalloc(C, CUBE_N);
-    grid_alloc(C, C.g_map_corner, M, 2.0f * 1.0f * 1.025f);
-    grid_alloc(C, C.g_map_surf, M, 2.0f * 1.0f * 1.025f);
+    grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f);     // 5-NN within 1 m, 3x3x3 cells
+    grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f);
     C.d_map_corner_in = (float4*)dalloc(C, sizeof(float4) * capLS);
     C.d_map_surf_in = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_map_full_in = (float4*)dalloc(C, sizeof(float4) * N);
@@ -130,7 +130,7 @@ static void allocate(Ctx& C) {
     C.d_vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
     C.d_vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     C.d_vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
-    C.sort_tmp_bytes = voxel_sort_tmp_bytes(C.cap_voxel) + 1024;
+    C.sort_tmp_bytes = std::max(voxel_sort_tmp_bytes(C.cap_voxel), cube_sort_tmp_bytes(C.cap_map)) + 1024;
     C.d_sort_tmp = dalloc(C, C.sort_tmp_bytes);
     C.d_ins_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_voxel);
     C.d_ins_val = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
@@ -176,6 +176,7 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     if (C.profiling) C.timing.scan_registration_ms = ev_ms(C, 0, 1);
     C.have_features = true;
     C.features_from_host = false;
+    C.features_swapped = false;
 }
 
 static void do_odometry(Ctx& C, aloam_odom_result* R) {
@@ -203,6 +204,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     // the current less-sharp / less-flat become the last clouds (:627-641)
     std::swap(C.d_lsharp, C.d_corner_last);
     std::swap(C.d_lflat, C.d_surf_last);
+    C.features_swapped = true;
     C.n_corner_last = C.n_lsharp;
     C.n_surf_last = C.n_lflat;
     set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);
@@ -406,13 +408,14 @@ int aloam_get_features(aloam_ctx* ctx, aloam_features* o) {
     API_BEGIN(ctx)
     if (!o) throw ApiError{ALOAM_E_ARG, "null features"};
     if (!C.have_features) throw ApiError{ALOAM_E_STATE, "no features yet"};
-    const bool swapped = false;
-    (void)swapped;
+    // after aloam_odometry the current less-sharp / less-flat clouds live in the last-cloud slots
+    const float4* lsharp = C.features_swapped ? C.d_corner_last : C.d_lsharp;
+    const float4* lflat = C.features_swapped ? C.d_surf_last : C.d_lflat;
     d2h_cloud(C, C.d_cloud, C.features_from_host ? 0 : C.n_full, &o->full);
     d2h_cloud(C, C.d_sharp, C.n_sharp, &o->sharp);
-    d2h_cloud(C, C.d_lsharp, C.n_lsharp, &o->less_sharp);
+    d2h_cloud(C, lsharp, C.n_lsharp, &o->less_sharp);
     d2h_cloud(C, C.d_flat, C.n_flat, &o->flat);
-    d2h_cloud(C, C.d_lflat, C.n_lflat, &o->less_flat);
+    d2h_cloud(C, lflat, C.n_lflat, &o->less_flat);
     if (o->sharp_idx && C.n_sharp) HIPCHK(hipMemcpyAsync(o->sharp_idx, C.d_sharp_idx, sizeof(int) * C.n_sharp, hipMemcpyDeviceToHost, C.stream));
     if (o->less_sharp_idx && C.n_lsharp) HIPCHK(hipMemcpyAsync(o->less_sharp_idx, C.d_lsharp_idx, sizeof(int) * C.n_lsharp, hipMemcpyDeviceToHost, C.stream));
     if (o->flat_idx && C.n_flat) HIPCHK(hipMemcpyAsync(o->flat_idx, C.d_flat_idx, sizeof(int) * C.n_flat, hipMemcpyDeviceToHost, C.stream));
@@ -435,6 +438,7 @@ int aloam_set_features(aloam_ctx* ctx, const float* sharp, int ns, const float* 
     C.n_sharp = ns; C.n_lsharp = nls; C.n_flat = nf; C.n_lflat = nlf; C.n_full = 0;
     C.have_features = true;
     C.features_from_host = true;
+    C.features_swapped = false;
     API_END
 }
 
@@ -596,7 +600,7 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
     if (nq) HIPCHK(hipMemcpyAsync(C.d_cl, queries, sizeof(float4) * nq, hipMemcpyHostToDevice, C.stream));
     set_counts2(C, C.d_map_in_n, n, 0);
     Grid g = C.g_surf_last;      // borrow the odometry surf grid's storage with the requested radius
-    g.min_cell = 2.0f * radius * 1.025f;
+    g.min_cell = radius * 1.025f;
     grid_build(C, g, C.d_in, C.d_map_in_n, std::max(n, 1), nullptr, nullptr);
     int* d_idx = (int*)C.d_scratch_i;
     float* d_d2 = (float*)(C.d_scratch_i + (size_t)nq * k);

@@ -42,21 +42,16 @@ __host__ __device__ inline dquat qinv(const dquat& q) {
     if (n2 > 0) return {-q.x / n2, -q.y / n2, -q.z / n2, q.w / n2};
     return {0, 0, 0, 0};
 }
-// Identity().slerp(t, q) (Quaternion.h:726-754)
+// Identity().slerp(t, q) (Quaternion.h:726-754) at t = 1, the only value on the hot path
+// (DISTORTION 0 => s = 1, laserOdometry.cpp:67,158-161; lidarFactor.hpp:29,81 get s = 1).
+// With t = 1 Eigen computes scale0 = sin(0*theta)/sin(theta) = +0 and scale1 = sin(theta)/sin(theta)
+// = 1 exactly (same bits divided by themselves; the |d| >= 1-eps branch gives 0 and 1 directly), so
+// the result is exactly sign(w) * q: the acos/sin evaluations are skipped without changing a bit
+// (up to the sign of a zero component, which no later operation can observe).
 __device__ inline dquat qslerp_identity(double t, const dquat& q) {
-    const double one = 1.0 - 2.220446049250313e-16;
-    double d = q.w;
-    double absD = fabs(d);
-    double s0, s1;
-    if (absD >= one) { s0 = 1.0 - t; s1 = t; }
-    else {
-        double theta = acos(absD);
-        double sinTheta = sin(theta);
-        s0 = sin((1.0 - t) * theta) / sinTheta;
-        s1 = sin(t * theta) / sinTheta;
-    }
-    if (d < 0) s1 = -s1;
-    return {s0 * 0.0 + s1 * q.x, s0 * 0.0 + s1 * q.y, s0 * 0.0 + s1 * q.z, s0 * 1.0 + s1 * q.w};
+    (void)t;
+    if (q.w < 0) return {-q.x, -q.y, -q.z, -q.w};
+    return q;
 }
 
 // ---- wave64 helpers ------------------------------------------------------------------
@@ -117,4 +112,138 @@ __device__ inline float sqdist(float ax, float ay, float az, float bx, float by,
     return dx * dx + dy * dy + dz * dz;
 }
 
+}  // namespace aloam
+
+namespace aloam {
+// ---- grid neighbourhood as contiguous x-rows --------------------------------------------------
+// Points are sorted by cell id c = (z*dy + y)*dx + x, so the cells [x0, x1] of one (y, z) row are one
+// contiguous point range. A (2m+1)^3 neighbourhood of the query's cell is (2m+1)^2 ranges, flattened
+// so all 64 lanes of a wave stream candidates regardless of how the points spread over the rows.
+template <int MAXR>
+struct RowSet {
+    int b[MAXR];
+    int pre[MAXR + 1];
+    int nr;
+};
+// rs lives in LDS, one per wave: every lane writes the same (wave-uniform) values.
+template <int MAXR>
+__device__ __forceinline__ int build_rows(const float ox, const float oy, const float oz, const float inv_cell,
+                                          const int gdx, const int gdy, const int gdz, const int* __restrict__ start,
+                                          float qx, float qy, float qz, int m, RowSet<MAXR>& rs) {
+    __builtin_amdgcn_wave_barrier();
+    const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
+    const int x0 = max(cx - m, 0), x1 = min(cx + m, gdx - 1);
+    int total = 0, nr = 0;
+    rs.pre[0] = 0;
+    if (x0 <= x1) {
+        for (int z = max(cz - m, 0); z <= min(cz + m, gdz - 1); z++)
+            for (int y = max(cy - m, 0); y <= min(cy + m, gdy - 1); y++) {
+                const int c = (z * gdy + y) * gdx;
+                const int b = start[c + x0], e = start[c + x1 + 1];
+                if (e > b && nr < MAXR) {
+                    rs.b[nr] = b;
+                    total += e - b;
+                    rs.pre[++nr] = total;
+                }
+            }
+    }
+    rs.nr = nr;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return total;
+}
+// flattened candidate t -> point position
+template <int MAXR>
+__device__ __forceinline__ int row_pos(const RowSet<MAXR>& rs, int t) {
+    int r = 0;
+    while (r + 1 < rs.nr && rs.pre[r + 1] <= t) r++;
+    return rs.b[r] + (t - rs.pre[r]);
+}
+}  // namespace aloam
+
+namespace aloam {
+// Exact radius k-NN of one query by one wave over the (2m+1)^3 cell neighbourhood: every lane keeps a
+// sorted top-K of the candidates it streams (4 loads in flight), then K rounds of a 64-bit wave-min
+// over the lanes' heads merge them. Keys (d2 bits, index) order equal distances by point index.
+// Returns the number found (<= K); out_pos = positions in the grid's sorted arrays.
+template <int K, int MAXR>
+__device__ __forceinline__ int wave_knn_rows(const float ox, const float oy, const float oz, const float inv_cell,
+                                             const int gdx, const int gdy, const int gdz,
+                                             const int* __restrict__ start, const float4* __restrict__ spts,
+                                             const int* __restrict__ sidx, float qx, float qy, float qz, float r2, int m,
+                                             int* out_pos, float* out_d2, int* out_idx, int* ncand, RowSet<MAXR>& rs) {
+    const int lane = lane_id();
+    const int total = build_rows<MAXR>(ox, oy, oz, inv_cell, gdx, gdy, gdz, start, qx, qy, qz, m, rs);
+    if (ncand) *ncand = total;
+    float bd[K];
+    int bi[K], bp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
+        int pp[4];
+        float4 vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = t0 + u * WAVE + lane;
+            pp[u] = t < total ? row_pos<MAXR>(rs, t) : -1;
+            vv[u] = pp[u] >= 0 ? spts[pp[u]] : make_float4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (pp[u] < 0) continue;
+            const float d2 = sqdist(vv[u].x, vv[u].y, vv[u].z, qx, qy, qz);
+            if (!(d2 < r2)) continue;
+            const int id = sidx[pp[u]];
+            if (d2 < bd[K - 1] || (d2 == bd[K - 1] && id < bi[K - 1])) {
+                float nd = d2; int ni = id, np = pp[u];
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                    if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
+                }
+            }
+        }
+    }
+    int head = 0, found = 0;
+    for (int k = 0; k < K; k++) {
+        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
+#pragma unroll
+        for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
+        const unsigned long long key = hp < 0 ? ~0ull : dist_key(hd, hi);
+        const unsigned long long mn = wave_min_u64(key);
+        if (mn == ~0ull) break;
+        const unsigned long long won = __ballot(key == mn);
+        if (key == mn) head++;
+        out_pos[k] = __shfl(hp, __ffsll((long long)won) - 1, WAVE);
+        out_d2[k] = __uint_as_float((unsigned)(mn >> 32));
+        out_idx[k] = (int)(mn & 0xffffffffu);
+        found++;
+    }
+    return found;
+}
+// PCL 1.8 VoxelGrid leaf grid from an ordered-int bbox (voxel_grid.cpp applyFilter)
+__device__ inline void voxel_params(const unsigned* bb, float leaf, bool* overflow, int minb[3], int* mul1, int* mul2) {
+    const float inv = 1.0f / leaf;
+    float mn[3], mx[3];
+    for (int a = 0; a < 3; a++) { mn[a] = ord2f(bb[a]); mx[a] = ord2f(bb[3 + a]); }
+    long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
+    long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
+    long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
+    *overflow = dx * dy * dz > 2147483647LL;
+    int divb[3];
+    for (int a = 0; a < 3; a++) {
+        minb[a] = (int)floorf(mn[a] * inv);
+        int maxb = (int)floorf(mx[a] * inv);
+        divb[a] = maxb - minb[a] + 1;
+    }
+    *mul1 = divb[0];
+    *mul2 = divb[0] * divb[1];
+}
+__device__ inline unsigned voxel_index(float4 p, float inv, const int minb[3], int mul1, int mul2) {
+    int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+    int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+    int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+    return (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+}
 }  // namespace aloam

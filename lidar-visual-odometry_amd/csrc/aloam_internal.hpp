@@ -16,7 +16,7 @@ constexpr int LINE_LSHARP_CAP = 120; // 20 per segment x 6  (:307)
 constexpr int LINE_FLAT_CAP = 24;    // 4 per segment x 6   (:359)
 constexpr int LINE_LDS_CAP = 4096;   // points per line kept in LDS (larger lines use global scratch)
 constexpr int CUBE_W = 21, CUBE_H = 21, CUBE_D = 11, CUBE_N = 21 * 21 * 11;  // laserMapping.cpp:74-82
-constexpr int GRID_MAX_CELLS = 1 << 22;
+constexpr int GRID_MAX_CELLS = 1 << 23;
 
 // ---- device-resident bookkeeping of scanRegistration ----
 struct ScanMeta {
@@ -112,6 +112,7 @@ struct Ctx {
     int n_full = 0, n_sharp = 0, n_lsharp = 0, n_flat = 0, n_lflat = 0;
     bool have_features = false;
     bool features_from_host = false;
+    bool features_swapped = false;     // odometry moved less_sharp/less_flat into the last-cloud slots
 
     // ---- laserOdometry ----
     bool odom_inited = false;
@@ -198,6 +199,7 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
 void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq);
 void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2);
 size_t voxel_sort_tmp_bytes(int cap);
+size_t cube_sort_tmp_bytes(int cap);
 void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout);
 void map_frame_launch(Ctx& C, aloam_map_result* R);
 void* dalloc(Ctx& C, size_t bytes);

@@ -2,10 +2,10 @@
 //
 // The reference accepts a neighbour only inside a fixed radius: 1-NN with d^2 < 25 in odometry
 // (src/laserOdometry.cpp:386-389,470-473) and 5-NN with d^2[4] < 1 in mapping
-// (src/laserMapping.cpp:582-584,648-650). So an exact radius-r k-NN over a grid with cells of edge
-// >= 2r returns FLANN's answer: a query's r-ball overlaps at most 2 cells per axis (8 cells), chosen
-// by which half of its cell it lies in. Distances are fp32 ((dx^2 + dy^2) + dz^2) like FLANN's
-// L2_Simple<float>; equal distances are ordered by point index.
+// (src/laserMapping.cpp:582-584,648-650). So an exact radius-r k-NN over a grid returns FLANN's
+// answer as long as the searched cell block contains the r-ball: with cells of edge >= r the query
+// cell's 3x3x3 block does (wave_knn_rows in aloam_device.hpp). Distances are fp32
+// ((dx^2 + dy^2) + dz^2) like FLANN's L2_Simple<float>; equal distances are ordered by point index.
 //
 // Build = counting sort by cell: bbox (ordered-int atomics) -> per-cell counts -> exclusive scan ->
 // scatter (atomic decrement, which leaves the count array zeroed for the next build).
@@ -120,8 +120,10 @@ __global__ void k_grid_scan1(const int* __restrict__ cnt, const GridDesc* d, int
 __global__ void k_grid_scan2(int* blk, const GridDesc* d) {
     __shared__ int sh[1024];
     const int nb = (d->ncells + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    // nb <= GRID_MAX_CELLS / SCAN_CHUNK = 1024
-    int v = threadIdx.x < nb ? blk[threadIdx.x] : 0;
+    // nb <= GRID_MAX_CELLS / SCAN_CHUNK = 2048: two entries per thread
+    const int i0 = 2 * threadIdx.x, i1 = i0 + 1;
+    const int v0 = i0 < nb ? blk[i0] : 0, v1 = i1 < nb ? blk[i1] : 0;
+    const int v = v0 + v1;
     sh[threadIdx.x] = v;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
@@ -130,7 +132,9 @@ __global__ void k_grid_scan2(int* blk, const GridDesc* d) {
         sh[threadIdx.x] += t;
         __syncthreads();
     }
-    if (threadIdx.x < nb) blk[threadIdx.x] = sh[threadIdx.x] - v;
+    const int ex = sh[threadIdx.x] - v;
+    if (i0 < nb) blk[i0] = ex;
+    if (i1 < nb) blk[i1] = ex + v0;
 }
 __global__ void k_grid_scan3(const int* __restrict__ cnt, const GridDesc* d, const int* blk, int* start) {
     __shared__ int sh[SCAN_CHUNK];
@@ -182,7 +186,7 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell) {
     g.desc = (GridDesc*)dalloc(C, sizeof(GridDesc));
     g.cell_count = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
     g.cell_start = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
-    g.blk = (int*)dalloc(C, sizeof(int) * 1024);
+    g.blk = (int*)dalloc(C, sizeof(int) * 2048);
     g.pts = (float4*)dalloc(C, sizeof(float4) * cap);
     g.idx = (int*)dalloc(C, sizeof(int) * cap);
     g.pcell = (int*)dalloc(C, sizeof(int) * cap);
@@ -204,76 +208,18 @@ void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, c
 }
 
 // ------------------------------------------------------------------------------------------
-// k-NN of one query by one wave: 8 cells, per-lane sorted top-K, K-round wave merge.
-template <int K>
-__device__ inline int wave_knn(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
-                               const int* __restrict__ sidx, float qx, float qy, float qz, float r2,
-                               int* out_pos, float* out_d2, int* out_idx) {
-    const int lane = lane_id();
-    float bd[K];
-    int bi[K], bp[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
-    float fx = (qx - gd.ox) * gd.inv_cell, fy = (qy - gd.oy) * gd.inv_cell, fz = (qz - gd.oz) * gd.inv_cell;
-    int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-    int x0 = (fx - cx < 0.5f) ? cx - 1 : cx, y0 = (fy - cy < 0.5f) ? cy - 1 : cy, z0 = (fz - cz < 0.5f) ? cz - 1 : cz;
-    for (int c8 = 0; c8 < 8; c8++) {
-        int x = x0 + (c8 & 1), y = y0 + ((c8 >> 1) & 1), z = z0 + (c8 >> 2);
-        if (x < 0 || y < 0 || z < 0 || x >= gd.dx || y >= gd.dy || z >= gd.dz) continue;
-        int c = (z * gd.dy + y) * gd.dx + x;
-        int b = start[c], e = start[c + 1];
-        for (int p = b + lane; p < e; p += WAVE) {
-            float4 v = spts[p];
-            float d2 = sqdist(v.x, v.y, v.z, qx, qy, qz);
-            if (!(d2 < r2)) continue;
-            int id = sidx[p];
-            if (d2 < bd[K - 1] || (d2 == bd[K - 1] && id < bi[K - 1])) {
-                // sorted insertion
-                float nd = d2; int ni = id, np = p;
-#pragma unroll
-                for (int k = 0; k < K; k++) {
-                    bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
-                    if (lt) {
-                        float td = bd[k]; int ti = bi[k], tp = bp[k];
-                        bd[k] = nd; bi[k] = ni; bp[k] = np;
-                        nd = td; ni = ti; np = tp;
-                    }
-                }
-            }
-        }
-    }
-    // merge: K rounds of wave argmin over the lanes' heads
-    int head = 0, found = 0;
-    for (int k = 0; k < K; k++) {
-        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
-#pragma unroll
-        for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
-        unsigned long long key = (hp < 0) ? ~0ull : dist_key(hd, hi);
-        unsigned long long mn = wave_min_u64(key);
-        if (mn == ~0ull) break;
-        if (key == mn) head++;
-        int win_pos = __shfl(hp, __ffsll((long long)__ballot(key == mn)) - 1, WAVE);
-        if (lane == 0) {
-            out_pos[k] = win_pos;
-            out_d2[k] = __uint_as_float((unsigned)(mn >> 32));
-            out_idx[k] = (int)(mn & 0xffffffffu);
-        }
-        found++;
-    }
-    return found;
-}
-
-template <int K>
+// aloam_knn(): exact radius k-NN (k <= 8) over a grid whose cells are >= the radius (27 cells).
 __global__ void k_knn(const GridDesc* __restrict__ gdp, const int* __restrict__ start, const float4* __restrict__ spts,
                       const int* __restrict__ sidx, const float4* __restrict__ q, int nq, int k, float r2, int* idx, float* d2) {
+    __shared__ RowSet<9> rows9[256 / WAVE];
     const int wq = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (wq >= nq) return;
     const GridDesc gd = *gdp;
-    int pos[K], oi[K];
-    float od[K];
-    for (int j = 0; j < K; j++) { pos[j] = -1; oi[j] = -1; od[j] = INFINITY; }
-    float4 qq = q[wq];
-    int f = wave_knn<K>(gd, start, spts, sidx, qq.x, qq.y, qq.z, r2, pos, od, oi);
+    int pos[8], oi[8];
+    float od[8];
+    const float4 qq = q[wq];
+    const int f = wave_knn_rows<8, 9>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, spts, sidx,
+                                       qq.x, qq.y, qq.z, r2, 1, pos, od, oi, nullptr, rows9[threadIdx.x / WAVE]);
     if (lane_id() == 0)
         for (int j = 0; j < k; j++) {
             idx[wq * k + j] = j < f ? oi[j] : -1;
@@ -285,7 +231,7 @@ void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, i
     const int threads = 256, per_block = threads / WAVE;
     const int nbk = (nq + per_block - 1) / per_block;
     const float r2 = radius * radius;
-    if (nbk > 0) k_knn<8><<<nbk, threads, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2);
+    if (nbk > 0) k_knn<<<nbk, threads, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2);
     HIPCHK(hipGetLastError());
 }
 

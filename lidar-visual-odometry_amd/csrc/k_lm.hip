@@ -21,7 +21,7 @@ constexpr int NACC = 29;         // 21 JtJ + 6 Jtr + cost + residual-block count
 constexpr int LM_MAX_BLOCKS = 512;
 
 // residual and 6-column tangent Jacobian of one factor at (q, t). Returns #residuals (0 = invalid).
-__device__ inline int eval_factor(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
+__device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
     if (f.type < 0) return 0;
     const dvec3 cp{f.cp[0], f.cp[1], f.cp[2]};
     dvec3 pr, lp;
@@ -40,15 +40,20 @@ __device__ inline int eval_factor(const aloam_factor& f, const dquat& q, const d
         const dvec3 w{a.x - b.x, a.y - b.y, a.z - b.z};
         const double n = sqrt(w.x * w.x + w.y * w.y + w.z * w.z);
         r[0] = nu.x / n; r[1] = nu.y / n; r[2] = nu.z / n;
-        // d nu = dlp x w ; dlp/d(theta_k) = -2 (pr x e_k) ; dlp/dt_k = e_k
-        for (int k = 0; k < 3; k++) {
-            dvec3 e{k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
-            dvec3 pe = dcross(pr, e);
-            dvec3 dlp{-2.0 * pe.x, -2.0 * pe.y, -2.0 * pe.z};
-            dvec3 cr = dcross(dlp, w), ct = dcross(e, w);
-            J[0][k] = cr.x / n; J[1][k] = cr.y / n; J[2][k] = cr.z / n;
-            J[0][3 + k] = ct.x / n; J[1][3 + k] = ct.y / n; J[2][3 + k] = ct.z / n;
+        // d nu = dlp x w, dlp/dtheta_k = -2 pr x e_k, dlp/dt_k = e_k:
+        //   J_rot[i][k] = (2 pr_i w_k - 2 (pr.w) delta_ik) / n ,  J_t[i][k] = (e_k x w)_i / n
+        const double inv = 1.0 / n;
+        const double pw2 = 2.0 * (pr.x * w.x + pr.y * w.y + pr.z * w.z);
+        const double prv[3] = {pr.x, pr.y, pr.z}, wv[3] = {w.x, w.y, w.z};
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) J[i][k] = (2.0 * prv[i] * wv[k] - (i == k ? pw2 : 0.0)) * inv;
         }
+        // e_k x w: e_x x w = (0, -w.z, w.y), e_y x w = (w.z, 0, -w.x), e_z x w = (-w.y, w.x, 0)
+        J[0][3] = 0.0;         J[0][4] = w.z * inv;  J[0][5] = -w.y * inv;
+        J[1][3] = -w.z * inv;  J[1][4] = 0.0;        J[1][5] = w.x * inv;
+        J[2][3] = w.y * inv;   J[2][4] = -w.x * inv; J[2][5] = 0.0;
         return 3;
     }
     if (f.type == 1 || f.type == 2) {
@@ -65,14 +70,15 @@ __device__ inline int eval_factor(const aloam_factor& f, const dquat& q, const d
         J[0][3] = nrm.x; J[0][4] = nrm.y; J[0][5] = nrm.z;
         return 1;
     }
-    // LidarDistanceFactor (lidarFactor.hpp:147-161)
+    // LidarDistanceFactor (lidarFactor.hpp:147-161): J_rot = -2 [pr]x, J_t = I
     r[0] = lp.x - f.a[0]; r[1] = lp.y - f.a[1]; r[2] = lp.z - f.a[2];
-    for (int k = 0; k < 3; k++) {
-        dvec3 e{k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
-        dvec3 pe = dcross(pr, e);
-        J[0][k] = -2.0 * pe.x; J[1][k] = -2.0 * pe.y; J[2][k] = -2.0 * pe.z;
-        for (int i = 0; i < 3; i++) J[i][3 + k] = (i == k) ? 1.0 : 0.0;
-    }
+    J[0][0] = 0.0;           J[0][1] = 2.0 * pr.z;   J[0][2] = -2.0 * pr.y;
+    J[1][0] = -2.0 * pr.z;   J[1][1] = 0.0;          J[1][2] = 2.0 * pr.x;
+    J[2][0] = 2.0 * pr.y;    J[2][1] = -2.0 * pr.x;  J[2][2] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) J[i][3 + k] = (i == k) ? 1.0 : 0.0;
     return 3;
 }
 
@@ -88,29 +94,43 @@ __device__ inline double huber_scale(double s, double* rho0) {
     return 1.0;
 }
 
-__device__ inline void accumulate(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
+__device__ __forceinline__ void add_row(const double* J, double r, double sc, double* acc) {
+    double Ji[6];
+#pragma unroll
+    for (int c = 0; c < 6; c++) Ji[c] = J[c] * sc;
+    const double ri = r * sc;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+        for (int b = a; b < 6; b++) acc[k++] += Ji[a] * Ji[b];
+#pragma unroll
+    for (int a = 0; a < 6; a++) acc[21 + a] += Ji[a] * ri;
+}
+
+__device__ __forceinline__ void accumulate(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
     double r[3], J[3][6];
     const int m = eval_factor(f, q, t, r, J);
     if (!m) return;
-    double sq = 0;
-    for (int i = 0; i < m; i++) sq += r[i] * r[i];
-    double rho0;
-    const double sc = huber_scale(sq, &rho0);
+    double rho0, sc;
+    if (m == 1) {
+        sc = huber_scale(r[0] * r[0], &rho0);
+        add_row(J[0], r[0], sc, acc);
+    } else {
+        double sq = r[0] * r[0];
+        sq += r[1] * r[1];
+        sq += r[2] * r[2];
+        sc = huber_scale(sq, &rho0);
+        add_row(J[0], r[0], sc, acc);
+        add_row(J[1], r[1], sc, acc);
+        add_row(J[2], r[2], sc, acc);
+    }
     acc[27] += 0.5 * rho0;
     acc[28] += 1.0;
-    for (int i = 0; i < m; i++) {
-        double Ji[6];
-        for (int c = 0; c < 6; c++) Ji[c] = J[i][c] * sc;
-        const double ri = r[i] * sc;
-        int k = 0;
-        for (int a = 0; a < 6; a++)
-            for (int b = a; b < 6; b++) acc[k++] += Ji[a] * Ji[b];
-        for (int a = 0; a < 6; a++) acc[21 + a] += Ji[a] * ri;
-    }
 }
 
 // ---- host-side-free LM math (thread 0 of the last workgroup) -------------------------------
-__device__ inline void plus7(const double* x, const double* d, double* out) {
+__device__ __forceinline__ void plus7(const double* x, const double* d, double* out) {
     const double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
     dquat q{x[0], x[1], x[2], x[3]};
     if (nd > 0.0) {
@@ -119,42 +139,68 @@ __device__ inline void plus7(const double* x, const double* d, double* out) {
         dquat r = qmul(dq, q);
         out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
     } else { out[0] = q.x; out[1] = q.y; out[2] = q.z; out[3] = q.w; }
+#pragma unroll
     for (int i = 0; i < 3; i++) out[4 + i] = x[4 + i] + d[3 + i];
 }
-__device__ inline double norm7(const double* a) { double s = 0; for (int i = 0; i < 7; i++) s += a[i] * a[i]; return sqrt(s); }
-__device__ inline double grad_max_norm(const double* x, const double* g) {
+__device__ __forceinline__ double norm7(const double* a) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) s += a[i] * a[i];
+    return sqrt(s);
+}
+__device__ __forceinline__ double grad_max_norm(const double* x, const double* g) {
     double ng[6], xp[7];
+#pragma unroll
     for (int i = 0; i < 6; i++) ng[i] = -g[i];
     plus7(x, ng, xp);
     double m = 0;
+#pragma unroll
     for (int i = 0; i < 7; i++) m = fmax(m, fabs(x[i] - xp[i]));
     return m;
 }
-__device__ inline double Aget(const double* A, int a, int b) {   // upper-triangle packed
+__device__ __forceinline__ double Aget(const double* A, int a, int b) {   // upper-triangle packed
     if (a > b) { int t = a; a = b; b = t; }
     return A[a * 6 - a * (a - 1) / 2 + (b - a)];
 }
-__device__ inline bool chol_solve6(double M[6][6], const double* rhs, double* y) {
-    double L[6][6] = {};
+__device__ __forceinline__ bool chol_solve6(double M[6][6], const double* rhs, double* y) {
+    double L[6][6];
+    bool ok = true;
+#pragma unroll
     for (int j = 0; j < 6; j++) {
         double s = M[j][j];
+#pragma unroll
         for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
-        if (!(s > 0.0)) return false;
+        ok = ok && (s > 0.0);
         L[j][j] = sqrt(s);
+#pragma unroll
         for (int i = j + 1; i < 6; i++) {
             double v = M[i][j];
+#pragma unroll
             for (int k = 0; k < j; k++) v -= L[i][k] * L[j][k];
             L[i][j] = v / L[j][j];
         }
     }
     double z[6];
-    for (int i = 0; i < 6; i++) { double v = rhs[i]; for (int k = 0; k < i; k++) v -= L[i][k] * z[k]; z[i] = v / L[i][i]; }
-    for (int i = 5; i >= 0; i--) { double v = z[i]; for (int k = i + 1; k < 6; k++) v -= L[k][i] * y[k]; y[i] = v / L[i][i]; }
-    for (int i = 0; i < 6; i++) if (!isfinite(y[i])) return false;
-    return true;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double v = rhs[i];
+#pragma unroll
+        for (int k = 0; k < i; k++) v -= L[i][k] * z[k];
+        z[i] = v / L[i][i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        double v = z[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) v -= L[k][i] * y[k];
+        y[i] = v / L[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) ok = ok && isfinite(y[i]);
+    return ok;
 }
 
-__device__ void lm_finish(LMState* st, aloam_lm_summary* out, int term) {
+__device__ __forceinline__ void lm_finish(LMState* st, aloam_lm_summary* out, int term) {
     st->done = 1;
     st->termination = term;
     if (out) {
@@ -168,19 +214,24 @@ __device__ void lm_finish(LMState* st, aloam_lm_summary* out, int term) {
 }
 
 // LevenbergMarquardtStrategy::ComputeStep + model cost change; loops over invalid steps.
-__device__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
+__device__ __forceinline__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
     while (true) {
         if (st->iteration >= max_iter) { lm_finish(st, out, 0); return; }
         st->iteration++;
         double As[6][6], gs[6];
+        #pragma unroll
         for (int a = 0; a < 6; a++) {
             gs[a] = st->scale[a] * st->g[a];
+            #pragma unroll
             for (int b = 0; b < 6; b++) As[a][b] = st->scale[a] * Aget(st->A, a, b) * st->scale[b];
         }
         if (!st->reuse_diag)
+            #pragma unroll
             for (int a = 0; a < 6; a++) st->diag[a] = fmin(fmax(As[a][a], 1e-6), 1e32);
         double M[6][6];
+        #pragma unroll
         for (int a = 0; a < 6; a++) {
+            #pragma unroll
             for (int b = 0; b < 6; b++) M[a][b] = As[a][b];
             const double D = sqrt(st->diag[a] / st->radius);
             M[a][a] += D * D;
@@ -190,11 +241,14 @@ __device__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
         st->reuse_diag = 1;
         double step[6], mcc = -1.0;
         if (ok) {
+            #pragma unroll
             for (int a = 0; a < 6; a++) step[a] = -y[a];
             double sg = 0, sAs = 0;
+            #pragma unroll
             for (int a = 0; a < 6; a++) {
                 sg += step[a] * gs[a];
                 double t = 0;
+                #pragma unroll
                 for (int b = 0; b < 6; b++) t += As[a][b] * step[b];
                 sAs += step[a] * t;
             }
@@ -207,9 +261,11 @@ __device__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
             continue;
         }
         double delta[6];
+        #pragma unroll
         for (int a = 0; a < 6; a++) delta[a] = step[a] * st->scale[a];
         plus7(st->x, delta, st->cand);
         double dx[7];
+        #pragma unroll
         for (int i = 0; i < 7; i++) dx[i] = st->x[i] - st->cand[i];
         st->step_norm = norm7(dx);
         st->mcc = mcc;
@@ -217,15 +273,19 @@ __device__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
     }
 }
 
-__device__ void lm_tail(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+__device__ __forceinline__ void lm_tail(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
     if (pass == 0) {
+        #pragma unroll
         for (int i = 0; i < 7; i++) st->x[i] = xp[i];
         st->nres = (int)tot[28];
         st->iteration = 0; st->successful = 0; st->done = 0;
         st->cost = tot[27]; st->initial_cost = tot[27];
         if (st->nres == 0) { st->cost = 0; lm_finish(st, out, 4); return; }
+        #pragma unroll
         for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        #pragma unroll
         for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        #pragma unroll
         for (int a = 0; a < 6; a++) st->scale[a] = 1.0 / (1.0 + sqrt(Aget(st->A, a, a)));
         st->x_norm = norm7(st->x);
         st->radius = 1e4; st->decrease_factor = 2.0; st->reuse_diag = 0;
@@ -239,9 +299,12 @@ __device__ void lm_tail(LMState* st, const double* tot, int pass, double* xp, al
     if (fabs(cost_change) <= 1e-6 * st->cost) { lm_finish(st, out, 1); return; }
     const double rel = cost_change / st->mcc;
     if (rel > 1e-3) {
+        #pragma unroll
         for (int i = 0; i < 7; i++) { st->x[i] = st->cand[i]; xp[i] = st->cand[i]; }
         st->x_norm = norm7(st->x);
+        #pragma unroll
         for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        #pragma unroll
         for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
         st->cost = new_cost;
         st->successful++;
@@ -259,6 +322,26 @@ __device__ void lm_tail(LMState* st, const double* tot, int pass, double* xp, al
     lm_next_step(st, out, max_iter);
 }
 
+// block-wide sum of NACC doubles per thread into tot[] (fixed tree => deterministic)
+template <int NT>
+__device__ __forceinline__ void block_reduce_acc(const double* acc, double (*sh)[NACC], double* tot) {
+    const int w = threadIdx.x / WAVE;
+#pragma unroll
+    for (int i = 0; i < NACC; i++) {
+        double v = wave_sum_d(acc[i]);
+        if (lane_id() == 0) sh[w][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NACC) {
+        double s = 0;
+        for (int ww = 0; ww < NT / WAVE; ww++) s += sh[ww][threadIdx.x];
+        tot[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// Multi-workgroup pass (large problems: mapping). The last workgroup to arrive reduces the
+// per-workgroup partials — one workgroup per thread, then the same block tree — and runs the LM tail.
 __global__ void __launch_bounds__(LB) k_lm_pass(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
                                                 double* partials, aloam_lm_summary* out, int pass, int max_iter,
                                                 const int* gate) {
@@ -274,19 +357,10 @@ __global__ void __launch_bounds__(LB) k_lm_pass(const aloam_factor* __restrict__
 #pragma unroll
     for (int i = 0; i < NACC; i++) acc[i] = 0;
     for (int i = blockIdx.x * LB + threadIdx.x; i < nslots; i += gridDim.x * LB) accumulate(f[i], q, t, acc);
-    const int w = threadIdx.x / WAVE;
-#pragma unroll
-    for (int i = 0; i < NACC; i++) {
-        double v = wave_sum_d(acc[i]);
-        if (lane_id() == 0) sh[w][i] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < NACC) {
-        double s = 0;
-        for (int ww = 0; ww < LB / WAVE; ww++) s += sh[ww][threadIdx.x];
-        __hip_atomic_store((unsigned long long*)&partials[blockIdx.x * NACC + threadIdx.x], __double_as_longlong(s),
+    block_reduce_acc<LB>(acc, sh, tot);
+    if (threadIdx.x < NACC)
+        __hip_atomic_store((unsigned long long*)&partials[blockIdx.x * NACC + threadIdx.x], __double_as_longlong(tot[threadIdx.x]),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -295,28 +369,73 @@ __global__ void __launch_bounds__(LB) k_lm_pass(const aloam_factor* __restrict__
     }
     __syncthreads();
     if (!last) return;
-    if (threadIdx.x < NACC) {
-        double s = 0;
-        for (int b = 0; b < (int)gridDim.x; b++)
-            s += __longlong_as_double(__hip_atomic_load((unsigned long long*)&partials[b * NACC + threadIdx.x],
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        tot[threadIdx.x] = s;
+    // every thread loads one workgroup's 29 partials (independent sc1 loads in flight)
+    double pacc[NACC];
+#pragma unroll
+    for (int i = 0; i < NACC; i++) pacc[i] = 0;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += LB) {
+#pragma unroll
+        for (int i = 0; i < NACC; i++)
+            pacc[i] += __longlong_as_double(__hip_atomic_load((unsigned long long*)&partials[b * NACC + i],
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        st->ticket = 0;
-        lm_tail(st, tot, pass, xp, out, max_iter);
+    block_reduce_acc<LB>(pacc, sh, tot);
+    __shared__ LMState ls;
+    {   // state -> LDS (all threads, 8-byte words), tail in LDS, LDS -> state
+        const int nw = sizeof(LMState) / 8;
+        for (int i = threadIdx.x; i < nw; i += LB) ((unsigned long long*)&ls)[i] = ((const unsigned long long*)st)[i];
+        __syncthreads();
+        if (threadIdx.x == 0) { ls.ticket = 0; lm_tail(&ls, tot, pass, xp, out, max_iter); }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nw; i += LB) ((unsigned long long*)st)[i] = ((const unsigned long long*)&ls)[i];
     }
+}
+
+// Whole Solve in ONE workgroup (small problems: odometry, <= a few thousand residual blocks):
+// every pass = all 1024 threads evaluate, block-reduce in LDS, thread 0 runs the LM tail.
+constexpr int LS = 512;
+__global__ void __launch_bounds__(LS) k_lm_solve_wg(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
+                                                    aloam_lm_summary* out, int max_iter, const int* gate) {
+    __shared__ double sh[LS / WAVE][NACC];
+    __shared__ double tot[NACC];
+    __shared__ int done;
+    __shared__ double xs[7];
+    __shared__ LMState ls;                     // the whole Solve keeps its state in LDS
+    if (gate && *gate == 0) return;
+    for (int pass = 0; pass <= max_iter; pass++) {
+        if (threadIdx.x < 7) xs[threadIdx.x] = pass == 0 ? xp[threadIdx.x] : ls.cand[threadIdx.x];
+        __syncthreads();
+        const dquat q{xs[0], xs[1], xs[2], xs[3]};
+        const double t[3] = {xs[4], xs[5], xs[6]};
+        double acc[NACC];
+#pragma unroll
+        for (int i = 0; i < NACC; i++) acc[i] = 0;
+        for (int i = threadIdx.x; i < nslots; i += LS) accumulate(f[i], q, t, acc);
+        block_reduce_acc<LS>(acc, sh, tot);
+        if (threadIdx.x == 0) {
+            lm_tail(&ls, tot, pass, xp, out, max_iter);
+            done = ls.done;
+        }
+        __syncthreads();
+        if (done) break;
+    }
+    (void)st;
 }
 
 static int lm_blocks(int nslots) { return std::max(1, std::min(LM_MAX_BLOCKS, (nslots + LB - 1) / LB)); }
 
-// one Ceres Solve: max_iter + 1 passes; `gate` (device int, may be null) disables the solve
+// one Ceres Solve over nslots factor slots; `gate` (device int, may be null) disables the solve.
+// Small problems run in one persistent workgroup, large ones as max_iter + 1 grid-wide passes.
+constexpr int LM_SINGLE_WG_MAX = 6144;
 void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate) {
-    const int nb = lm_blocks(nslots);
     aloam_lm_summary* out = C.d_lm_sum + round;
-    for (int pass = 0; pass <= C.P.max_solver_iterations; pass++)
-        k_lm_pass<<<nb, LB, 0, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_partials, out, pass, C.P.max_solver_iterations, gate);
+    if (nslots <= LM_SINGLE_WG_MAX) {
+        k_lm_solve_wg<<<1, LS, 0, C.stream>>>(d_f, nslots, d_x, C.d_lm, out, C.P.max_solver_iterations, gate);
+    } else {
+        const int nb = lm_blocks(nslots);
+        for (int pass = 0; pass <= C.P.max_solver_iterations; pass++)
+            k_lm_pass<<<nb, LB, 0, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_partials, out, pass, C.P.max_solver_iterations, gate);
+    }
     HIPCHK(hipGetLastError());
 }
 

@@ -15,6 +15,9 @@
 //   map_update       transformUpdate (:148-152)
 //   insert + rebuild append the stacks to their cubes, counting-sort the map by cube, per-cube
 //                    VoxelGrid of the surrounding cubes (:737-801)
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 #include "eigen_small.hpp"
@@ -104,6 +107,7 @@ __global__ void __launch_bounds__(256) k_map_knn5(
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const MapState* __restrict__ m, int* __restrict__ nbr, unsigned long long* cand_count) {
+    __shared__ RowSet<9> rows9[256 / WAVE];
     const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     if (qi >= ub_c + ub_s) return;
     if (!m->optimize) return;
@@ -116,49 +120,10 @@ __global__ void __launch_bounds__(256) k_map_knn5(
     const int* cs = corner ? cs_c : cs_s;
     const float4* sp = corner ? sp_c : sp_s;
     const int* si = corner ? si_c : si_s;
-    // per-lane sorted top-5 then 5 wave-min rounds (ties by point index)
-    float bd[5]; int bi[5], bp[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
-    const float fx = (sel.x - gd.ox) * gd.inv_cell, fy = (sel.y - gd.oy) * gd.inv_cell, fz = (sel.z - gd.oz) * gd.inv_cell;
-    const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-    const int x0 = (fx - cx < 0.5f) ? cx - 1 : cx, y0 = (fy - cy < 0.5f) ? cy - 1 : cy, z0 = (fz - cz < 0.5f) ? cz - 1 : cz;
-    int ncand = 0;
-    for (int c8 = 0; c8 < 8; c8++) {
-        const int x = x0 + (c8 & 1), y = y0 + ((c8 >> 1) & 1), z = z0 + (c8 >> 2);
-        if (x < 0 || y < 0 || z < 0 || x >= gd.dx || y >= gd.dy || z >= gd.dz) continue;
-        const int c = (z * gd.dy + y) * gd.dx + x;
-        const int b = cs[c], e = cs[c + 1];
-        ncand += e - b;
-        for (int p = b + lane_id(); p < e; p += WAVE) {
-            const float4 v = sp[p];
-            const float d2 = sqdist(v.x, v.y, v.z, sel.x, sel.y, sel.z);
-            if (!(d2 < 1.0f)) continue;
-            const int id = si[p];
-            if (d2 < bd[4] || (d2 == bd[4] && id < bi[4])) {
-                float nd = d2; int ni = id, np = p;
-#pragma unroll
-                for (int k = 0; k < 5; k++) {
-                    const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
-                    if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
-                }
-            }
-        }
-    }
-    int head = 0, res[5];
-    int found = 0;
-    for (int k = 0; k < 5; k++) {
-        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
-#pragma unroll
-        for (int j = 0; j < 5; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
-        const unsigned long long key = hp < 0 ? ~0ull : dist_key(hd, hi);
-        const unsigned long long mn = wave_min_u64(key);
-        if (mn == ~0ull) break;
-        const unsigned long long won = __ballot(key == mn);
-        if (key == mn) head++;
-        res[k] = __shfl(hp, __ffsll((long long)won) - 1, WAVE);
-        found++;
-    }
+    int res[5], ri[5], ncand = 0;
+    float rd[5];
+    const int found = wave_knn_rows<5, 9>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, cs, sp, si,
+                                          sel.x, sel.y, sel.z, 1.0f, 1, res, rd, ri, &ncand, rows9[threadIdx.x / WAVE]);
     if (lane_id() == 0) {
         if (found == 5) for (int k = 0; k < 5; k++) out[k] = res[k];
         else out[0] = -1;
@@ -265,11 +230,14 @@ __global__ void k_map_insert(const float4* __restrict__ stack, const int* d_n, i
 }
 
 // cube bookkeeping arrays: cnt_old, cnt_new, first_old, first_new, off, seg_nout, final_off (each CUBE_N+1)
-struct CubeArrays { int *cnt_old, *cnt_new, *first_old, *first_new, *off, *seg_nout, *final_off; };
+struct CubeArrays { int *first_old, *last_old, *first_new, *last_new, *off, *seg_nout, *final_off; };
+// counts from run boundaries (the old map and the sorted new points are both ordered by cube)
+__device__ __forceinline__ int old_count(const CubeArrays& a, int c) { return a.last_old[c] >= a.first_old[c] ? a.last_old[c] - a.first_old[c] + 1 : 0; }
+__device__ __forceinline__ int new_count(const CubeArrays& a, int c) { return a.last_new[c] >= a.first_new[c] ? a.last_new[c] - a.first_new[c] + 1 : 0; }
 
 __global__ void k_cube_reset(CubeArrays a) {
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c <= CUBE_N; c += gridDim.x * blockDim.x) {
-        a.cnt_old[c] = 0; a.cnt_new[c] = 0; a.first_old[c] = 0x7fffffff; a.first_new[c] = 0x7fffffff; a.seg_nout[c] = 0;
+        a.last_old[c] = -1; a.last_new[c] = -1; a.first_old[c] = 0x7fffffff; a.first_new[c] = 0x7fffffff; a.seg_nout[c] = 0;
     }
 }
 __global__ void k_cube_count_old(const int* __restrict__ cube, const int* d_n, CubeArrays a) {
@@ -277,16 +245,16 @@ __global__ void k_cube_count_old(const int* __restrict__ cube, const int* d_n, C
     for (int i = blockIdx.x * MB + threadIdx.x; i < n; i += gridDim.x * MB) {
         const int c = cube[i];
         if (c < 0) continue;
-        atomicAdd(&a.cnt_old[c], 1);
-        atomicMin(&a.first_old[c], i);
+        if (i == 0 || cube[i - 1] != c) a.first_old[c] = i;
+        if (i == n - 1 || cube[i + 1] != c) a.last_old[c] = i;
     }
 }
 __global__ void k_cube_count_new(const unsigned* __restrict__ skey, int ub, CubeArrays a) {
     for (int p = blockIdx.x * MB + threadIdx.x; p < ub; p += gridDim.x * MB) {
         const unsigned c = skey[p];
         if (c >= (unsigned)CUBE_N) continue;
-        atomicAdd(&a.cnt_new[c], 1);
-        atomicMin(&a.first_new[c], p);
+        if (p == 0 || skey[p - 1] != c) a.first_new[c] = p;
+        if (p == ub - 1 || skey[p + 1] != c) a.last_new[c] = p;
     }
 }
 // single block: exclusive scan over cubes of v(c); mode 0: cnt_old+cnt_new -> off ; mode 1: final counts -> final_off
@@ -300,8 +268,8 @@ __global__ void k_cube_scan(CubeArrays a, const unsigned char* __restrict__ vali
         const int c = base + threadIdx.x;
         int v = 0;
         if (c < CUBE_N) {
-            if (mode == 0) v = a.cnt_old[c] + a.cnt_new[c];
-            else v = valid[c] ? a.seg_nout[c] : a.cnt_old[c] + a.cnt_new[c];
+            if (mode == 0) v = old_count(a, c) + new_count(a, c);
+            else v = valid[c] ? a.seg_nout[c] : old_count(a, c) + new_count(a, c);
         }
         sh[threadIdx.x] = v;
         __syncthreads();
@@ -334,7 +302,7 @@ __global__ void k_cube_scatter(const float4* __restrict__ old_pts, const int* __
     for (int p = blockIdx.x * MB + threadIdx.x; p < ub_new; p += stride) {
         const unsigned c = skey[p];
         if (c >= (unsigned)CUBE_N) continue;
-        const int pos = a.off[c] + a.cnt_old[c] + (p - a.first_new[c]);
+        const int pos = a.off[c] + old_count(a, c) + (p - a.first_new[c]);
         B[pos] = ins_pts[sval[p]];
         Bcube[pos] = (int)c;
     }
@@ -358,6 +326,148 @@ __global__ void k_map_register(const float4* __restrict__ full, int n, const Map
 __global__ void k_copy_int(const int* src, int* dst) { *dst = *src; }
 
 // ------------------------------------------------------------------------------------------
+// Per-cube VoxelGrid of the surrounding cubes (:788-801) as ONE stable radix sort: key = (rank of
+// the cube in the surrounding list) << 32 | leaf index inside that cube's own PCL grid (or the point
+// position when PCL's int32 leaf count overflows: pass-through); points of other cubes sort last. Stable => the points of a leaf are summed in the cube's order.
+constexpr unsigned long long CV_NONE = 0x7fffffffffull;   // > any (rank<<32|idx), rank < 125
+struct CubeVox { unsigned bb[125][6]; int minb[125][3]; int mul1[125], mul2[125], ovf[125]; int rank_of[CUBE_N]; int first_run[126]; int nrun; };
+
+__global__ void k_cubevox_init(CubeVox* v, const MapState* m) {
+    for (int i = threadIdx.x; i < CUBE_N; i += blockDim.x) v->rank_of[i] = -1;
+    for (int i = threadIdx.x; i < 125 * 6; i += blockDim.x) (&v->bb[0][0])[i] = (i % 6) < 3 ? 0xffffffffu : 0u;
+    for (int i = threadIdx.x; i < 126; i += blockDim.x) v->first_run[i] = 0x7fffffff;
+    __syncthreads();
+    for (int r = threadIdx.x; r < m->valid_num; r += blockDim.x) v->rank_of[m->valid_ind[r]] = r;
+    if (threadIdx.x == 0) v->nrun = 0;
+}
+// one workgroup per surrounding cube: bbox of its points in B
+__global__ void k_cubevox_bbox(const float4* __restrict__ B, CubeArrays a, const MapState* m, CubeVox* v, float leaf) {
+    __shared__ unsigned sh[6];
+    const int r = blockIdx.x;
+    if (r >= m->valid_num) return;
+    const int c = m->valid_ind[r];
+    if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    for (int p = a.off[c] + threadIdx.x; p < a.off[c + 1]; p += blockDim.x) {
+        const float4 q = B[p];
+        const unsigned u[3] = {f2ord(q.x), f2ord(q.y), f2ord(q.z)};
+        for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], u[d]); mx[d] = max(mx[d], u[d]); }
+    }
+    for (int d = 0; d < 3; d++) { atomicMin(&sh[d], mn[d]); atomicMax(&sh[3 + d], mx[d]); }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int d = 0; d < 6; d++) v->bb[r][d] = sh[d];
+        bool ovf;
+        int minb[3], mul1, mul2;
+        voxel_params(sh, leaf, &ovf, minb, &mul1, &mul2);      // same bbox -> leaf grid as k_voxel.hip
+        for (int d = 0; d < 3; d++) v->minb[r][d] = minb[d];
+        v->mul1[r] = mul1; v->mul2[r] = mul2; v->ovf[r] = ovf;
+    }
+}
+__global__ void k_cubevox_keys(const float4* __restrict__ B, const int* __restrict__ Bcube, CubeArrays a, const CubeVox* __restrict__ v,
+                               float leaf, int ub, unsigned long long* __restrict__ keys, int* __restrict__ vals) {
+    const int total = a.off[CUBE_N];
+    const float inv = 1.0f / leaf;
+    for (int p = blockIdx.x * MB + threadIdx.x; p < ub; p += gridDim.x * MB) {
+        unsigned long long k = CV_NONE;
+        if (p < total) {
+            const int r = v->rank_of[Bcube[p]];
+            if (r >= 0) {
+                const int mb[3] = {v->minb[r][0], v->minb[r][1], v->minb[r][2]};
+                const unsigned idx = v->ovf[r] ? (unsigned)p : voxel_index(B[p], inv, mb, v->mul1[r], v->mul2[r]);
+                k = ((unsigned long long)r << 32) | idx;
+            }
+        }
+        keys[p] = k;
+        vals[p] = p;
+    }
+}
+// run heads (leaf changes) -> global run ids by a block count + small scan, first run of each cube
+__global__ void k_cubevox_flags(const unsigned long long* __restrict__ keys, int ub, int* blk) {
+    __shared__ int sh[MB / WAVE];
+    const int i = blockIdx.x * MB + threadIdx.x;
+    const int f = i < ub && keys[i] != CV_NONE && (i == 0 || keys[i] != keys[i - 1]);
+    const int s = wave_sum_i(f);
+    if (lane_id() == 0) sh[threadIdx.x / WAVE] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < MB / WAVE; w++) t += sh[w]; blk[blockIdx.x] = t; }
+}
+__global__ void k_cubevox_heads(const unsigned long long* __restrict__ keys, int ub, const int* blk, int* heads, CubeVox* v) {
+    __shared__ int sh[MB / WAVE];
+    const int i = blockIdx.x * MB + threadIdx.x;
+    const int f = i < ub && keys[i] != CV_NONE && (i == 0 || keys[i] != keys[i - 1]);
+    const unsigned long long mk = __ballot(f);
+    if (lane_id() == 0) sh[threadIdx.x / WAVE] = __popcll(mk);
+    __syncthreads();
+    int before = blk[blockIdx.x];
+    for (int w = 0; w < (int)(threadIdx.x / WAVE); w++) before += sh[w];
+    if (f) {
+        const int run = before + __popcll(mk & lanemask_lt64());
+        heads[run] = i;
+        const int r = (int)(keys[i] >> 32);
+        if (i == 0 || (int)(keys[i - 1] >> 32) != r) v->first_run[r] = run;
+    }
+}
+// one thread per run: centroid summed in sorted (= cube) order, written at the cube's offset
+__global__ void k_cubevox_centroids(const float4* __restrict__ B, const unsigned long long* __restrict__ keys, const int* __restrict__ vals,
+                                    const int* __restrict__ heads, const int* nrun_p, int ub, const MapState* m, const CubeVox* v,
+                                    CubeArrays a, float4* __restrict__ out) {
+    const int nrun = *nrun_p;
+    const int run = blockIdx.x * MB + threadIdx.x;
+    if (run >= nrun) return;
+    const int h0 = heads[run];
+    int h1 = run + 1 < nrun ? heads[run + 1] : ub;
+    const int r = (int)(keys[h0] >> 32);
+    const int c = m->valid_ind[r];
+    float4 s = B[vals[h0]];
+    int cnt = 1;
+    for (int t = h0 + 1; t < h1 && keys[t] == keys[h0]; t++) {
+        const float4 q = B[vals[t]];
+        s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+        cnt++;
+    }
+    const float fc = (float)cnt;
+    const int local = run - v->first_run[r];
+    out[a.off[c] + local] = make_float4(s.x / fc, s.y / fc, s.z / fc, s.w / fc);
+    // the last run of the cube records the cube's leaf count
+    const bool last_of_cube = (run + 1 == nrun) || ((int)(keys[heads[run + 1]] >> 32) != r);
+    if (last_of_cube) a.seg_nout[c] = local + 1;
+}
+
+size_t cube_sort_tmp_bytes(int cap) {
+    size_t bytes = 0;
+    HIPCHK(rocprim::radix_sort_pairs((void*)nullptr, bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int*)nullptr, (int*)nullptr,
+                                     (unsigned)cap, 0, 39, (hipStream_t)0));
+    return bytes;
+}
+
+__global__ void k_scan_small_m(int* a, int nb, int* total) {
+    __shared__ int sh[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < nb; base += 1024) {
+        int i = base + threadIdx.x;
+        int v = i < nb ? a[i] : 0;
+        sh[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += t;
+            __syncthreads();
+        }
+        int incl = sh[threadIdx.x];
+        if (i < nb) a[i] = carry + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+// ------------------------------------------------------------------------------------------
 static int nblk(int n) { return std::max(1, std::min(2048, (n + MB - 1) / MB)); }
 
 static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, const int* d_stack_n, float leaf) {
@@ -371,8 +481,8 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     // scratch carving: cube arrays live in d_cube_cnt ([7][CUBE_N+1])
     CubeArrays a;
     int* base = C.d_cube_cnt + which * 7 * (CUBE_N + 1);
-    a.cnt_old = base; a.cnt_new = base + (CUBE_N + 1); a.first_old = base + 2 * (CUBE_N + 1);
-    a.first_new = base + 3 * (CUBE_N + 1); a.off = base + 4 * (CUBE_N + 1); a.seg_nout = base + 5 * (CUBE_N + 1);
+    a.first_old = base; a.last_old = base + (CUBE_N + 1); a.first_new = base + 2 * (CUBE_N + 1);
+    a.last_new = base + 3 * (CUBE_N + 1); a.off = base + 4 * (CUBE_N + 1); a.seg_nout = base + 5 * (CUBE_N + 1);
     a.final_off = base + 6 * (CUBE_N + 1);
     if (C.n_mc + C.n_ms + 2 * ub_new > C.cap_map) throw ApiError{ALOAM_E_CAPACITY, "map capacity exceeded"};
     unsigned* k1 = (unsigned*)C.d_vkeys;
@@ -384,9 +494,27 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     k_cube_count_new<<<nblk(ub_new), MB, 0, st>>>(k2, ub_new, a);
     k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 0, nullptr);
     k_cube_scatter<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(A, Acube, d_n_old, C.d_ins_pts, k2, C.d_ins_val2, ub_new, a, B, Bcube);
-    // per-cube VoxelGrid of the surrounding cubes into the insertion scratch at the same offsets
+    // per-cube VoxelGrid of the surrounding cubes into Cf at the same offsets (one stable radix sort)
     float4* Cf = C.d_map_tmp;
-    segment_voxel_launch(C, B, a.off, C.d_map->valid_ind, &C.d_map->valid_num, 125, leaf, Cf, a.seg_nout, C.d_seg_keys);
+    const int ub_tot = n_old_ub + ub_new;
+    CubeVox* cv = (CubeVox*)C.d_seg_keys;                         // scratch header
+    unsigned long long* vk1 = C.d_seg_keys + 32768;
+    unsigned long long* vk2 = vk1 + (size_t)C.cap_map;
+    int* vv1 = (int*)(vk2 + (size_t)C.cap_map);
+    int* vv2 = vv1 + (size_t)C.cap_map;
+    int* heads = vv2 + (size_t)C.cap_map;
+    const int nbt = (ub_tot + MB - 1) / MB;
+    k_cubevox_init<<<1, 1024, 0, st>>>(cv, C.d_map);
+    k_cubevox_bbox<<<125, 256, 0, st>>>(B, a, C.d_map, cv, leaf);
+    k_cubevox_keys<<<nblk(ub_tot), MB, 0, st>>>(B, Bcube, a, cv, leaf, ub_tot, vk1, vv1);
+    if (ub_tot > 0) {
+        size_t bytes = C.sort_tmp_bytes;
+        HIPCHK(rocprim::radix_sort_pairs(C.d_sort_tmp, bytes, vk1, vk2, vv1, vv2, (unsigned)ub_tot, 0, 39, st));
+        k_cubevox_flags<<<nbt, MB, 0, st>>>(vk2, ub_tot, C.d_blk);
+        k_scan_small_m<<<1, 1024, 0, st>>>(C.d_blk, nbt, &cv->nrun);
+        k_cubevox_heads<<<nbt, MB, 0, st>>>(vk2, ub_tot, C.d_blk, heads, cv);
+        k_cubevox_centroids<<<nbt, MB, 0, st>>>(B, vk2, vv2, heads, &cv->nrun, ub_tot, C.d_map, cv, a, Cf);
+    }
     k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 1, d_n_old);
     k_cube_final<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(B, Bcube, Cf, C.d_cube_valid, a, A, Acube);
     HIPCHK(hipGetLastError());

@@ -12,31 +12,23 @@
 
 namespace aloam {
 
-// wave_knn<1> lives in k_grid.hip; a local copy keeps this file self-contained.
+// Exact 1-NN within d^2 < 25 (laserOdometry.cpp:386-389) in two phases on a grid of edge g = 2.56 m:
+// the query cell's 3x3x3 block holds every point closer than g, so a best distance < 0.99 g found
+// there is final; otherwise the 5x5x5 block (>= 2g = 5.1 m around the query) is searched.
 __device__ inline int wave_nn1(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
-                               const int* __restrict__ sidx, float qx, float qy, float qz, float r2, int* out_idx, float* out_d2) {
-    unsigned long long best = ~0ull;
-    float fx = (qx - gd.ox) * gd.inv_cell, fy = (qy - gd.oy) * gd.inv_cell, fz = (qz - gd.oz) * gd.inv_cell;
-    int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-    int x0 = (fx - cx < 0.5f) ? cx - 1 : cx, y0 = (fy - cy < 0.5f) ? cy - 1 : cy, z0 = (fz - cz < 0.5f) ? cz - 1 : cz;
-    for (int c8 = 0; c8 < 8; c8++) {
-        int x = x0 + (c8 & 1), y = y0 + ((c8 >> 1) & 1), z = z0 + (c8 >> 2);
-        if (x < 0 || y < 0 || z < 0 || x >= gd.dx || y >= gd.dy || z >= gd.dz) continue;
-        int c = (z * gd.dy + y) * gd.dx + x;
-        int b = start[c], e = start[c + 1];
-        for (int p = b + lane_id(); p < e; p += WAVE) {
-            float4 v = spts[p];
-            float d2 = sqdist(v.x, v.y, v.z, qx, qy, qz);
-            if (d2 < r2) {
-                unsigned long long k = dist_key(d2, sidx[p]);
-                best = k < best ? k : best;
-            }
-        }
-    }
-    best = wave_min_u64(best);
-    if (best == ~0ull) return 0;
-    *out_idx = (int)(best & 0xffffffffu);
-    *out_d2 = __uint_as_float((unsigned)(best >> 32));
+                               const int* __restrict__ sidx, float qx, float qy, float qz, int* out_idx, float* out_d2,
+                               RowSet<9>& r9, RowSet<25>& r25) {
+    int pos, idx;
+    float d2;
+    const float acc = 0.99f * gd.cell;
+    int f = wave_knn_rows<1, 9>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, spts, sidx, qx, qy, qz,
+                                25.0f, 1, &pos, &d2, &idx, nullptr, r9);
+    if (!(f && d2 < acc * acc))
+        f = wave_knn_rows<1, 25>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, spts, sidx, qx, qy, qz,
+                                 25.0f, 2, &pos, &d2, &idx, nullptr, r25);
+    if (!f) return 0;
+    *out_idx = idx;
+    *out_d2 = d2;
     return 1;
 }
 
@@ -44,58 +36,92 @@ __device__ inline int line_of(float intensity) { return int(intensity); }
 
 // forward/backward scan-line search of laserOdometry.cpp:400-441 (corner) / :483-532 (surf)
 // mode 0 = corner (one candidate set), 1 = surf (two sets).
+// Processes 4 chunks of 64 candidates per step (4 coalesced loads in flight per lane); the break
+// index is the first flagged position in scan order over the 256, so results equal the serial loop.
 template <int MODE>
 __device__ inline void window_search(const float4* __restrict__ cl, int n, int closest, int cid, float sx, float sy, float sz,
                                      int* ind2, int* ind3) {
     const int lane = lane_id();
+    constexpr int U = 4;
     float best2 = 25.0f, best3 = 25.0f;
     int i2 = -1, i3 = -1;
     // ---- forward (increasing index) ----
-    for (int base = closest + 1; base < n; base += WAVE) {
-        const int j = base + lane;
-        const bool in = j < n;
-        float4 p = in ? cl[j] : make_float4(0, 0, 0, 0);
-        const int line = line_of(p.w);
-        const bool brk = in && (line > (cid + 2.5));
-        const unsigned long long bm = __ballot(brk);
-        const int first_brk = bm ? base + (__ffsll((long long)bm) - 1) : 0x7fffffff;
-        const bool live = in && j < first_brk;
-        const float d = sqdist(p.x, p.y, p.z, sx, sy, sz);
-        bool c2, c3;
-        if (MODE == 0) { c2 = live && !(line <= cid); c3 = false; }
-        else { c2 = live && line <= cid; c3 = live && line > cid; }
-        unsigned long long k2 = c2 ? dist_key(d, j) : ~0ull, k3 = c3 ? dist_key(d, j) : ~0ull;
+    for (int base = closest + 1; base < n; base += U * WAVE) {
+        float4 p[U];
+        int line[U];
+        unsigned long long bm[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = base + u * WAVE + lane;
+            p[u] = j < n ? cl[j] : make_float4(0, 0, 0, 0);
+        }
+        int first_brk = 0x7fffffff;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = base + u * WAVE + lane;
+            line[u] = line_of(p[u].w);
+            bm[u] = __ballot(j < n && (line[u] > (cid + 2.5)));
+            if (bm[u] && first_brk == 0x7fffffff) first_brk = base + u * WAVE + (__ffsll((long long)bm[u]) - 1);
+        }
+        unsigned long long k2 = ~0ull, k3 = ~0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = base + u * WAVE + lane;
+            const bool live = j < n && j < first_brk;
+            const float d = sqdist(p[u].x, p[u].y, p[u].z, sx, sy, sz);
+            const unsigned long long key = dist_key(d, j);
+            if (MODE == 0) { if (live && !(line[u] <= cid) && key < k2) k2 = key; }
+            else {
+                if (live && line[u] <= cid && key < k2) k2 = key;
+                if (live && line[u] > cid && key < k3) k3 = key;
+            }
+        }
         k2 = wave_min_u64(k2);
         if (k2 != ~0ull) { float dm = __uint_as_float((unsigned)(k2 >> 32)); if (dm < best2) { best2 = dm; i2 = (int)(k2 & 0xffffffffu); } }
         if (MODE == 1) {
             k3 = wave_min_u64(k3);
             if (k3 != ~0ull) { float dm = __uint_as_float((unsigned)(k3 >> 32)); if (dm < best3) { best3 = dm; i3 = (int)(k3 & 0xffffffffu); } }
         }
-        if (bm) break;
+        if (first_brk != 0x7fffffff) break;
     }
     // ---- backward (decreasing index): first occurrence = largest index among equal distances ----
-    for (int base = closest - 1; base >= 0; base -= WAVE) {
-        const int j = base - lane;
-        const bool in = j >= 0;
-        float4 p = in ? cl[j] : make_float4(0, 0, 0, 0);
-        const int line = line_of(p.w);
-        const bool brk = in && (line < (cid - 2.5));
-        const unsigned long long bm = __ballot(brk);
-        const int first_brk = bm ? base - (__ffsll((long long)bm) - 1) : -1;
-        const bool live = in && j > first_brk;
-        const float d = sqdist(p.x, p.y, p.z, sx, sy, sz);
-        bool c2, c3;
-        if (MODE == 0) { c2 = live && !(line >= cid); c3 = false; }
-        else { c2 = live && line >= cid; c3 = live && line < cid; }
-        const unsigned ord = 0x7fffffffu - (unsigned)j;
-        unsigned long long k2 = c2 ? dist_key(d, (int)ord) : ~0ull, k3 = c3 ? dist_key(d, (int)ord) : ~0ull;
+    for (int base = closest - 1; base >= 0; base -= U * WAVE) {
+        float4 p[U];
+        int line[U];
+        unsigned long long bm[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = base - u * WAVE - lane;
+            p[u] = j >= 0 ? cl[j] : make_float4(0, 0, 0, 0);
+        }
+        int first_brk = -1;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = base - u * WAVE - lane;
+            line[u] = line_of(p[u].w);
+            bm[u] = __ballot(j >= 0 && (line[u] < (cid - 2.5)));
+            if (bm[u] && first_brk == -1) first_brk = base - u * WAVE - (__ffsll((long long)bm[u]) - 1);
+        }
+        unsigned long long k2 = ~0ull, k3 = ~0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = base - u * WAVE - lane;
+            const bool live = j >= 0 && j > first_brk;
+            const float d = sqdist(p[u].x, p[u].y, p[u].z, sx, sy, sz);
+            const unsigned long long key = dist_key(d, (int)(0x7fffffffu - (unsigned)j));
+            if (MODE == 0) { if (live && !(line[u] >= cid) && key < k2) k2 = key; }
+            else {
+                if (live && line[u] >= cid && key < k2) k2 = key;
+                if (live && line[u] < cid && key < k3) k3 = key;
+            }
+        }
         k2 = wave_min_u64(k2);
         if (k2 != ~0ull) { float dm = __uint_as_float((unsigned)(k2 >> 32)); if (dm < best2) { best2 = dm; i2 = (int)(0x7fffffffu - (unsigned)(k2 & 0xffffffffu)); } }
         if (MODE == 1) {
             k3 = wave_min_u64(k3);
             if (k3 != ~0ull) { float dm = __uint_as_float((unsigned)(k3 >> 32)); if (dm < best3) { best3 = dm; i3 = (int)(0x7fffffffu - (unsigned)(k3 & 0xffffffffu)); } }
         }
-        if (bm) break;
+        if (first_brk != -1) break;
     }
     *ind2 = i2;
     *ind3 = i3;
@@ -107,9 +133,13 @@ __global__ void __launch_bounds__(256) k_odom_search(
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt) {
+    __shared__ RowSet<9> rows9[256 / WAVE];
+    __shared__ RowSet<25> rows25[256 / WAVE];
     const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     const int lane = lane_id();
     if (qi >= n_sharp + n_flat) return;
+    RowSet<9>& r9 = rows9[threadIdx.x / WAVE];
+    RowSet<25>& r25 = rows25[threadIdx.x / WAVE];
     const bool is_corner = qi < n_sharp;
     const float4 pi = is_corner ? sharp[qi] : flat[qi - n_sharp];
     // TransformToStart (:154-172)
@@ -127,8 +157,8 @@ __global__ void __launch_bounds__(256) k_odom_search(
     int closest = -1;
     float d2 = 0.f;
     int found;
-    if (is_corner) found = n > 0 ? wave_nn1(*gdc, cs_c, sp_c, si_c, sx, sy, sz, 25.0f, &closest, &d2) : 0;
-    else found = n > 0 ? wave_nn1(*gds, cs_s, sp_s, si_s, sx, sy, sz, 25.0f, &closest, &d2) : 0;
+    if (is_corner) found = n > 0 ? wave_nn1(*gdc, cs_c, sp_c, si_c, sx, sy, sz, &closest, &d2, r9, r25) : 0;
+    else found = n > 0 ? wave_nn1(*gds, cs_s, sp_s, si_s, sx, sy, sz, &closest, &d2, r9, r25) : 0;
     if (found) {
         const int cid = line_of(cl[closest].w);
         int i2, i3;

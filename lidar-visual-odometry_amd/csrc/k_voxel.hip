@@ -22,30 +22,6 @@ constexpr int VB = 256;
 
 struct VoxHdr { unsigned bb[6]; int nrun; int pad; };
 
-__device__ inline void voxel_params(const unsigned* bb, float leaf, bool* overflow, int minb[3], int* mul1, int* mul2) {
-    const float inv = 1.0f / leaf;
-    float mn[3], mx[3];
-    for (int a = 0; a < 3; a++) { mn[a] = ord2f(bb[a]); mx[a] = ord2f(bb[3 + a]); }
-    long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
-    long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
-    long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
-    *overflow = dx * dy * dz > 2147483647LL;
-    int divb[3];
-    for (int a = 0; a < 3; a++) {
-        minb[a] = (int)floorf(mn[a] * inv);
-        int maxb = (int)floorf(mx[a] * inv);
-        divb[a] = maxb - minb[a] + 1;
-    }
-    *mul1 = divb[0];
-    *mul2 = divb[0] * divb[1];
-}
-__device__ inline unsigned voxel_index(float4 p, float inv, const int minb[3], int mul1, int mul2) {
-    int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
-    int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
-    int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
-    return (unsigned)(i0 + i1 * mul1 + i2 * mul2);
-}
-
 __global__ void k_vox_init(VoxHdr* h) {
     if (threadIdx.x < 6) h->bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     if (threadIdx.x == 0) h->nrun = 0;
