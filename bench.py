@@ -7,6 +7,11 @@ streamed through the full pipeline; the warmup frames (>= 5) prime the local map
 sweep: feature extraction, 10 odometry rounds (search + 4-iteration LM), 10 mapping rounds, map
 update. Inputs are resident in HBM before the timed region (ALOAM_INPUT_DEVICE).
 
+--mode pipeline (default) runs the reference's node split: scanRegistration+laserOdometry on one
+context/stream and laserMapping on another, scan k's mapping overlapping scan k+1's front end (the
+reference runs the three nodes as concurrent processes). --mode serial runs all three stages of a
+scan back to back on one stream. Every scan still goes through all three stages in the timed region.
+
 N > 1 ranks (torchrun, one process per GPU, RCCL): each rank runs an independent replica sequence
 (a pose chain does not shard), value = all ranks' scans / max-over-ranks time ("scaling": "weak").
 
@@ -35,6 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-frames", type=int, default=24, help="frames of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", choices=("pipeline", "serial"), default="pipeline")
     ap.add_argument("--profile-json", default="", help="also dump per-frame stage timings here")
     return ap.parse_args()
 
@@ -64,27 +70,55 @@ def main():
     d_frames = [torch.from_numpy(f).to(dev) for f in frames]
     torch.cuda.synchronize()
 
-    ctx = lvo.Context(lvo.abi.default_params(64), device=local_rank)
+    params = lvo.abi.default_params(64)
     traj = []
-    for k in range(W):
-        od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
-        traj.append(mp["t_w_curr"])
-
-    ctx.set_profiling(True)
     search_ms = search_bytes = 0.0
     launches = 0
     stage = np.zeros(3)
+
+    def account(tm_front, tm_back):
+        nonlocal search_ms, search_bytes, launches, stage
+        search_ms += tm_back["map_search_ms"]
+        search_bytes += tm_back["map_search_bytes"]
+        launches += tm_back["map_search_launches"]
+        stage += [tm_front["scan_registration_ms"], tm_front["odometry_ms"], tm_back["mapping_ms"]]
+
+    if args.mode == "serial":
+        ctx = lvo.Context(params, device=local_rank)
+        for k in range(W):
+            od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            traj.append(mp["t_w_curr"])
+        ctx.set_profiling(True)
+    else:
+        pipe = lvo.Pipeline(params, device=local_rank)
+        for k in range(W):
+            od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
+        traj.append(pipe.flush()["t_w_curr"])
+        pipe.set_profiling(True)
+
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(W, W + K):
-        od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
-        tm = ctx.timing()
-        search_ms += tm["map_search_ms"]
-        search_bytes += tm["map_search_bytes"]
-        launches += tm["map_search_launches"]
-        stage += [tm["scan_registration_ms"], tm["odometry_ms"], tm["mapping_ms"]]
+    if args.mode == "serial":
+        for k in range(W, W + K):
+            od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            tm = ctx.timing()
+            account(tm, tm)
+            traj.append(mp["t_w_curr"])
+    else:
+        for k in range(W, W + K):
+            od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            tf = pipe.front.timing()
+            if mp is not None:
+                account(tf, pipe.last_back_timing)
+                traj.append(mp["t_w_curr"])
+            else:
+                account(tf, {"map_search_ms": 0, "map_search_bytes": 0, "map_search_launches": 0, "mapping_ms": 0})
+        mp = pipe.flush()
+        account({"scan_registration_ms": 0, "odometry_ms": 0}, pipe.last_back_timing)
         traj.append(mp["t_w_curr"])
     torch.cuda.synchronize()
     if dist:
@@ -94,7 +128,10 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ctx.set_profiling(False)
+    if args.mode == "serial":
+        ctx.set_profiling(False)
+    else:
+        pipe.set_profiling(False)
 
     total_scans = K * world
     value = total_scans / elapsed
@@ -126,6 +163,7 @@ def main():
             "stage_ms": {"scan_registration": round(stage[0], 4), "odometry": round(stage[1], 4),
                          "mapping": round(stage[2], 4)},
             "parallelism": f"replicas x{world}",
+            "mode": args.mode + (" (front end scan k+1 || mapping scan k, 2 HIP streams)" if args.mode == "pipeline" else ""),
         },
         "roofline": {
             "kernel": "k_map_knn5 (mapping 5-NN correspondence search)",
@@ -146,19 +184,29 @@ def main():
         n_cpu = min(args.cpu_frames, W + K)
         otraj = []
         t_cpu = 0.0
+        st_cpu = np.zeros(3)
         for k in range(n_cpu):
             t1 = time.perf_counter()
             od, mp = orc.process_scan(frames[k])
-            t_cpu += time.perf_counter() - t1 if k >= 1 else 0.0
+            if k >= 1:
+                t_cpu += time.perf_counter() - t1
+                st_cpu += orc.stage_times()
             otraj.append(mp["t_w_curr"])
-        cpu_value = (n_cpu - 1) / t_cpu if t_cpu > 0 else None
+        serial = (n_cpu - 1) / t_cpu if t_cpu > 0 else None
+        # the reference deploys the three stages as three single-threaded ROS processes: pipelined
+        # throughput = 1 / slowest stage on 3 cores (SURVEY §8(d) CPU baseline, form 2)
+        pipelined = (n_cpu - 1) / (float(np.max(st_cpu)) * 1e-3) if np.max(st_cpu) > 0 else None   # stage times in ms
+        cpu_value = pipelined if args.mode == "pipeline" else serial
         result["cpu_baseline"] = {
             "value": round(cpu_value, 4) if cpu_value else None,
             "unit": "scans/s",
-            "cores": 1,
+            "cores": 3 if args.mode == "pipeline" else 1,
             "kind": "port",
             "sample": f"frames 1..{n_cpu - 1} of the same synthetic HDL-64 sequence through oracle/liboracle.so "
-                      "(scanRegistration + laserOdometry + laserMapping, kd-tree, Ceres-style LM, single thread)",
+                      "(scanRegistration + laserOdometry + laserMapping, kd-tree, Ceres-style LM); "
+                      + ("3-node pipelined = 1/max(stage), one core per stage" if args.mode == "pipeline" else "serial, 1 core"),
+            "serial_1core": round(serial, 4) if serial else None,
+            "stage_ms": [round(v, 3) for v in (st_cpu / max(n_cpu - 1, 1))],
         }
         m = min(len(otraj), len(traj))
         ate = float(np.sqrt(np.mean(np.sum((np.array(traj[:m]) - np.array(otraj[:m])) ** 2, axis=1))))
@@ -167,7 +215,7 @@ def main():
 
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
+    (ctx if args.mode == "serial" else pipe).close()
     if dist:
         dist.destroy_process_group()
 

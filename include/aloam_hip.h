@@ -181,9 +181,17 @@ int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out);
 int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out);
 
 /* ---- whole per-scan pipeline: scanRegistration -> laserOdometry -> laserMapping ----- */
-/* map_out may be NULL; mapping then runs only when do_mapping != 0. */
+/* map_out may be NULL. With ALOAM_NO_MAPPING in flags the call stops after laserOdometry and
+ * leaves the published corner/surf/full clouds + pose for aloam_forward_mapping_input. */
+#define ALOAM_NO_MAPPING 2
 int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags,
                        aloam_odom_result* odom_out, aloam_map_result* map_out);
+/* The /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3 and /laser_odom_to_init
+ * hand-off (laserOdometry.cpp:588-663 -> laserMapping.cpp:192-234) between two contexts on the
+ * same device, device to device: `src` ran laserOdometry (front end), `dst` runs laserMapping.
+ * Lets the two stages of consecutive scans run concurrently on two streams, as the reference's
+ * separate ROS nodes do. */
+int aloam_forward_mapping_input(aloam_ctx* src, aloam_ctx* dst);
 
 /* ---- lower-level entry points (tests, tools) -------------------------------------- */
 /* Residuals (3 per factor; plane types fill 1) and the tangent-space Jacobian

@@ -55,7 +55,8 @@ def _declare(L):
     L.aloam_knn.argtypes = [vp, F, C.c_int, F, C.c_int, C.c_int, C.c_float, I, F]
     L.aloam_set_profiling.argtypes = [vp, C.c_int]
     L.aloam_get_timing.argtypes = [vp, C.POINTER(abi.Timing)]
-    for name in ("aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
+    L.aloam_forward_mapping_input.argtypes = [vp, vp]
+    for name in ("aloam_forward_mapping_input", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
                  "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
                  "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
                  "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing"):
@@ -79,6 +80,7 @@ EXPORTED_SYMBOLS = [
     "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
     "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
     "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing",
+    "aloam_forward_mapping_input",
 ]
 
 
@@ -192,14 +194,20 @@ class Context:
         return b[:min(c.n, cap)].copy()
 
     # ---- whole pipeline ----
-    def process_scan(self, pts=None, device_ptr=None, n=None):
+    def process_scan(self, pts=None, device_ptr=None, n=None, mapping=True):
         o, m = abi.OdomResult(), abi.MapResult()
+        fl = 0 if mapping else abi.ALOAM_NO_MAPPING
         if device_ptr is not None:
-            self._check(lib().aloam_process_scan(self.h, C.c_void_p(device_ptr), int(n), abi.ALOAM_INPUT_DEVICE, C.byref(o), C.byref(m)))
+            self._check(lib().aloam_process_scan(self.h, C.c_void_p(device_ptr), int(n), abi.ALOAM_INPUT_DEVICE | fl,
+                                                 C.byref(o), C.byref(m)))
         else:
             pts = np.ascontiguousarray(pts, np.float32)
-            self._check(lib().aloam_process_scan(self.h, pts.ctypes.data_as(C.c_void_p), len(pts), 0, C.byref(o), C.byref(m)))
+            self._check(lib().aloam_process_scan(self.h, pts.ctypes.data_as(C.c_void_p), len(pts), fl, C.byref(o), C.byref(m)))
         return abi.odom_to_dict(o), abi.map_to_dict(m)
+
+    def forward_mapping_input(self, dst):
+        """Hand this context's published odometry output to `dst`'s laserMapping (device to device)."""
+        self._check(lib().aloam_forward_mapping_input(self.h, dst.h))
 
     # ---- low level ----
     def eval_factors(self, factors, x, robust=True):
@@ -239,3 +247,53 @@ class Context:
         t = abi.Timing()
         self._check(lib().aloam_get_timing(self.h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
+
+
+class Pipeline:
+    """The reference's node split on one GPU: scanRegistration + laserOdometry on a front-end context
+    and laserMapping on a back-end context (each with its own HIP stream), so scan k's mapping runs
+    while scan k+1 goes through the front end — what the three ROS processes do concurrently
+    (src/scanRegistration.cpp, src/laserOdometry.cpp, src/laserMapping.cpp:934 `process` thread).
+    Results are the same as Context.process_scan's, one mapping result behind."""
+
+    def __init__(self, params=None, device=0):
+        from concurrent.futures import ThreadPoolExecutor
+        self.front = Context(params, device)
+        self.back = Context(params, device)
+        self._pool = ThreadPoolExecutor(max_workers=1)   # ctypes calls release the GIL
+        self._pending = None
+        self._profiling = False
+        self.last_back_timing = None
+
+    def set_profiling(self, on):
+        self.front.set_profiling(on)
+        self.back.set_profiling(on)
+        self._profiling = bool(on)
+
+    def _map_job(self):
+        mp = self.back.mapping()
+        return mp, (self.back.timing() if self._profiling else None)
+
+    def push(self, pts=None, device_ptr=None, n=None):
+        """Front end of the new scan, overlapped with the previous scan's mapping.
+        Returns (odometry result of this scan, mapping result of the previous published scan or None)."""
+        od, _ = self.front.process_scan(pts, device_ptr, n, mapping=False)
+        mp = self.flush()
+        if od["publish_to_mapping"]:
+            self.front.forward_mapping_input(self.back)
+            self._pending = self._pool.submit(self._map_job)
+        return od, mp
+
+    def flush(self):
+        """Mapping result of the last pushed scan (or None)."""
+        if self._pending is None:
+            return None
+        mp, self.last_back_timing = self._pending.result()
+        self._pending = None
+        return mp
+
+    def close(self):
+        self.flush()
+        self._pool.shutdown()
+        self.front.close()
+        self.back.close()

@@ -15,6 +15,7 @@ ALOAM_E_SCAN_LINES = -4
 ALOAM_E_STATE = -5
 ALOAM_E_NODEVICE = -6
 ALOAM_INPUT_DEVICE = 1
+ALOAM_NO_MAPPING = 2
 ALOAM_MAX_ROUNDS = 16
 
 

@@ -91,6 +91,11 @@ static void allocate(Ctx& C) {
     C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);
     C.d_lm = (LMState*)dalloc(C, sizeof(LMState));
     C.d_partials = (double*)dalloc(C, sizeof(double) * 512 * 32);
+    C.d_coop_part = (double*)dalloc(C, sizeof(double) * 2 * 64 * 32);
+    C.d_bar = (unsigned*)dalloc(C, sizeof(unsigned) * 4);
+    HIPCHK(hipHostMalloc((void**)&C.h_bar_err, sizeof(int) * 4, hipHostMallocMapped));   // read at every sync, no copy
+    std::memset(C.h_bar_err, 0, sizeof(int) * 4);
+    HIPCHK(hipHostGetDevicePointer((void**)&C.d_bar_err, C.h_bar_err, 0));
     C.d_lm_sum = (aloam_lm_summary*)dalloc(C, sizeof(aloam_lm_summary) * 2 * ALOAM_MAX_ROUNDS);
     C.d_round_cnt = (int*)dalloc(C, sizeof(int) * 4 * ALOAM_MAX_ROUNDS);
     C.d_last_n = (int*)dalloc(C, sizeof(int) * 2);
@@ -139,7 +144,14 @@ static void allocate(Ctx& C) {
     C.ev_ready = true;
 }
 
-static void sync(Ctx& C) { HIPCHK(hipStreamSynchronize(C.stream)); }
+static void sync(Ctx& C) {
+    HIPCHK(hipStreamSynchronize(C.stream));
+    if (*(volatile int*)C.h_bar_err) {   // a solver grid barrier timed out: reset it and report (results void)
+        HIPCHK(hipMemset(C.d_bar, 0, sizeof(unsigned) * 4));
+        *(volatile int*)C.h_bar_err = 0;
+        throw ApiError{ALOAM_E_HIP, "LM grid barrier timed out (workgroups not co-resident)"};
+    }
+}
 
 static float ev_ms(Ctx& C, int a, int b) {
     float ms = 0.f;
@@ -362,6 +374,7 @@ aloam_ctx* aloam_create(const aloam_params* p, int device) {
     } catch (const HipError& e) {
         g_create_err = e.msg;
         for (auto& b : C->bufs) (void)hipFree(b.p);
+        if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
         delete C;
         return nullptr;
     }
@@ -376,6 +389,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->stream) (void)hipStreamSynchronize(C->stream);
     if (C->ev_ready) for (int i = 0; i < Ctx::NEV; i++) (void)hipEventDestroy(C->ev[i]);
     for (auto& b : C->bufs) (void)hipFree(b.p);
+    if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
     if (C->stream) (void)hipStreamDestroy(C->stream);
     delete C;
 }
@@ -535,8 +549,31 @@ int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags, aloa
     aloam_odom_result od{};
     do_odometry(C, &od);
     if (o) *o = od;
-    if (od.publish_to_mapping) do_mapping(C, m);
+    if (od.publish_to_mapping && !(flags & ALOAM_NO_MAPPING)) do_mapping(C, m);
     else if (m) std::memset(m, 0, sizeof(*m));
+    API_END
+}
+
+int aloam_forward_mapping_input(aloam_ctx* src, aloam_ctx* dst) {
+    if (!src || src == dst) return ALOAM_E_ARG;
+    Ctx& S = *(Ctx*)src;
+    API_BEGIN(dst)
+    if (S.device != C.device) throw ApiError{ALOAM_E_ARG, "contexts on different devices"};
+    if (!S.have_map_input) throw ApiError{ALOAM_E_STATE, "source has no published odometry output"};
+    if (S.n_map_corner_in > MAXL * LINE_LSHARP_CAP || S.n_map_surf_in > C.cap_in || S.n_map_full_in > C.cap_in)
+        throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
+    hipStream_t st = C.stream;   // the source's stream is idle: its API calls return synchronised
+    if (S.n_map_corner_in) HIPCHK(hipMemcpyAsync(C.d_map_corner_in, S.d_map_corner_in, sizeof(float4) * S.n_map_corner_in, hipMemcpyDeviceToDevice, st));
+    if (S.n_map_surf_in) HIPCHK(hipMemcpyAsync(C.d_map_surf_in, S.d_map_surf_in, sizeof(float4) * S.n_map_surf_in, hipMemcpyDeviceToDevice, st));
+    if (S.n_map_full_in) HIPCHK(hipMemcpyAsync(C.d_map_full_in, S.d_map_full_in, sizeof(float4) * S.n_map_full_in, hipMemcpyDeviceToDevice, st));
+    C.n_map_corner_in = S.n_map_corner_in; C.n_map_surf_in = S.n_map_surf_in; C.n_map_full_in = S.n_map_full_in;
+    set_counts2(C, C.d_map_in_n, C.n_map_corner_in, C.n_map_surf_in);
+    for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = S.h_map.q_wodom[k];
+    for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = S.h_map.t_wodom[k];
+    HIPCHK(hipMemcpyAsync((char*)C.d_map + offsetof(MapState, q_wodom), C.h_map.q_wodom, sizeof(double) * 7, hipMemcpyHostToDevice, st));
+    sync(C);
+    C.have_map_input = true;
+    S.have_map_input = false;
     API_END
 }
 

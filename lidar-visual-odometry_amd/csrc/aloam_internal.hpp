@@ -126,6 +126,10 @@ struct Ctx {
     int cap_factors = 0;
     LMState* d_lm = nullptr;
     double* d_partials = nullptr;
+    double* d_coop_part = nullptr;  // 2 x 64 x 29 doubles (LM pass partials, double-buffered)
+    unsigned* d_bar = nullptr;       // grid barrier {count, generation}
+    int* d_bar_err = nullptr;        // set if a grid barrier timed out (device view of h_bar_err)
+    int* h_bar_err = nullptr;        // mapped pinned host word
     aloam_lm_summary* d_lm_sum = nullptr;   // [ALOAM_MAX_ROUNDS]
     int* d_round_cnt = nullptr;             // [ALOAM_MAX_ROUNDS][2] correspondences per round
 

@@ -18,7 +18,6 @@ namespace aloam {
 
 constexpr int LB = 256;          // threads per LM workgroup
 constexpr int NACC = 29;         // 21 JtJ + 6 Jtr + cost + residual-block count
-constexpr int LM_MAX_BLOCKS = 512;
 
 // residual and 6-column tangent Jacobian of one factor at (q, t). Returns #residuals (0 = invalid).
 __device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
@@ -134,8 +133,10 @@ __device__ __forceinline__ void plus7(const double* x, const double* d, double* 
     const double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
     dquat q{x[0], x[1], x[2], x[3]};
     if (nd > 0.0) {
-        const double sdd = sin(nd) / nd;
-        dquat dq{sdd * d[0], sdd * d[1], sdd * d[2], cos(nd)};
+        double sn, cs;
+        sincos(nd, &sn, &cs);
+        const double sdd = sn / nd;
+        dquat dq{sdd * d[0], sdd * d[1], sdd * d[2], cs};
         dquat r = qmul(dq, q);
         out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
     } else { out[0] = q.x; out[1] = q.y; out[2] = q.z; out[3] = q.w; }
@@ -149,6 +150,11 @@ __device__ __forceinline__ double norm7(const double* a) {
     return sqrt(s);
 }
 __device__ __forceinline__ double grad_max_norm(const double* x, const double* g) {
+    // translation part of x - Plus(x, -g) is g_t up to one rounding of x_t (< 1e-10 for |x_t| < 1e5):
+    // when it alone already fails the 1e-10 gradient tolerance, skip the sincos of Plus.
+    const double gt = fmax(fabs(g[3]), fmax(fabs(g[4]), fabs(g[5])));
+    const double xt = fmax(fabs(x[4]), fmax(fabs(x[5]), fabs(x[6])));
+    if (gt > 1e-9 && xt < 1e5) return gt;
     double ng[6], xp[7];
 #pragma unroll
     for (int i = 0; i < 6; i++) ng[i] = -g[i];
@@ -163,7 +169,7 @@ __device__ __forceinline__ double Aget(const double* A, int a, int b) {   // upp
     return A[a * 6 - a * (a - 1) / 2 + (b - a)];
 }
 __device__ __forceinline__ bool chol_solve6(double M[6][6], const double* rhs, double* y) {
-    double L[6][6];
+    double L[6][6], inv[6];
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 6; j++) {
@@ -172,12 +178,13 @@ __device__ __forceinline__ bool chol_solve6(double M[6][6], const double* rhs, d
         for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
         ok = ok && (s > 0.0);
         L[j][j] = sqrt(s);
+        inv[j] = 1.0 / L[j][j];            // one division per column; the rest multiply
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
             double v = M[i][j];
 #pragma unroll
             for (int k = 0; k < j; k++) v -= L[i][k] * L[j][k];
-            L[i][j] = v / L[j][j];
+            L[i][j] = v * inv[j];
         }
     }
     double z[6];
@@ -186,14 +193,14 @@ __device__ __forceinline__ bool chol_solve6(double M[6][6], const double* rhs, d
         double v = rhs[i];
 #pragma unroll
         for (int k = 0; k < i; k++) v -= L[i][k] * z[k];
-        z[i] = v / L[i][i];
+        z[i] = v * inv[i];
     }
 #pragma unroll
     for (int i = 5; i >= 0; i--) {
         double v = z[i];
 #pragma unroll
         for (int k = i + 1; k < 6; k++) v -= L[k][i] * y[k];
-        y[i] = v / L[i][i];
+        y[i] = v * inv[i];
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) ok = ok && isfinite(y[i]);
@@ -322,127 +329,172 @@ __device__ __forceinline__ void lm_tail(LMState* st, const double* tot, int pass
     lm_next_step(st, out, max_iter);
 }
 
-// block-wide sum of NACC doubles per thread into tot[] (fixed tree => deterministic)
-template <int NT>
-__device__ __forceinline__ void block_reduce_acc(const double* acc, double (*sh)[NACC], double* tot) {
-    const int w = threadIdx.x / WAVE;
-#pragma unroll
-    for (int i = 0; i < NACC; i++) {
-        double v = wave_sum_d(acc[i]);
-        if (lane_id() == 0) sh[w][i] = v;
+// Sum of NACC doubles over `nrows` rows of an LDS table rows[r*NACC + i] into tot[] (fixed order =>
+// deterministic): 8 x NACC threads each add every 8th row of one column, then NACC threads add the
+// 8 partials. Independent LDS loads, no shuffle dependency chains (the 29 chained wave reductions
+// this replaces cost ~6 us per pass).
+__device__ __forceinline__ void reduce_rows(const double* rows, int nrows, double* part8, double* tot) {
+    const int j = threadIdx.x;
+    if (j < 8 * NACC) {
+        const int i = j % NACC, c = j / NACC;
+        double s0 = 0, s1 = 0;
+        int r = c;
+        for (; r + 8 < nrows; r += 16) { s0 += rows[r * NACC + i]; s1 += rows[(r + 8) * NACC + i]; }
+        if (r < nrows) s0 += rows[r * NACC + i];
+        part8[c * NACC + i] = s0 + s1;
     }
     __syncthreads();
-    if (threadIdx.x < NACC) {
+    if (j < NACC) {
         double s = 0;
-        for (int ww = 0; ww < NT / WAVE; ww++) s += sh[ww][threadIdx.x];
-        tot[threadIdx.x] = s;
+#pragma unroll
+        for (int c = 0; c < 8; c++) s += part8[c * NACC + j];
+        tot[j] = s;
     }
     __syncthreads();
 }
-
-// Multi-workgroup pass (large problems: mapping). The last workgroup to arrive reduces the
-// per-workgroup partials — one workgroup per thread, then the same block tree — and runs the LM tail.
-__global__ void __launch_bounds__(LB) k_lm_pass(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
-                                                double* partials, aloam_lm_summary* out, int pass, int max_iter,
-                                                const int* gate) {
-    __shared__ double sh[LB / WAVE][NACC];
-    __shared__ double tot[NACC];
-    __shared__ int last;
-    if (gate && *gate == 0) return;                  // mapping skipped (laserMapping.cpp:554)
-    if (pass > 0 && st->done) return;
-    const double* xs = pass == 0 ? xp : st->cand;
-    const dquat q{xs[0], xs[1], xs[2], xs[3]};
-    const double t[3] = {xs[4], xs[5], xs[6]};
-    double acc[NACC];
+// block-wide sum of NACC doubles per thread (NT >= 8 * NACC threads); rows = NT*NACC LDS doubles
+template <int NT>
+__device__ __forceinline__ void block_reduce_acc(const double* acc, double* rows, double* part8, double* tot) {
+    static_assert(NT >= 8 * NACC, "reduce_rows needs 8*NACC threads");
 #pragma unroll
-    for (int i = 0; i < NACC; i++) acc[i] = 0;
-    for (int i = blockIdx.x * LB + threadIdx.x; i < nslots; i += gridDim.x * LB) accumulate(f[i], q, t, acc);
-    block_reduce_acc<LB>(acc, sh, tot);
-    if (threadIdx.x < NACC)
-        __hip_atomic_store((unsigned long long*)&partials[blockIdx.x * NACC + threadIdx.x], __double_as_longlong(tot[threadIdx.x]),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < NACC; i++) rows[threadIdx.x * NACC + i] = acc[i];
+    __syncthreads();
+    reduce_rows(rows, NT, part8, tot);
+}
+
+// Grid barrier for the persistent multi-workgroup solver (count + generation; the last arriver
+// resets the count, so consecutive launches with different grid sizes need no re-initialisation).
+// Bounded spin: a barrier that does not complete flags an error instead of hanging the queue.
+__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned nblocks, int* err) {
+    // All cross-workgroup data (partials, counters) moves through agent-scope RELAXED atomics, which
+    // are coherent across XCDs on their own; ordering is by completion (s_waitcnt vmcnt(0) before
+    // the next access). Acquire/release here would add an L2 writeback + invalidate per poll.
+    __shared__ int ok;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned prev = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (prev == gridDim.x - 1);
+        ok = 1;
+        const unsigned gen = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (arrived == nblocks - 1) {
+            const unsigned r = __hip_atomic_fetch_sub(&bar[0], nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&bar[1], 1u + 0u * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            int spins = 0;
+            while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 22)) { ok = 0; atomicExch(err, 1); break; }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (!last) return;
-    // every thread loads one workgroup's 29 partials (independent sc1 loads in flight)
-    double pacc[NACC];
-#pragma unroll
-    for (int i = 0; i < NACC; i++) pacc[i] = 0;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += LB) {
-#pragma unroll
-        for (int i = 0; i < NACC; i++)
-            pacc[i] += __longlong_as_double(__hip_atomic_load((unsigned long long*)&partials[b * NACC + i],
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    block_reduce_acc<LB>(pacc, sh, tot);
-    __shared__ LMState ls;
-    {   // state -> LDS (all threads, 8-byte words), tail in LDS, LDS -> state
-        const int nw = sizeof(LMState) / 8;
-        for (int i = threadIdx.x; i < nw; i += LB) ((unsigned long long*)&ls)[i] = ((const unsigned long long*)st)[i];
-        __syncthreads();
-        if (threadIdx.x == 0) { ls.ticket = 0; lm_tail(&ls, tot, pass, xp, out, max_iter); }
-        __syncthreads();
-        for (int i = threadIdx.x; i < nw; i += LB) ((unsigned long long*)st)[i] = ((const unsigned long long*)&ls)[i];
-    }
+    return ok;
 }
 
-// Whole Solve in ONE workgroup (small problems: odometry, <= a few thousand residual blocks):
-// every pass = all 1024 threads evaluate, block-reduce in LDS, thread 0 runs the LM tail.
-constexpr int LS = 512;
-__global__ void __launch_bounds__(LS) k_lm_solve_wg(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
-                                                    aloam_lm_summary* out, int max_iter, const int* gate) {
-    __shared__ double sh[LS / WAVE][NACC];
+// Whole Solve as ONE persistent launch over G workgroups: each pass evaluates its slice, publishes
+// a 29-double partial, meets the others at a grid barrier, then EVERY workgroup reduces the G
+// partials in the same fixed order and runs the identical LM tail on its own LDS copy of the state
+// (bitwise-identical on all workgroups, so no broadcast and one barrier per pass).
+constexpr int CB = 256;
+constexpr int LM_COOP_MAX = 64;
+constexpr int LM_CACHE = 1024;                      // factor slots per workgroup kept in LDS (80 KB)
+#ifdef ALOAM_LM_TIMING
+__device__ unsigned long long g_lm_ts[8][5];   // micro-benchmark only: block-0 phase stamps per pass
+#define LM_TS(p, k) do { if (blockIdx.x == 0 && threadIdx.x == 0 && (p) < 8) g_lm_ts[p][k] = wall_clock64(); } while (0)
+#else
+#define LM_TS(p, k) do { } while (0)
+#endif
+__global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
+                                                double* partials, unsigned* bar, int* err, aloam_lm_summary* out,
+                                                int max_iter, const int* gate) {
+    __shared__ double rows[CB * NACC];
+    __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
+    __shared__ double xl[7];
     __shared__ int done;
-    __shared__ double xs[7];
-    __shared__ LMState ls;                     // the whole Solve keeps its state in LDS
-    if (gate && *gate == 0) return;
+    __shared__ LMState ls;
+    extern __shared__ aloam_factor fcache[];        // this workgroup's contiguous slice of factor slots
+    if (gate && *gate == 0) return;                 // mapping skipped (laserMapping.cpp:554)
+    const unsigned G = gridDim.x;
+    const int per = (nslots + G - 1) / G;
+    const int f0 = blockIdx.x * per, f1 = min(nslots, f0 + per);
+    const bool cached = per <= LM_CACHE;            // slots read from HBM once, then from LDS
+    if (threadIdx.x < 7) xl[threadIdx.x] = xp[threadIdx.x];
+    __syncthreads();
     for (int pass = 0; pass <= max_iter; pass++) {
-        if (threadIdx.x < 7) xs[threadIdx.x] = pass == 0 ? xp[threadIdx.x] : ls.cand[threadIdx.x];
-        __syncthreads();
+        const double* xs = pass == 0 ? xl : ls.cand;
         const dquat q{xs[0], xs[1], xs[2], xs[3]};
         const double t[3] = {xs[4], xs[5], xs[6]};
         double acc[NACC];
 #pragma unroll
         for (int i = 0; i < NACC; i++) acc[i] = 0;
-        for (int i = threadIdx.x; i < nslots; i += LS) accumulate(f[i], q, t, acc);
-        block_reduce_acc<LS>(acc, sh, tot);
+        if (!cached) {
+            for (int i = f0 + threadIdx.x; i < f1; i += CB) accumulate(f[i], q, t, acc);
+        } else if (pass == 0) {
+            for (int i = f0 + threadIdx.x; i < f1; i += CB) { const aloam_factor fi = f[i]; fcache[i - f0] = fi; accumulate(fi, q, t, acc); }
+        } else {
+            for (int i = threadIdx.x; i < f1 - f0; i += CB) accumulate(fcache[i], q, t, acc);
+        }
+        LM_TS(pass, 4);
+        block_reduce_acc<CB>(acc, rows, part8, tot);
+        LM_TS(pass, 0);
+        double* part = partials + (size_t)(pass & 1) * LM_COOP_MAX * NACC;
+        if (threadIdx.x < NACC)
+            __hip_atomic_store((unsigned long long*)&part[blockIdx.x * NACC + threadIdx.x], __double_as_longlong(tot[threadIdx.x]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!grid_barrier(bar, G, err)) return;
+        LM_TS(pass, 1);
+        for (int i = threadIdx.x; i < (int)G * NACC; i += CB)     // all partials -> LDS in one round trip
+            rows[i] = __longlong_as_double(__hip_atomic_load((unsigned long long*)&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __syncthreads();
+        reduce_rows(rows, G, part8, tot);
+        LM_TS(pass, 2);
         if (threadIdx.x == 0) {
-            lm_tail(&ls, tot, pass, xp, out, max_iter);
+            lm_tail(&ls, tot, pass, xl, blockIdx.x == 0 ? out : nullptr, max_iter);
             done = ls.done;
         }
         __syncthreads();
+        LM_TS(pass, 3);
         if (done) break;
     }
-    (void)st;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 7) xp[threadIdx.x] = xl[threadIdx.x];
+        const int nw = sizeof(LMState) / 8;
+        for (int i = threadIdx.x; i < nw; i += CB) ((unsigned long long*)st)[i] = ((const unsigned long long*)&ls)[i];
+    }
 }
 
-static int lm_blocks(int nslots) { return std::max(1, std::min(LM_MAX_BLOCKS, (nslots + LB - 1) / LB)); }
-
 // one Ceres Solve over nslots factor slots; `gate` (device int, may be null) disables the solve.
-// Small problems run in one persistent workgroup, large ones as max_iter + 1 grid-wide passes.
-constexpr int LM_SINGLE_WG_MAX = 6144;
 void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate) {
     aloam_lm_summary* out = C.d_lm_sum + round;
-    if (nslots <= LM_SINGLE_WG_MAX) {
-        k_lm_solve_wg<<<1, LS, 0, C.stream>>>(d_f, nslots, d_x, C.d_lm, out, C.P.max_solver_iterations, gate);
-    } else {
-        const int nb = lm_blocks(nslots);
-        for (int pass = 0; pass <= C.P.max_solver_iterations; pass++)
-            k_lm_pass<<<nb, LB, 0, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_partials, out, pass, C.P.max_solver_iterations, gate);
+    // >= 2 slots per thread keeps a pass's evaluation well above the barrier cost; <= LM_CACHE slots
+    // per workgroup lets every pass after the first read the slots from LDS
+    static const int spt = getenv("ALOAM_LM_SPT") ? std::max(1, atoi(getenv("ALOAM_LM_SPT"))) : 2;   // tuning knob
+    int G = std::max((nslots + spt * CB - 1) / (spt * CB), (nslots + LM_CACHE - 1) / LM_CACHE);
+    G = std::max(1, std::min(LM_COOP_MAX, G));
+    const int per = (nslots + G - 1) / G;
+    const size_t lds = per <= LM_CACHE ? sizeof(aloam_factor) * (size_t)per : 0;
+    static bool attr = false;
+    if (!attr) {   // static rows (59 KB) + up to 80 KB of cached slots: above the default dynamic limit
+        HIPCHK(hipFuncSetAttribute((const void*)k_lm_coop, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(sizeof(aloam_factor) * LM_CACHE)));
+        attr = true;
     }
+    k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_coop_part, C.d_bar, C.d_bar_err, out,
+                                      C.P.max_solver_iterations, gate);
     HIPCHK(hipGetLastError());
 }
 
 // ---- test entry: per-factor residuals / Jacobians and the normal equations ----
 __global__ void k_eval_factors(const aloam_factor* __restrict__ f, int n, const double* x, int robust, double* res,
                                double* jac, double* neq) {
-    __shared__ double sh[LB / WAVE][NACC];
+    __shared__ double rows[LB * NACC];
+    __shared__ double part8[8 * NACC];
+    __shared__ double tot[NACC];
     const dquat q{x[0], x[1], x[2], x[3]};
     const double t[3] = {x[4], x[5], x[6]};
     double acc[NACC];
@@ -467,10 +519,8 @@ __global__ void k_eval_factors(const aloam_factor* __restrict__ f, int n, const 
             for (int a = 0; a < 6; a++) acc[21 + a] += Js[k][a] * rs[k];
         }
     }
-    const int w = threadIdx.x / WAVE;
-    for (int i = 0; i < NACC; i++) { double v = wave_sum_d(acc[i]); if (lane_id() == 0) sh[w][i] = v; }
-    __syncthreads();
-    if (threadIdx.x < 28) { double s = 0; for (int ww = 0; ww < LB / WAVE; ww++) s += sh[ww][threadIdx.x]; neq[threadIdx.x] = s; }
+    block_reduce_acc<LB>(acc, rows, part8, tot);
+    if (threadIdx.x < 28) neq[threadIdx.x] = tot[threadIdx.x];
 }
 
 void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq) {
