@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle_binding as ob
-from lvo_amd_loader import abi, synth
+from lvo_amd_loader import abi, lvo, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -48,8 +48,6 @@ def test_scan_registration_edge_cases(gpu_ctx_factory):
     bad = pts.copy()
     bad[::97, 0] = np.nan
     bad[5::101, :3] *= 0.001
-    for p in (abi.default_params(16),):
-        p.input_is_dense = 0
     ctx2 = gpu_ctx_factory(16, input_is_dense=0)
     p = abi.default_params(16)
     p.input_is_dense = 0
@@ -64,6 +62,13 @@ def test_scan_registration_edge_cases(gpu_ctx_factory):
     assert_features_equal(ctx.features(), orc.features())
     ctx.scan_registration(pts[:0])
     assert ctx.feature_counts() == [0, 0, 0, 0, 0]
+
+
+def test_unsupported_scan_lines_is_an_error(gpu_ctx_factory):
+    """scanRegistration.cpp:201-205 aborts on N_SCANS outside {16, 32, 64}: an error code here."""
+    ctx = gpu_ctx_factory(40, generic_scan_lines=0)
+    with pytest.raises(lvo.ALOAMError):
+        ctx.scan_registration(synth.scan("vlp16", 0))
 
 
 def test_tied_curvatures_follow_std_sort(gpu_ctx_factory):
