@@ -20,7 +20,7 @@ from . import _abi as abi  # noqa: F401
 from . import synth  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "libaloam_hip.so")
+LIB_PATH = os.environ.get("ALOAM_LIB_PATH") or os.path.join(_HERE, "csrc", "libaloam_hip.so")   # override: profiling builds only
 _lib = None
 
 

@@ -222,6 +222,164 @@ __device__ __forceinline__ int wave_knn_rows(const float ox, const float oy, con
     }
     return found;
 }
+// Exact radius k-NN of one query by ONE THREAD over the 3x3x3 cell block (m = 1): the 9 (y, z)
+// rows of 3 cells are 9 contiguous point ranges, their bounds loaded together; candidates stream
+// 4 at a time (point + index loads in flight) into a sorted top-K keyed by (d2, index) — the same
+// total order as the wave version, hence the same neighbours in the same order. For sparse
+// neighbourhoods (the mapping stacks see ~10-60 candidates) this beats a wave per query.
+template <int K>
+__device__ __forceinline__ int thread_knn27(const float ox, const float oy, const float oz, const float inv_cell,
+                                            const int gdx, const int gdy, const int gdz,
+                                            const int* __restrict__ start, const float4* __restrict__ spts,
+                                            const int* __restrict__ sidx, float qx, float qy, float qz, float r2,
+                                            int* out_pos, float* out_d2, int* out_idx, int* ncand) {
+    const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gdx - 1);
+    int rb[9], re[9];
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
+        const bool ok = x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
+        const int c = (z * gdy + y) * gdx;
+        rb[r] = ok ? start[c + x0] : 0;
+        re[r] = ok ? start[c + x1 + 1] : 0;
+    }
+    float bd[K];
+    int bi[K], bp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    int total = 0;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        const int e = re[r];
+        total += e - rb[r];
+        for (int p = rb[r]; p < e; p += 4) {
+            float4 v[4];
+            int id[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool in = p + u < e;
+                v[u] = in ? spts[p + u] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+                id[u] = in ? sidx[p + u] : 0x7fffffff;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+                if (!(d2 < r2)) continue;
+                if (d2 < bd[K - 1] || (d2 == bd[K - 1] && id[u] < bi[K - 1])) {
+                    float nd = d2; int ni = id[u], np = p + u;
+#pragma unroll
+                    for (int k = 0; k < K; k++) {
+                        const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                        if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
+                    }
+                }
+            }
+        }
+    }
+    if (ncand) *ncand = total;
+    int found = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        out_pos[k] = bp[k]; out_d2[k] = bd[k]; out_idx[k] = bi[k];
+        found += bp[k] >= 0;
+    }
+    return found;
+}
+// Exact radius k-NN of one query by a GROUP of GS aligned lanes (GS | 64) over the 3x3x3 cell
+// block: every lane loads the 9 row bounds (same addresses across the group: one coalesced round
+// trip), the rows are flattened through their prefix sums, lane l streams candidates l, l+GS, ...
+// (4 point + index loads in flight), keeps a sorted top-K by (d2, index), and K rounds of a group
+// min over 64-bit keys merge the lanes' lists. Same total order as the wave / thread versions.
+// Every lane returns the same result.
+template <int K, int GS>
+__device__ __forceinline__ int group_knn27(const float ox, const float oy, const float oz, const float inv_cell,
+                                           const int gdx, const int gdy, const int gdz,
+                                           const int* __restrict__ start, const float4* __restrict__ spts,
+                                           const int* __restrict__ sidx, float qx, float qy, float qz, float r2, bool active,
+                                           int* out_pos, float* out_d2, int* out_idx, int* ncand) {
+    const int gl = lane_id() & (GS - 1);
+    int rb[9], pre[10];
+    pre[0] = 0;
+    {
+        const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
+        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gdx - 1);
+        int re[9];
+#pragma unroll
+        for (int r = 0; r < 9; r++) {
+            const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
+            const bool ok = active && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
+            const int c = (z * gdy + y) * gdx;
+            rb[r] = ok ? start[c + x0] : 0;
+            re[r] = ok ? start[c + x1 + 1] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < 9; r++) pre[r + 1] = pre[r] + (re[r] - rb[r]);
+    }
+    const int total = pre[9];
+    if (ncand) *ncand = total;
+    float bd[K];
+    int bi[K], bp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    for (int t0 = gl; t0 < total; t0 += 4 * GS) {
+        float4 v[4];
+        int id[4], ps[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = t0 + u * GS;
+            int p = -1;
+            if (t < total) {
+                int base = rb[0] - pre[0];
+#pragma unroll
+                for (int r = 1; r < 9; r++) if (t >= pre[r]) base = rb[r] - pre[r];
+                p = base + t;
+            }
+            ps[u] = p;
+            v[u] = p >= 0 ? spts[p] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+            id[u] = p >= 0 ? sidx[p] : 0x7fffffff;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+            if (!(ps[u] >= 0 && d2 < r2)) continue;
+            if (d2 < bd[K - 1] || (d2 == bd[K - 1] && id[u] < bi[K - 1])) {
+                float nd = d2; int ni = id[u], np = ps[u];
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                    if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
+                }
+            }
+        }
+    }
+    // merge: K rounds of a group-wide min over the lanes' heads
+    int head = 0, found = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
+#pragma unroll
+        for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
+        const unsigned long long key = hp < 0 ? ~0ull : dist_key(hd, hi);
+        unsigned long long mn = key;
+#pragma unroll
+        for (int o = 1; o < GS; o <<= 1) {
+            const unsigned long long t = __shfl_xor(mn, o, WAVE);
+            mn = t < mn ? t : mn;
+        }
+        // the owner of the minimum (unique: indices are unique) publishes its position
+        const bool mine = key == mn && mn != ~0ull;
+        int pos = mine ? hp : -1;
+#pragma unroll
+        for (int o = 1; o < GS; o <<= 1) pos = max(pos, __shfl_xor(pos, o, WAVE));
+        if (mine) head++;
+        out_pos[k] = pos;
+        out_d2[k] = mn == ~0ull ? INFINITY : __uint_as_float((unsigned)(mn >> 32));
+        out_idx[k] = mn == ~0ull ? -1 : (int)(mn & 0xffffffffu);
+        found += mn != ~0ull;
+    }
+    return found;
+}
 // PCL 1.8 VoxelGrid leaf grid from an ordered-int bbox (voxel_grid.cpp applyFilter)
 __device__ inline void voxel_params(const unsigned* bb, float leaf, bool* overflow, int minb[3], int* mul1, int* mul2) {
     const float inv = 1.0f / leaf;

@@ -199,7 +199,8 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);
 void odom_compose(Ctx& C);
-void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* d_nslots);
+// nslots = host upper bound; d_nslots2 (optional, device int[2]) = live slots as a sum of two counts
+void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2 = nullptr);
 void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq);
 void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2);
 size_t voxel_sort_tmp_bytes(int cap);

@@ -410,7 +410,7 @@ __device__ unsigned long long g_lm_ts[8][5];   // micro-benchmark only: block-0 
 #endif
 __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
                                                 double* partials, unsigned* bar, int* err, aloam_lm_summary* out,
-                                                int max_iter, const int* gate) {
+                                                int max_iter, const int* gate, const int* dn, int cache_cap) {
     __shared__ double rows[CB * NACC];
     __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
@@ -419,10 +419,11 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
     __shared__ LMState ls;
     extern __shared__ aloam_factor fcache[];        // this workgroup's contiguous slice of factor slots
     if (gate && *gate == 0) return;                 // mapping skipped (laserMapping.cpp:554)
+    if (dn) nslots = min(nslots, dn[0] + dn[1]);    // live slot count known on the device only
     const unsigned G = gridDim.x;
     const int per = (nslots + G - 1) / G;
     const int f0 = blockIdx.x * per, f1 = min(nslots, f0 + per);
-    const bool cached = per <= LM_CACHE;            // slots read from HBM once, then from LDS
+    const bool cached = per <= cache_cap;           // slots read from HBM once, then from LDS
     if (threadIdx.x < 7) xl[threadIdx.x] = xp[threadIdx.x];
     __syncthreads();
     for (int pass = 0; pass <= max_iter; pass++) {
@@ -469,7 +470,7 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
 }
 
 // one Ceres Solve over nslots factor slots; `gate` (device int, may be null) disables the solve.
-void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate) {
+void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2) {
     aloam_lm_summary* out = C.d_lm_sum + round;
     // >= 2 slots per thread keeps a pass's evaluation well above the barrier cost; <= LM_CACHE slots
     // per workgroup lets every pass after the first read the slots from LDS
@@ -485,7 +486,7 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
         attr = true;
     }
     k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_coop_part, C.d_bar, C.d_bar_err, out,
-                                      C.P.max_solver_iterations, gate);
+                                      C.P.max_solver_iterations, gate, d_nslots2, lds ? per : 0);
     HIPCHK(hipGetLastError());
 }
 

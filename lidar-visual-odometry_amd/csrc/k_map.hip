@@ -101,97 +101,117 @@ __global__ void k_map_gate(MapState* m, const GridDesc* gc, const GridDesc* gs) 
     m->optimize = (gc->n > 10 && gs->n > 50) ? 1 : 0;
 }
 
-// one wave per stack point: 5-NN within 1 m (d^2[4] < 1.0, :583-584,649-650)
-__global__ void __launch_bounds__(256) k_map_knn5(
-    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n, int ub_c, int ub_s,
-    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
-    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    const MapState* __restrict__ m, int* __restrict__ nbr, unsigned long long* cand_count) {
-    __shared__ RowSet<9> rows9[256 / WAVE];
-    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-    if (qi >= ub_c + ub_s) return;
-    if (!m->optimize) return;
-    const bool corner = qi < ub_c;
-    const int li = corner ? qi : qi - ub_c;
-    int* out = nbr + (size_t)qi * 5;
-    if (li >= stack_n[corner ? 0 : 1]) { if (lane_id() == 0) out[0] = -1; return; }
-    const float4 sel = associate_to_map(m->parameters, corner ? cstack[li] : sstack[li]);
-    const GridDesc gd = corner ? *gdc : *gds;
-    const int* cs = corner ? cs_c : cs_s;
-    const float4* sp = corner ? sp_c : sp_s;
-    const int* si = corner ? si_c : si_s;
-    int res[5], ri[5], ncand = 0;
-    float rd[5];
-    const int found = wave_knn_rows<5, 9>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, cs, sp, si,
-                                          sel.x, sel.y, sel.z, 1.0f, 1, res, rd, ri, &ncand, rows9[threadIdx.x / WAVE]);
-    if (lane_id() == 0) {
-        if (found == 5) for (int k = 0; k < 5; k++) out[k] = res[k];
-        else out[0] = -1;
-        if (cand_count) atomicAdd(cand_count, (unsigned long long)ncand);
+// line / plane fit of one stack point's 5 neighbours (kNN order) -> factor (:585-620, :650-686)
+__device__ __forceinline__ void fit_factor(bool corner, const float4 po, const float4* __restrict__ sp, const int* nb, aloam_factor& f) {
+    f.type = -1; f.pad = 0;
+    f.cp[0] = po.x; f.cp[1] = po.y; f.cp[2] = po.z;
+    if (corner) {
+        double pts[5][3];
+        double cx = 0, cy = 0, cz = 0;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const float4 v = sp[nb[j]];
+            pts[j][0] = v.x; pts[j][1] = v.y; pts[j][2] = v.z;
+            cx = cx + pts[j][0]; cy = cy + pts[j][1]; cz = cz + pts[j][2];
+        }
+        cx = cx / 5.0; cy = cy / 5.0; cz = cz / 5.0;
+        double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const double zm[3] = {pts[j][0] - cx, pts[j][1] - cy, pts[j][2] - cz};
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) cov[r * 3 + c] = cov[r * 3 + c] + zm[r] * zm[c];
+        }
+        double ev[3], evec[9];
+        eigen_sym3(cov, ev, evec);
+        if (ev[2] > 3 * ev[1]) {
+            const double u[3] = {evec[2], evec[5], evec[8]};
+            f.type = 0;
+            f.a[0] = 0.1 * u[0] + cx; f.a[1] = 0.1 * u[1] + cy; f.a[2] = 0.1 * u[2] + cz;
+            f.b[0] = -0.1 * u[0] + cx; f.b[1] = -0.1 * u[1] + cy; f.b[2] = -0.1 * u[2] + cz;
+        }
+    } else {
+        double A[15], b[5], P[5][3];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const float4 v = sp[nb[j]];
+            P[j][0] = v.x; P[j][1] = v.y; P[j][2] = v.z;
+            A[j * 3] = P[j][0]; A[j * 3 + 1] = P[j][1]; A[j * 3 + 2] = P[j][2];
+            b[j] = -1;
+        }
+        double n[3];
+        colpiv_qr_5x3(A, b, n);
+        const double negOA = 1 / sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        const double z = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+        if (z > 0) { const double s = sqrt(z); n[0] /= s; n[1] /= s; n[2] /= s; }
+        bool valid = true;
+#pragma unroll
+        for (int j = 0; j < 5; j++)
+            if (fabs(n[0] * P[j][0] + n[1] * P[j][1] + n[2] * P[j][2] + negOA) > 0.2) valid = false;
+        if (valid) {
+            f.type = 2;
+            f.a[0] = n[0]; f.a[1] = n[1]; f.a[2] = n[2];
+            f.b[0] = negOA; f.b[1] = 0; f.b[2] = 0;
+        }
     }
 }
 
-// one thread per stack point: line / plane fit and the factor (:585-620, :650-686)
-__global__ void k_map_fit(const float4* __restrict__ cstack, const float4* __restrict__ sstack, int ub_c, int ub_s,
-                          const float4* __restrict__ sp_c, const float4* __restrict__ sp_s, const int* __restrict__ nbr,
-                          const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt) {
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi >= ub_c + ub_s) return;
-    aloam_factor f;
-    f.type = -1; f.pad = 0;
-    if (!m->optimize) return;
-    const int* nb = nbr + (size_t)qi * 5;
+// One mapping association round, 8 lanes per stack point (corner stack, then surf stack):
+// pointAssociateToMap (:581,647), 5-NN within 1 m (d^2[4] < 1.0, :583-584,649-650) over the
+// surround map's 1.025 m grid (group_knn27), then the group's first lane fits the line / plane
+// and writes the factor record. Correspondence counts and (profiling) candidate counts are
+// aggregated per wave before the atomics.
+constexpr int AG = 8;     // lanes per query (measured best of 4 / 8 / 16 at C3)
+__global__ void __launch_bounds__(256) k_map_assoc(
+    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n, int ub_c, int ub_s,
+    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
+    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
+    const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp) {
+    // slots are compact: corner stack at [0, nc), surf stack at [nc, nc + ns) — the reference's
+    // AddResidualBlock order; the solver reads nc + ns from the device
+    // every independent load is issued up front (one round trip before the grid walk)
+    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / AG;
     const bool corner = qi < ub_c;
-    if (nb[0] >= 0) {
-        const float4 po = corner ? cstack[qi] : sstack[qi - ub_c];
-        f.cp[0] = po.x; f.cp[1] = po.y; f.cp[2] = po.z;
-        if (corner) {
-            double pts[5][3];
-            double cx = 0, cy = 0, cz = 0;
-            for (int j = 0; j < 5; j++) {
-                const float4 v = sp_c[nb[j]];
-                pts[j][0] = v.x; pts[j][1] = v.y; pts[j][2] = v.z;
-                cx = cx + pts[j][0]; cy = cy + pts[j][1]; cz = cz + pts[j][2];
-            }
-            cx = cx / 5.0; cy = cy / 5.0; cz = cz / 5.0;
-            double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            for (int j = 0; j < 5; j++) {
-                const double zm[3] = {pts[j][0] - cx, pts[j][1] - cy, pts[j][2] - cz};
-                for (int r = 0; r < 3; r++) for (int c = 0; c < 3; c++) cov[r * 3 + c] = cov[r * 3 + c] + zm[r] * zm[c];
-            }
-            double ev[3], evec[9];
-            eigen_sym3(cov, ev, evec);
-            if (ev[2] > 3 * ev[1]) {
-                const double u[3] = {evec[2], evec[5], evec[8]};
-                f.type = 0;
-                f.a[0] = 0.1 * u[0] + cx; f.a[1] = 0.1 * u[1] + cy; f.a[2] = 0.1 * u[2] + cz;
-                f.b[0] = -0.1 * u[0] + cx; f.b[1] = -0.1 * u[1] + cy; f.b[2] = -0.1 * u[2] + cz;
-            }
-        } else {
-            double A[15], b[5], P[5][3];
-            for (int j = 0; j < 5; j++) {
-                const float4 v = sp_s[nb[j]];
-                P[j][0] = v.x; P[j][1] = v.y; P[j][2] = v.z;
-                A[j * 3] = P[j][0]; A[j * 3 + 1] = P[j][1]; A[j * 3 + 2] = P[j][2];
-                b[j] = -1;
-            }
-            double n[3];
-            colpiv_qr_5x3(A, b, n);
-            const double negOA = 1 / sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-            const double z = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
-            if (z > 0) { const double s = sqrt(z); n[0] /= s; n[1] /= s; n[2] /= s; }
-            bool valid = true;
-            for (int j = 0; j < 5; j++)
-                if (fabs(n[0] * P[j][0] + n[1] * P[j][1] + n[2] * P[j][2] + negOA) > 0.2) { valid = false; break; }
-            if (valid) {
-                f.type = 2;
-                f.a[0] = n[0]; f.a[1] = n[1]; f.a[2] = n[2];
-                f.b[0] = negOA; f.b[1] = 0; f.b[2] = 0;
-            }
-        }
+    const int li = corner ? qi : qi - ub_c;
+    const int opt = m->optimize;
+    const int nc = stack_n[0], ns = stack_n[1];
+    double par[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
+    const float4 po = corner ? cstack[min(li, max(ub_c - 1, 0))] : sstack[min(li, max(ub_s - 1, 0))];
+    const GridDesc gd = corner ? *gdc : *gds;
+    if (!opt) return;
+    const bool lead = (lane_id() & (AG - 1)) == 0;
+    const bool live = qi < ub_c + ub_s && li < (corner ? nc : ns);
+    if (!__ballot(live)) return;                    // whole wave past the (downsampled) stacks
+    int type = -1, ncand = 0;
+    const float4 sel = associate_to_map(par, po);
+    const float4* sp = corner ? sp_c : sp_s;
+    int pos[5], idx[5];
+    float d2[5];
+    int found = 5;
+    if (exp & 1) { for (int k = 0; k < 5; k++) pos[k] = (li * 7 + k) % 64; }
+    else found = group_knn27<5, AG>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
+                                    corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand);
+    if (live && lead) {
+        aloam_factor f;
+        f.type = -1; f.pad = 0;
+        if (found == 5 && !(exp & 2)) fit_factor(corner, po, sp, pos, f);
+        out[corner ? li : nc + li] = f;
+        type = f.type;
     }
-    out[qi] = f;
-    if (f.type >= 0) atomicAdd(&round_cnt[corner ? 0 : 1], 1);
+    // wave-aggregated counters
+    const unsigned long long vc = __ballot(type >= 0 && corner), vs = __ballot(type >= 0 && !corner);
+    if (lane_id() == 0) {
+        if (vc) atomicAdd(&round_cnt[0], __popcll(vc));
+        if (vs) atomicAdd(&round_cnt[1], __popcll(vs));
+    }
+    if (cand_count) {
+        const int t = wave_sum_i(lead ? ncand : 0);
+        if (lane_id() == 0 && t) atomicAdd(cand_count, (unsigned long long)t);
+    }
 }
 
 __global__ void k_map_invalidate(aloam_factor* out, int n) {
@@ -521,6 +541,7 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
 }
 
 // The whole laserMapping frame; results are read back by the caller (aloam_api.hip).
+static const int g_exp = getenv("ALOAM_EXP") ? atoi(getenv("ALOAM_EXP")) : 0;   // profiling experiments only
 void map_frame_launch(Ctx& C, aloam_map_result* R) {
     hipStream_t st = C.stream;
     (void)R;
@@ -538,18 +559,16 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
     HIPCHK(hipMemsetAsync(C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, 0, sizeof(int) * 2 * ALOAM_MAX_ROUNDS, st));
     if (nq > 0) {
         if (nq > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity exceeded"};
-        k_map_invalidate<<<(nq + 255) / 256, 256, 0, st>>>(C.d_factors, nq);
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
         for (int it = 0; it < rounds; it++) {
             prof_mark(C, 6 + 2 * (ALOAM_MAX_ROUNDS + it));
-            k_map_knn5<<<(nq * WAVE + 255) / 256, 256, 0, st>>>(
+            k_map_assoc<<<(nq * AG + 255) / 256, 256, 0, st>>>(
                 C.d_cstack, C.d_sstack, C.d_stack_n, ub_c, ub_s,
                 C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
-                C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_nbr, C.profiling ? C.d_cand : nullptr);
+                C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
+                C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it, C.profiling ? C.d_cand : nullptr, g_exp);
             prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
-            k_map_fit<<<(nq + 127) / 128, 128, 0, st>>>(C.d_cstack, C.d_sstack, ub_c, ub_s, C.g_map_corner.pts, C.g_map_surf.pts,
-                                                        C.d_nbr, C.d_map, C.d_factors, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it);
-            lm_run(C, C.d_factors, nq, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize);
+            lm_run(C, C.d_factors, nq, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize, C.d_stack_n);
         }
     }
     k_map_update<<<1, 1, 0, st>>>(C.d_map);

@@ -165,34 +165,65 @@ __global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta*
         for (int i = threadIdx.x; i < N_SCANS; i += SB) hist[i * nb + blockIdx.x] = h[i];
 }
 
-// single block: exclusive scan of hist (line-major) and the line offsets
-__global__ void k_bucket_scan(int* hist, int nb, int N_SCANS, ScanMeta* meta) {
-    __shared__ int sh[1024];
-    __shared__ int carry;
+// single block: exclusive scan of hist (line-major [line][block]) and the line offsets. Chunks of
+// BS_E * 1024 counts are staged in LDS (padded against bank conflicts), each thread sums BS_E
+// consecutive counts, a wave-shuffle block scan combines the 1024 sums, and the chunk is rewritten
+// in place — ~33k counts (HDL-64) in one pass instead of a 20-step Hillis-Steele per 1024.
+constexpr int BS_T = 1024, BS_E = 32, BS_CHUNK = BS_T * BS_E;
+__host__ __device__ __forceinline__ int bs_pad(int i) { return i + (i >> 5); }
+__global__ void __launch_bounds__(BS_T) k_bucket_scan(int* hist, int nb, int N_SCANS, ScanMeta* meta) {
+    extern __shared__ int buf[];                                   // bs_pad(BS_CHUNK) ints
+    __shared__ int wsum[BS_T / WAVE];
+    __shared__ int carry_sh;
     const int total_n = nb * N_SCANS;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < total_n; base += 1024) {
-        int i = base + threadIdx.x;
-        int v = i < total_n ? hist[i] : 0;
-        sh[threadIdx.x] = v;
+    const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+    int carry = 0;
+    for (int base = 0; base < total_n; base += BS_CHUNK) {
+        const int cn = min(BS_CHUNK, total_n - base);
+        for (int i = t; i < BS_CHUNK; i += BS_T) buf[bs_pad(i)] = i < cn ? hist[base + i] : 0;
         __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += t;
-            __syncthreads();
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < BS_E; k++) s += buf[bs_pad(t * BS_E + k)];
+        // block exclusive scan of s
+        int incl = s;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int v = __shfl_up(incl, o, WAVE);
+            if (lane >= o) incl += v;
         }
-        int incl = sh[threadIdx.x];
-        if (i < total_n) {
-            hist[i] = carry + incl - v;
-            if (i % nb == 0) meta->line_off[i / nb] = carry + incl - v;
+        if (lane == WAVE - 1) wsum[w] = incl;
+        __syncthreads();
+        if (w == 0) {
+            int x = lane < BS_T / WAVE ? wsum[lane] : 0;
+            int xi = x;
+#pragma unroll
+            for (int o = 1; o < BS_T / WAVE; o <<= 1) {
+                const int v = __shfl_up(xi, o, WAVE);
+                if (lane >= o) xi += v;
+            }
+            if (lane < BS_T / WAVE) wsum[lane] = xi - x;               // exclusive wave offsets
+            if (lane == BS_T / WAVE - 1) carry_sh = xi;                // chunk total
         }
         __syncthreads();
-        if (threadIdx.x == 1023) carry += incl;
+        int run = carry + wsum[w] + incl - s;
+#pragma unroll
+        for (int k = 0; k < BS_E; k++) {
+            const int j = bs_pad(t * BS_E + k);
+            const int v = buf[j];
+            buf[j] = run;
+            run += v;
+        }
+        __syncthreads();
+        for (int i = t; i < cn; i += BS_T) {
+            const int v = buf[bs_pad(i)];
+            hist[base + i] = v;
+            if ((base + i) % nb == 0) meta->line_off[(base + i) / nb] = v;
+        }
+        carry += carry_sh;
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
+    if (t == 0) {
         meta->line_off[N_SCANS] = carry;
         meta->cloud_size = carry;
     }
@@ -346,6 +377,8 @@ __device__ void dev_std_sort(int* first, int* last, CurvLess less) {
 // ------------------------------------------------------------------------------------------
 // One workgroup (1024 threads) per scan line: (:277-408)
 constexpr int LT = 1024;
+constexpr int LINE_HDR = 256;                          // LDS header (LineShared) ahead of the line arrays
+constexpr size_t line_lds_bytes() { return LINE_HDR + (size_t)LINE_LDS_CAP * (4 * 4 + 4 + 8 + 2) + (LINE_LDS_CAP / 32 + 2) * 4; }
 
 __device__ inline void suppress_neighbours(int ind, const float* X, const float* Y, const float* Z, volatile int8_t* picked) {
     for (int l = 1; l <= 5; l++) {
@@ -375,6 +408,76 @@ __device__ inline void bitonic_sort_u64(unsigned long long* k, int n2) {
     }
 }
 
+// Block bitonic sort of n2 (power of two, 256 <= n2 <= 4 * LT) u64 keys held in LDS, ascending.
+// Thread t keeps positions 4t..4t+3 in registers: strides 1-2 are in-thread, strides 4-128 are
+// lane exchanges inside the wave (__shfl_xor), only strides >= 256 go through LDS + barriers
+// (10 barrier steps for 4096 keys instead of 78).
+__device__ __forceinline__ void cmpx(unsigned long long& a, unsigned long long& b, bool asc) {
+    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+    a = asc ? lo : hi;
+    b = asc ? hi : lo;
+}
+__device__ void bitonic_sort_reg4(unsigned long long* k, int n2) {
+    const int t = threadIdx.x;
+    const bool act = 4 * t < n2;
+    unsigned long long v[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = act ? k[4 * t + r] : ~0ull;
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 256) {
+                __syncthreads();
+                if (act) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) k[4 * t + r] = v[r];
+                }
+                __syncthreads();
+                if (act) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int g = 4 * t + r;
+                        const unsigned long long o = k[g ^ stride];
+                        const bool asc = (g & size) == 0, lower = (g & stride) == 0;
+                        const unsigned long long mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
+                        v[r] = (lower == asc) ? mn : mx;
+                    }
+                }
+            } else if (stride >= 4) {
+                const int lo = stride >> 2;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int g = 4 * t + r;
+                    const unsigned long long o = __shfl_xor(v[r], lo, WAVE);
+                    const bool asc = (g & size) == 0, lower = (g & stride) == 0;
+                    const unsigned long long mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
+                    v[r] = (lower == asc) ? mn : mx;
+                }
+            } else if (stride == 2) {
+                const bool asc = ((4 * t) & size) == 0;
+                cmpx(v[0], v[2], asc);
+                cmpx(v[1], v[3], asc);
+            } else {
+                const bool asc0 = ((4 * t) & size) == 0, asc1 = ((4 * t + 2) & size) == 0;
+                cmpx(v[0], v[1], asc0);
+                cmpx(v[2], v[3], asc1);
+            }
+        }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) k[4 * t + r] = v[r];
+    }
+    __syncthreads();
+}
+
+#ifdef ALOAM_LF_TIMING
+__device__ unsigned long long g_lf_ts[64][8];      // micro-benchmark only: per-line phase stamps
+#define LF_TS(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts[blockIdx.x][k] = wall_clock64(); } while (0)
+extern "C" int aloam_dbg_lf_ts(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_ts), sizeof(g_lf_ts)); }
+#else
+#define LF_TS(k) do { } while (0)
+#endif
 __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__ cloud, const float* __restrict__ gcurv,
                                                       const ScanMeta* meta, int N_SCANS,
                                                       float4* g_xyz, unsigned long long* g_keys, int* g_i,
@@ -382,12 +485,12 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                                                       float4* line_lf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     // all LDS is dynamic (Guideline 17: no statics ahead of the dynamic base)
-    struct LineShared { int flag, ncand, nrun, cnt[3]; unsigned bb[6]; int wsum[LT / WAVE]; };
+    struct LineShared { int flag, ncand, nrun, cnt[3]; unsigned bb[6]; int wsum[LT / WAVE]; int tie[6]; };
     LineShared& SH = *(LineShared*)smem_raw;
-    unsigned char* smem = smem_raw + 128;
-    static_assert(sizeof(LineShared) <= 128, "LineShared");
+    unsigned char* smem = smem_raw + LINE_HDR;
+    static_assert(sizeof(LineShared) <= LINE_HDR, "LineShared");
     int& s_flag = SH.flag; int& s_ncand = SH.ncand; int& s_nrun = SH.nrun;
-    int* s_cnt = SH.cnt; unsigned* s_bb = SH.bb; int* s_wsum = SH.wsum;
+    int* s_cnt = SH.cnt; unsigned* s_bb = SH.bb; int* s_wsum = SH.wsum; int* s_tie = SH.tie;
     const int line = blockIdx.x;
     const int off0 = meta->line_off[line], off1 = meta->line_off[line + 1];
     const int nl = off1 - off0;
@@ -403,6 +506,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
     int* S;                 // sorted global indices per segment position
     volatile int8_t* picked;
     int8_t* label;
+    unsigned* gapw;         // bit i of word i/32: pair (i, i+1) is a suppression stop
     unsigned long long* keys;
     if (!big) {
         X = (float*)smem;
@@ -413,6 +517,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         keys = (unsigned long long*)(S + LINE_LDS_CAP);
         picked = (volatile int8_t*)(keys + LINE_LDS_CAP);
         label = (int8_t*)(picked + LINE_LDS_CAP);
+        gapw = (unsigned*)(label + LINE_LDS_CAP);
     } else {
         float* gx = (float*)g_xyz;     // 4 floats per cloud point of scratch
         X = gx + off0;
@@ -423,6 +528,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         keys = g_keys + 2 * (size_t)off0;   // 2x room for the power-of-two padding
         picked = (volatile int8_t*)(g_i + (size_t)meta->cloud_size + off0);
         label = (int8_t*)(g_i + 2 * (size_t)meta->cloud_size + off0);
+        gapw = (unsigned*)((int8_t*)(g_i + (size_t)meta->cloud_size + off0) + ((nl + 3) & ~3));   // rest of picked's int slab
     }
     for (int k = threadIdx.x; k < nl; k += LT) {
         float4 p = cloud[off0 + k];
@@ -433,98 +539,176 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
     }
     if (threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
     __syncthreads();
-    // ---- segment sorts (:282-289): stable rank sort, libstdc++ replica on exact ties ----
-    for (int j = 0; j < 6; j++) {
-        const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
-        const int m = ep - sp + 1, b0 = sp - off0;
-        if (threadIdx.x == 0) s_flag = 0;
+    LF_TS(0);
+    // ---- gap bits: pair (i, i+1) of the line is a suppression stop when its fp32 squared
+    // distance > 0.05 (:321-338, :366-383 compute exactly this for every neighbour test) ----
+    for (int wd = threadIdx.x; wd < (nl + 31) / 32; wd += LT) {
+        unsigned bits = 0;
+        for (int bb = 0; bb < 32; bb++) {
+            const int i = wd * 32 + bb;
+            if (i + 1 < nl) {
+                const float dx = X[i + 1] - X[i], dy = Y[i + 1] - Y[i], dz = Z[i + 1] - Z[i];
+                if (dx * dx + dy * dy + dz * dz > 0.05) bits |= 1u << bb;
+            }
+        }
+        gapw[wd] = bits;
+    }
+    // ---- segment sorts (:282-289), all 6 segments at once. LDS lines: one bitonic sort of
+    // (segment, curvature bits, position) keys — stable by position, like the rank order; big lines:
+    // rank sort. A segment with exact curvature ties is redone by the libstdc++ introsort replica
+    // (thread 0), since std::sort's unstable order is what the reference produces. ----
+    if (threadIdx.x < 6) s_tie[threadIdx.x] = 0;
+    __syncthreads();
+    if (!big) {
+        const int M = e - s;                                             // positions s .. e-1
+        int n2 = 256;
+        while (n2 < M) n2 <<= 1;
+        for (int i = threadIdx.x; i < n2; i += LT) {
+            unsigned long long key = ~0ull;
+            if (i < M) {
+                const int a = s + i;
+                int j = (int)(((long long)i * 6) / (e - s));
+                while (j > 0 && a < s + (e - s) * j / 6) j--;
+                while (j < 5 && a >= s + (e - s) * (j + 1) / 6) j++;
+                key = ((unsigned long long)j << 44) | ((unsigned long long)__float_as_uint(Cv[a - off0]) << 12) | (unsigned)i;
+            }
+            keys[i] = key;
+        }
         __syncthreads();
-        int any_tie = 0;
-        for (int a = threadIdx.x; a < m; a += LT) {
-            const float ca = Cv[b0 + a];
+        bitonic_sort_reg4(keys, n2);
+        for (int i = threadIdx.x; i < M; i += LT) {
+            const unsigned long long key = keys[i];
+            S[s - off0 + i] = s + (int)(key & 0xfffu);
+            if (i > 0 && (keys[i - 1] >> 12) == (key >> 12)) s_tie[(int)(key >> 44)] = 1;
+        }
+    } else {
+        for (int a = s + threadIdx.x; a <= e - 1; a += LT) {
+            int j = (int)(((long long)(a - s) * 6) / (e - s));          // segment of a (sp_j <= a)
+            while (j > 0 && a < s + (e - s) * j / 6) j--;
+            while (j < 5 && a >= s + (e - s) * (j + 1) / 6) j++;
+            const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
+            const int b0 = sp - off0, ai = a - sp, m = ep - sp + 1;
+            const float ca = Cv[a - off0];
             int rank = 0, ties = 0;
-            for (int b = 0; b < m; b++) {
-                const float cb = Cv[b0 + b];
-                rank += (cb < ca) || (cb == ca && b < a);
+            for (int bi = 0; bi < m; bi++) {
+                const float cb = Cv[b0 + bi];
+                rank += (cb < ca) || (cb == ca && bi < ai);
                 ties += (cb == ca);
             }
-            S[b0 + rank] = sp + a;
-            any_tie |= (ties > 1);
-        }
-        if (any_tie) s_flag = 1;
-        __syncthreads();
-        if (s_flag) {
-            if (threadIdx.x == 0) {
-                for (int a = 0; a < m; a++) S[b0 + a] = sp + a;
-                dev_std_sort(S + b0, S + b0 + m, CurvLess{Cv, off0});
-            }
-            __syncthreads();
+            S[b0 + rank] = a;
+            if (ties > 1) s_tie[j] = 1;
         }
     }
-    // ---- greedy selection, one wave, segments in order (:291-390) ----
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < 6; j++) {
+            if (!s_tie[j]) continue;
+            const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
+            const int b0 = sp - off0, m = ep - sp + 1;
+            for (int a = 0; a < m; a++) S[b0 + a] = sp + a;
+            dev_std_sort(S + b0, S + b0 + m, CurvLess{Cv, off0});
+        }
+    }
+    __syncthreads();
+    LF_TS(1);
+    // ---- greedy selection, one wave, segments in order (:291-390). Suppression of the <= 5
+    // neighbours each side is a prefix of non-gap pairs, read from the gap bits and marked by
+    // lanes in parallel. ----
     if (threadIdx.x < WAVE) {
         const int lane = threadIdx.x;
         int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+        // suppression extents of line position p: marks p+1..p+nf and p-1..p-nb (:321-338)
+        auto extents = [&](int p, int& nf, int& nbk) {
+            const int q0 = p - 5;                                              // pairs p-5 .. p+4
+            const int w0 = q0 >> 5, sh = q0 & 31;
+            const unsigned long long win = ((unsigned long long)gapw[w0 + 1] << 32 | gapw[w0]) >> sh;
+            const unsigned fwd = (unsigned)(win >> 5) & 31u;                 // bit 0 = pair (p, p+1)
+            const unsigned bwd = (unsigned)(win & 31u);                        // bit 4 = pair (p-1, p)
+            nf = fwd ? __builtin_ctz(fwd) : 5;
+            nbk = bwd ? __builtin_clz(bwd << 27) : 5;
+        };
+        auto mark = [&](int p, int nf, int nbk) {
+            if (lane >= 1 && lane <= nf) picked[p + lane] = 1;
+            if (lane >= 33 && lane <= 32 + nbk) picked[p - (lane - 32)] = 1;
+        };
         for (int j = 0; j < 6; j++) {
             const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
+            // corners: chunks of 64 sorted positions from the largest curvature; per pick only the
+            // picked flags are re-read, everything else of the chunk stays in registers
             int largest = 0;
-            int cur = ep;
-            while (cur >= sp) {
-                const int k = cur - lane;
+            bool stop = false;
+            for (int top = ep; top >= sp && !stop; top -= WAVE) {
+                const int k = top - lane;
                 const bool valid = k >= sp;
                 const int ind = valid ? S[k - off0] : sp;
-                const bool elig = valid && picked[ind - off0] == 0 && (double)Cv[ind - off0] > 0.1;
-                const unsigned long long mk = __ballot(elig);
-                if (!mk) { cur -= WAVE; continue; }
-                const int f = __ffsll((long long)mk) - 1;
-                const int indf = __shfl(ind, f, WAVE);
-                largest++;
-                if (largest > 20) break;
-                if (lane == 0) {
-                    if (largest <= 2) {
-                        label[indf - off0] = 2;
-                        line_sharp[line * LINE_SHARP_CAP + n_sharp] = indf;
-                    } else {
-                        label[indf - off0] = 1;
+                const bool cv_ok = valid && (double)Cv[ind - off0] > 0.1;
+                if (!__ballot(cv_ok)) break;                                   // sorted: nothing > 0.1 remains
+                int nf = 0, nbk = 0;
+                if (cv_ok) extents(ind - off0, nf, nbk);
+                int last = -1;
+                while (true) {
+                    const unsigned long long mk = __ballot(cv_ok && lane > last && picked[ind - off0] == 0);
+                    if (!mk) break;
+                    const int f = __ffsll((long long)mk) - 1;
+                    last = f;
+                    const int indf = __shfl(ind, f, WAVE);
+                    largest++;
+                    if (largest > 20) { stop = true; break; }
+                    const int pf = __shfl(nf, f, WAVE), pb = __shfl(nbk, f, WAVE);
+                    if (lane == 0) {
+                        if (largest <= 2) {
+                            label[indf - off0] = 2;
+                            line_sharp[line * LINE_SHARP_CAP + n_sharp] = indf;
+                        } else {
+                            label[indf - off0] = 1;
+                        }
+                        line_lsharp[line * LINE_LSHARP_CAP + n_lsharp] = indf;
+                        picked[indf - off0] = 1;
                     }
-                    line_lsharp[line * LINE_LSHARP_CAP + n_lsharp] = indf;
-                    picked[indf - off0] = 1;
-                    suppress_neighbours(indf - off0, X, Y, Z, picked);
+                    mark(indf - off0, pf, pb);
+                    if (largest <= 2) n_sharp++;
+                    n_lsharp++;
+                    __threadfence_block();
+                    __builtin_amdgcn_wave_barrier();
                 }
-                if (largest <= 2) n_sharp++;
-                n_lsharp++;
-                __threadfence_block();
-                cur = cur - f - 1;
             }
+            // flats: from the smallest curvature; the 4th pick is not marked (:366-388)
             int smallest = 0;
-            cur = sp;
-            while (cur <= ep) {
-                const int k = cur + lane;
+            stop = false;
+            for (int bot = sp; bot <= ep && !stop; bot += WAVE) {
+                const int k = bot + lane;
                 const bool valid = k <= ep;
                 const int ind = valid ? S[k - off0] : sp;
-                const bool elig = valid && picked[ind - off0] == 0 && (double)Cv[ind - off0] < 0.1;
-                const unsigned long long mk = __ballot(elig);
-                if (!mk) { cur += WAVE; continue; }
-                const int f = __ffsll((long long)mk) - 1;
-                const int indf = __shfl(ind, f, WAVE);
-                if (lane == 0) {
-                    label[indf - off0] = -1;
-                    line_flat[line * LINE_FLAT_CAP + n_flat] = indf;
+                const bool cv_ok = valid && (double)Cv[ind - off0] < 0.1;
+                if (!__ballot(cv_ok)) break;                                   // sorted: nothing < 0.1 remains
+                int nf = 0, nbk = 0;
+                if (cv_ok) extents(ind - off0, nf, nbk);
+                int last = -1;
+                while (true) {
+                    const unsigned long long mk = __ballot(cv_ok && lane > last && picked[ind - off0] == 0);
+                    if (!mk) break;
+                    const int f = __ffsll((long long)mk) - 1;
+                    last = f;
+                    const int indf = __shfl(ind, f, WAVE);
+                    if (lane == 0) {
+                        label[indf - off0] = -1;
+                        line_flat[line * LINE_FLAT_CAP + n_flat] = indf;
+                    }
+                    n_flat++;
+                    smallest++;
+                    if (smallest >= 4) { stop = true; break; }
+                    const int pf = __shfl(nf, f, WAVE), pb = __shfl(nbk, f, WAVE);
+                    if (lane == 0) picked[indf - off0] = 1;
+                    mark(indf - off0, pf, pb);
+                    __threadfence_block();
+                    __builtin_amdgcn_wave_barrier();
                 }
-                n_flat++;
-                smallest++;
-                if (smallest >= 4) break;
-                if (lane == 0) {
-                    picked[indf - off0] = 1;
-                    suppress_neighbours(indf - off0, X, Y, Z, picked);
-                }
-                __threadfence_block();
-                cur = cur + f + 1;
             }
         }
         if (lane == 0) { s_cnt[0] = n_sharp; s_cnt[1] = n_lsharp; s_cnt[2] = n_flat; }
     }
     __syncthreads();
+    LF_TS(2);
     // ---- less-flat candidates: label <= 0 in [s, e-1], cloud order (:392-398) ----
     // compact into S (reused) by a block-wide scan over chunks of LT
     if (threadIdx.x == 0) s_ncand = 0;
@@ -544,6 +728,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         __syncthreads();
     }
     const int nc = s_ncand;
+    LF_TS(3);
     // ---- VoxelGrid(0.2) of the candidates (PCL 1.8 applyFilter), points summed in input order ----
     if (threadIdx.x < 6) s_bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     __syncthreads();
@@ -554,7 +739,15 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
             unsigned v[3] = {f2ord(X[k]), f2ord(Y[k]), f2ord(Z[k])};
             for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
         }
-        for (int d = 0; d < 3; d++) { atomicMin(&s_bb[d], mn[d]); atomicMax(&s_bb[3 + d], mx[d]); }
+#pragma unroll
+        for (int d = 0; d < 3; d++)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mn[d] = min(mn[d], (unsigned)__shfl_xor((int)mn[d], o, WAVE));
+                mx[d] = max(mx[d], (unsigned)__shfl_xor((int)mx[d], o, WAVE));
+            }
+        if (lane_id() == 0)
+            for (int d = 0; d < 3; d++) { atomicMin(&s_bb[d], mn[d]); atomicMax(&s_bb[3 + d], mx[d]); }
     }
     __syncthreads();
     const float inv = 1.0f / 0.2f;
@@ -590,7 +783,10 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         keys[t] = key;
     }
     __syncthreads();
-    bitonic_sort_u64(keys, n2);
+    LF_TS(4);
+    if (!big && n2 >= 256) bitonic_sort_reg4(keys, n2);
+    else bitonic_sort_u64(keys, n2);
+    LF_TS(5);
     // run heads -> centroids; run r's head position stored in S[nc + r] region? reuse Cv as int
     int* heads = (int*)Cv;   // curvature no longer needed
     if (threadIdx.x == 0) s_nrun = 0;
@@ -609,6 +805,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         __syncthreads();
     }
     const int nrun = s_nrun;
+    LF_TS(6);
     for (int r = threadIdx.x; r < nrun; r += LT) {
         const int h0 = heads[r], h1 = (r + 1 < nrun) ? heads[r + 1] : nc;
         int k = S[(int)(keys[h0] & 0xffffffffu)];
@@ -623,6 +820,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
     if (threadIdx.x == 0) {
         cnt_out[0] = s_cnt[0]; cnt_out[1] = s_cnt[1]; cnt_out[2] = s_cnt[2]; cnt_out[3] = nrun;
     }
+    LF_TS(7);
 }
 
 // concatenate per-line outputs in line order (:304-310,356,407)
@@ -681,10 +879,16 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
         k_filter_scatter<<<nb, SB, 0, st>>>(in, n, P.input_is_dense, thres, C.d_blk, C.d_cl);
         k_bucket_classify<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, N_SCANS, P.generic_min_elev_deg, P.generic_max_elev_deg,
                                              C.d_sid, C.d_ori, C.d_hist, nb, C.d_meta);
-        k_bucket_scan<<<1, 1024, 0, st>>>(C.d_hist, nb, N_SCANS, C.d_meta);
+        static bool scan_attr = false;
+        const size_t scan_lds = sizeof(int) * (size_t)bs_pad(BS_CHUNK);
+        if (!scan_attr) {
+            HIPCHK(hipFuncSetAttribute((const void*)k_bucket_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds));
+            scan_attr = true;
+        }
+        k_bucket_scan<<<1, BS_T, scan_lds, st>>>(C.d_hist, nb, N_SCANS, C.d_meta);
         k_bucket_scatter<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, C.d_sid, C.d_ori, C.d_hist, nb, N_SCANS, C.d_cloud);
         k_curvature<<<nb, SB, 0, st>>>(C.d_cloud, C.d_meta, C.d_curv);
-        const size_t lds = 128 + (size_t)LINE_LDS_CAP * (4 * 4 + 4 + 8 + 2);
+        const size_t lds = line_lds_bytes();
         k_line_features<<<N_SCANS, LT, lds, st>>>(C.d_cloud, C.d_curv, C.d_meta, N_SCANS, C.d_scratch_xyz,
                                                   C.d_scratch_keys, C.d_scratch_i, C.d_line_sharp, C.d_line_lsharp,
                                                   C.d_line_flat, C.d_line_cnt, C.d_line_lf);

@@ -1,0 +1,24 @@
+"""Profiling probe (not a test): k_line_features phase timing (build micro/libaloam_lf.so with -DALOAM_LF_TIMING)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+os.environ["ALOAM_LIB_PATH"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaloam_lf.so")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+from lvo_amd_loader import lvo  # noqa: E402
+
+ctx = lvo.Context(lvo.abi.default_params(64))
+pts = lvo.synth.scan("hdl64", 7)
+for _ in range(3):
+    ctx.scan_registration(pts)
+ts = np.zeros((64, 8), np.uint64)
+lvo.lib().aloam_dbg_lf_ts(ts.ctypes.data_as(C.c_void_p))
+d = np.diff(ts[:51].astype(np.float64), axis=1) / 100.0   # 100 MHz -> us
+names = ["sort", "greedy", "lessflat", "vox-keys", "bitonic", "runs", "centroid"]
+for i, n in enumerate(names):
+    print(f"{n:9s} mean {d[:, i].mean():7.2f} us  max {d[:, i].max():7.2f}")
+print("total per block: mean %.1f max %.1f us; block start spread %.1f us" % (
+    (ts[:51, 7] - ts[:51, 0]).astype(float).mean() / 100, (ts[:51, 7] - ts[:51, 0]).astype(float).max() / 100,
+    (ts[:51, 0].max() - ts[:51, 0].min()) / 100.0))
