@@ -86,6 +86,9 @@ static void allocate(Ctx& C) {
     HIPCHK(hipMemcpy(C.d_odom, &C.h_odom, sizeof(OdomState), hipMemcpyHostToDevice));
     grid_alloc(C, C.g_corner_last, capLS, 2.5f * 1.025f);   // two-phase 1-NN, k_odom.hip
     grid_alloc(C, C.g_surf_last, N, 2.5f * 1.025f);
+    const int layers = std::min(MAXL, std::max(P.scan_line, 1));
+    grid_alloc(C, C.g_corner_win, capLS, 2.5f * 1.025f, layers);   // window search: cells x scan line
+    grid_alloc(C, C.g_surf_win, N, 2.5f * 1.025f, layers);
     C.cap_factors = capLS + N;
     C.d_factors = (aloam_factor*)dalloc(C, sizeof(aloam_factor) * C.cap_factors);
     C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);
@@ -99,6 +102,7 @@ static void allocate(Ctx& C) {
     C.d_lm_sum = (aloam_lm_summary*)dalloc(C, sizeof(aloam_lm_summary) * 2 * ALOAM_MAX_ROUNDS);
     C.d_round_cnt = (int*)dalloc(C, sizeof(int) * 4 * ALOAM_MAX_ROUNDS);
     C.d_last_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_last_sorted = (int*)dalloc(C, sizeof(int) * 2);
     C.d_cand = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2);
     // mapping
     const int M = std::max(P.max_map_points, 1024);
@@ -222,6 +226,9 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);
     grid_build(C, C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
     grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
+    grid_build(C, C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
+    grid_build(C, C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
+    odom_last_sorted(C);
     const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
     r.publish_to_mapping = (C.odom_frame_count % skip == 0);
     if (r.publish_to_mapping) C.odom_frame_count = 0;
@@ -294,6 +301,7 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
     r.map_surf_num = C.h_map.n_surf_map;
     r.corner_stack_num = stackn[0];
     r.surf_stack_num = stackn[1];
+    C.map_slots_hint = stackn[0] + stackn[1];
     r.map_total_points = C.n_mc + C.n_ms;
     for (int k = 0; k < 7; k++) (k < 4 ? r.q_w_curr[k] : r.t_w_curr[k - 4]) = C.h_map.parameters[k];
     C.have_map_input = false;
@@ -470,6 +478,9 @@ int aloam_set_odom_state(aloam_ctx* ctx, const double q[4], const double t[3], c
     set_counts2(C, C.d_last_n, nc, ns);
     grid_build(C, C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(nc, 1), nullptr, nullptr);
     grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(ns, 1), nullptr, nullptr);
+    grid_build(C, C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
+    grid_build(C, C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
+    odom_last_sorted(C);
     sync(C);
     C.odom_inited = true;
     API_END

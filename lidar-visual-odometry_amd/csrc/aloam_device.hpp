@@ -125,40 +125,53 @@ struct RowSet {
     int pre[MAXR + 1];
     int nr;
 };
-// rs lives in LDS, one per wave: every lane writes the same (wave-uniform) values.
+// rs lives in LDS, one per wave. Lane r < (2m+1)^2 owns row r: its two cell_start loads are issued
+// by all lanes at once (one round trip), a wave prefix sum turns the row lengths into offsets.
+// Empty rows stay in the set with zero length.
 template <int MAXR>
 __device__ __forceinline__ int build_rows(const float ox, const float oy, const float oz, const float inv_cell,
                                           const int gdx, const int gdy, const int gdz, const int* __restrict__ start,
                                           float qx, float qy, float qz, int m, RowSet<MAXR>& rs) {
-    __builtin_amdgcn_wave_barrier();
+    static_assert(MAXR <= WAVE, "one row per lane");
+    const int lane = lane_id();
     const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
     const int x0 = max(cx - m, 0), x1 = min(cx + m, gdx - 1);
-    int total = 0, nr = 0;
-    rs.pre[0] = 0;
-    if (x0 <= x1) {
-        for (int z = max(cz - m, 0); z <= min(cz + m, gdz - 1); z++)
-            for (int y = max(cy - m, 0); y <= min(cy + m, gdy - 1); y++) {
-                const int c = (z * gdy + y) * gdx;
-                const int b = start[c + x0], e = start[c + x1 + 1];
-                if (e > b && nr < MAXR) {
-                    rs.b[nr] = b;
-                    total += e - b;
-                    rs.pre[++nr] = total;
-                }
-            }
+    const int w = 2 * m + 1;
+    const int nrow = w * w;
+    int b = 0, len = 0;
+    if (lane < nrow && lane < MAXR) {
+        const int y = cy - m + lane % w, z = cz - m + lane / w;
+        if (x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz) {
+            const int c = (z * gdy + y) * gdx;
+            b = start[c + x0];
+            len = start[c + x1 + 1] - b;
+        }
     }
-    rs.nr = nr;
+    int incl = len;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int v = __shfl_up(incl, o, WAVE);
+        if (lane >= o) incl += v;
+    }
+    const int nr = min(nrow, MAXR);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nr) { rs.b[lane] = b; rs.pre[lane + 1] = incl; }
+    if (lane == 0) { rs.pre[0] = 0; rs.nr = nr; }
+    const int total = __shfl(incl, nr - 1, WAVE);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return total;
 }
-// flattened candidate t -> point position
+// flattened candidate t -> point position (binary search over the row offsets)
 template <int MAXR>
 __device__ __forceinline__ int row_pos(const RowSet<MAXR>& rs, int t) {
-    int r = 0;
-    while (r + 1 < rs.nr && rs.pre[r + 1] <= t) r++;
-    return rs.b[r] + (t - rs.pre[r]);
+    int lo = 0, hi = rs.nr - 1;          // last row r with pre[r] <= t
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rs.pre[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    return rs.b[lo] + (t - rs.pre[lo]);
 }
 }  // namespace aloam
 

@@ -30,6 +30,7 @@ struct GridDesc {
     unsigned bb[6];                // ordered-encoded bbox: min xyz, max xyz
     float ox, oy, oz, cell, inv_cell;
     int dx, dy, dz, ncells, n;
+    int nlayers;                   // > 1: cells also split by scan line (layer = int(intensity))
 };
 struct Grid {
     GridDesc* desc = nullptr;      // device
@@ -39,6 +40,7 @@ struct Grid {
     float4* pts = nullptr;         // points sorted by cell
     int* idx = nullptr;            // original index of each sorted point
     int* pcell = nullptr;          // cell of each input point
+    int nlayers = 1;
     int cap = 0;
     float min_cell = 1.f;
 };
@@ -122,12 +124,15 @@ struct Ctx {
     float4 *d_corner_last = nullptr, *d_surf_last = nullptr;
     int n_corner_last = 0, n_surf_last = 0;
     Grid g_corner_last, g_surf_last;
+    Grid g_corner_win, g_surf_win;  // scan-line-layered grids of the last clouds (window search)
     aloam_factor* d_factors = nullptr;
     int cap_factors = 0;
     LMState* d_lm = nullptr;
     double* d_partials = nullptr;
     double* d_coop_part = nullptr;  // 2 x 64 x 29 doubles (LM pass partials, double-buffered)
     unsigned* d_bar = nullptr;       // grid barrier {count, generation}
+    int map_slots_hint = 0;
+    int* d_last_sorted = nullptr;    // [2]: corner_last / surf_last ordered by scan line          // last mapping frame's stack sizes (LM grid sizing only)
     int* d_bar_err = nullptr;        // set if a grid barrier timed out (device view of h_bar_err)
     int* h_bar_err = nullptr;        // mapped pinned host word
     aloam_lm_summary* d_lm_sum = nullptr;   // [ALOAM_MAX_ROUNDS]
@@ -195,12 +200,14 @@ struct ApiError {
 // ---- launch entry points (defined in the k_*.hip files) ----
 void scan_registration_launch(Ctx& C, const float4* in, int n);
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of, const unsigned char* cube_valid);
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell);
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);
 void odom_compose(Ctx& C);
 // nslots = host upper bound; d_nslots2 (optional, device int[2]) = live slots as a sum of two counts
-void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2 = nullptr);
+void odom_last_sorted(Ctx& C);
+void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2 = nullptr,
+            int live_hint = 0);
 void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq);
 void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2);
 size_t voxel_sort_tmp_bytes(int cap);

@@ -16,13 +16,13 @@ namespace aloam {
 
 constexpr int GB = 256;
 
-__device__ inline void grid_params(const unsigned bb[6], float min_cell, GridDesc* d) {
+__device__ inline void grid_params(const unsigned bb[6], float min_cell, int nlayers, GridDesc* d) {
     float mn[3], mx[3];
     for (int a = 0; a < 3; a++) { mn[a] = ord2f(bb[a]); mx[a] = ord2f(bb[3 + a]); }
     float cell = min_cell;
     int dims[3];
     for (int it = 0; it < 64; it++) {
-        long long prod = 1;
+        long long prod = nlayers;
         for (int a = 0; a < 3; a++) {
             float ext = mx[a] - mn[a];
             if (!(ext >= 0.f)) ext = 0.f;
@@ -35,7 +35,8 @@ __device__ inline void grid_params(const unsigned bb[6], float min_cell, GridDes
     d->ox = mn[0]; d->oy = mn[1]; d->oz = mn[2];
     d->cell = cell; d->inv_cell = 1.0f / cell;
     d->dx = dims[0]; d->dy = dims[1]; d->dz = dims[2];
-    d->ncells = dims[0] * dims[1] * dims[2];
+    d->ncells = dims[0] * dims[1] * dims[2] * nlayers;
+    d->nlayers = nlayers;
 }
 
 __device__ inline int cell_coord(float v, float o, float inv) { return (int)floorf((v - o) * inv); }
@@ -77,16 +78,16 @@ __global__ void k_grid_bbox(const float4* __restrict__ pts, const int* d_n, cons
 }
 
 __global__ void k_grid_count(const float4* __restrict__ pts, const int* d_n, const int* cube_of,
-                             const unsigned char* cube_valid, GridDesc* d, float min_cell, int* cell_count, int* pcell) {
+                             const unsigned char* cube_valid, GridDesc* d, float min_cell, int nlayers, int* cell_count, int* pcell) {
     __shared__ GridDesc gd;
     if (threadIdx.x == 0) {
         unsigned bb[6];
         for (int a = 0; a < 6; a++) bb[a] = d->bb[a];
         gd.n = d->n;
-        grid_params(bb, min_cell, &gd);
+        grid_params(bb, min_cell, nlayers, &gd);
         if (blockIdx.x == 0) {
             d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
-            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells;
+            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers;
         }
     }
     __syncthreads();
@@ -97,7 +98,8 @@ __global__ void k_grid_count(const float4* __restrict__ pts, const int* d_n, con
         int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
         int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
         int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
-        int c = (cz * gd.dy + cy) * gd.dx + cx;
+        const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
+        int c = ((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx;
         pcell[i] = c;
         atomicAdd(&cell_count[c], 1);
     }
@@ -180,9 +182,10 @@ __global__ void k_grid_scatter(const float4* __restrict__ pts, const int* d_n, c
     }
 }
 
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell) {
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers) {
     g.cap = cap;
     g.min_cell = min_cell;
+    g.nlayers = nlayers;
     g.desc = (GridDesc*)dalloc(C, sizeof(GridDesc));
     g.cell_count = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
     g.cell_start = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
@@ -198,7 +201,7 @@ void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, c
     const int nb = std::max(1, std::min(1024, (cap_n + GB - 1) / GB));
     k_grid_init<<<1, 64, 0, st>>>(g.desc);
     k_grid_bbox<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc);
-    k_grid_count<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc, g.min_cell, g.cell_count, g.pcell);
+    k_grid_count<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc, g.min_cell, g.nlayers, g.cell_count, g.pcell);
     const int nsb = GRID_MAX_CELLS / SCAN_CHUNK;
     k_grid_scan1<<<nsb, GB, 0, st>>>(g.cell_count, g.desc, g.blk);
     k_grid_scan2<<<1, 1024, 0, st>>>(g.blk, g.desc);

@@ -470,15 +470,19 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
 }
 
 // one Ceres Solve over nslots factor slots; `gate` (device int, may be null) disables the solve.
-void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2) {
+void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2,
+            int live_hint) {
     aloam_lm_summary* out = C.d_lm_sum + round;
-    // >= 2 slots per thread keeps a pass's evaluation well above the barrier cost; <= LM_CACHE slots
-    // per workgroup lets every pass after the first read the slots from LDS
-    static const int spt = getenv("ALOAM_LM_SPT") ? std::max(1, atoi(getenv("ALOAM_LM_SPT"))) : 2;   // tuning knob
-    int G = std::max((nslots + spt * CB - 1) / (spt * CB), (nslots + LM_CACHE - 1) / LM_CACHE);
+    // Grid size from the expected live slot count (exact for odometry; last frame's stack sizes for
+    // mapping, whose live count is only known on the device): ~1 slot per thread keeps the
+    // evaluation short (fp64 latency-bound), capped so the per-pass grid barrier stays cheap.
+    // Correctness never depends on G: the kernel splits the device-side count over the grid.
+    const int est = std::max(1, std::min(nslots, live_hint > 0 ? live_hint + live_hint / 4 : nslots));
+    static const int spt = getenv("ALOAM_LM_SPT") ? std::max(1, atoi(getenv("ALOAM_LM_SPT"))) : 1;   // tuning knob
+    int G = std::max((est + spt * CB - 1) / (spt * CB), (est + LM_CACHE - 1) / LM_CACHE);
     G = std::max(1, std::min(LM_COOP_MAX, G));
-    const int per = (nslots + G - 1) / G;
-    const size_t lds = per <= LM_CACHE ? sizeof(aloam_factor) * (size_t)per : 0;
+    const int cap = std::min(LM_CACHE, (nslots + G - 1) / G);          // LDS slots per workgroup
+    const size_t lds = sizeof(aloam_factor) * (size_t)cap;
     static bool attr = false;
     if (!attr) {   // static rows (59 KB) + up to 80 KB of cached slots: above the default dynamic limit
         HIPCHK(hipFuncSetAttribute((const void*)k_lm_coop, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -486,7 +490,7 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
         attr = true;
     }
     k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_coop_part, C.d_bar, C.d_bar_err, out,
-                                      C.P.max_solver_iterations, gate, d_nslots2, lds ? per : 0);
+                                      C.P.max_solver_iterations, gate, d_nslots2, cap);
     HIPCHK(hipGetLastError());
 }
 

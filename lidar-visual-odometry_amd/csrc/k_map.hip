@@ -568,7 +568,8 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
                 C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
                 C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it, C.profiling ? C.d_cand : nullptr, g_exp);
             prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
-            lm_run(C, C.d_factors, nq, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize, C.d_stack_n);
+            lm_run(C, C.d_factors, nq, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize, C.d_stack_n,
+                   C.map_slots_hint);
         }
     }
     k_map_update<<<1, 1, 0, st>>>(C.d_map);

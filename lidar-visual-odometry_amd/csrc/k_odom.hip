@@ -127,14 +127,139 @@ __device__ inline void window_search(const float4* __restrict__ cl, int n, int c
     *ind3 = i3;
 }
 
+// The same window search through the grid. When the last cloud is ordered by scan line (it is
+// built line by line: laserOdometry.cpp:627-641 takes scanRegistration's per-line output), the
+// scan from `closest` visits exactly: forward = {j > closest, line in [c, c+2]}, backward =
+// {j < closest, line in [c-2, c]} (the break fires at the first line outside). Only points with
+// d^2 < 25 can win (the running minimum starts at 25), and those lie in the 5x5x5 block of 2.56 m
+// cells. Per set, the first occurrence of the minimum in scan order is the (d^2, j) minimum going
+// forward and the (d^2, -j) minimum going backward; backward replaces forward only when strictly
+// closer — the serial loop's result, without walking whole scan lines.
+// Rows of the scan-line-layered grid for the lines lo..hi around the query (5 z x 5 y rows of
+// 5 x-cells per line, <= 125 rows): lane r owns rows r and r + 64; two wave prefix sums.
+__device__ __forceinline__ int build_rows_layers(const GridDesc& gd, const int* __restrict__ start, float qx, float qy,
+                                                 float qz, int lo, int hi, int skip, RowSet<128>& rs) {
+    const int lane = lane_id();
+    const int cx = (int)floorf((qx - gd.ox) * gd.inv_cell), cy = (int)floorf((qy - gd.oy) * gd.inv_cell),
+              cz = (int)floorf((qz - gd.oz) * gd.inv_cell);
+    const int x0 = max(cx - 2, 0), x1 = min(cx + 2, gd.dx - 1);
+    const int nrow = (hi - lo + 1) * 25;
+    int b[2], len[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int r = lane + h * WAVE;
+        b[h] = 0; len[h] = 0;
+        if (r < nrow) {
+            const int L = lo + r / 25, rr = r % 25;
+            const int y = cy - 2 + rr % 5, z = cz - 2 + rr / 5;
+            if (L != skip && L >= 0 && L < gd.nlayers && x0 <= x1 && y >= 0 && y < gd.dy && z >= 0 && z < gd.dz) {
+                const int c = ((L * gd.dz + z) * gd.dy + y) * gd.dx;
+                b[h] = start[c + x0];
+                len[h] = start[c + x1 + 1] - b[h];
+            }
+        }
+    }
+    int inc0 = len[0], inc1 = len[1];
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int v0 = __shfl_up(inc0, o, WAVE), v1 = __shfl_up(inc1, o, WAVE);
+        if (lane >= o) { inc0 += v0; inc1 += v1; }
+    }
+    const int t0 = __shfl(inc0, WAVE - 1, WAVE);
+    inc1 += t0;
+    const int nr = min(nrow, 128);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nr) { rs.b[lane] = b[0]; rs.pre[lane + 1] = inc0; }
+    if (lane + WAVE < nr) { rs.b[lane + WAVE] = b[1]; rs.pre[lane + WAVE + 1] = inc1; }
+    if (lane == 0) { rs.pre[0] = 0; rs.nr = nr; }
+    const int total = nr > WAVE ? __shfl(inc1, nr - WAVE - 1, WAVE) : __shfl(inc0, nr - 1, WAVE);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return total;
+}
+
+// The same window search through the scan-line-layered grid. When the last cloud is ordered by
+// scan line (it is built line by line: laserOdometry.cpp:627-641 takes scanRegistration's
+// per-line output), the serial scan from `closest` visits exactly: forward = {j > closest, line
+// in [c, c+2]}, backward = {j < closest, line in [c-2, c]} (its break fires at the first line
+// outside). Only points with d^2 < 25 can win (the running minimum starts at 25), and those lie in
+// the 5x5x5 block of >= 2.56 m cells of their own line's layer. Per set, the first occurrence of
+// the minimum in scan order is the (d^2, j) minimum going forward and the (d^2, -j) minimum going
+// backward; backward replaces forward only when strictly closer — the serial loop's result.
+template <int MODE>
+__device__ inline void grid_window(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
+                                   const int* __restrict__ sidx, int closest, int cid, float sx, float sy, float sz,
+                                   int* ind2, int* ind3, RowSet<128>& rs) {
+    const int lane = lane_id();
+    const int total = build_rows_layers(gd, start, sx, sy, sz, cid - 2, cid + 2, MODE == 0 ? cid : -1000, rs);
+    // sets: 0 = fwd ind2, 1 = bwd ind2, 2 = fwd ind3, 3 = bwd ind3 (corner: ind2 sets only)
+    unsigned long long k[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
+        int pp[4];
+        float4 vv[4];
+        int jj[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = t0 + u * WAVE + lane;
+            pp[u] = t < total ? row_pos<128>(rs, t) : -1;
+            vv[u] = pp[u] >= 0 ? spts[pp[u]] : make_float4(0, 0, 0, 0);
+            jj[u] = pp[u] >= 0 ? sidx[pp[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (pp[u] < 0) continue;
+            const float d = sqdist(vv[u].x, vv[u].y, vv[u].z, sx, sy, sz);
+            if (!(d < 25.0f)) continue;
+            const int line = line_of(vv[u].w), j = jj[u];
+            const bool fwd = j > closest, bwd = j < closest;
+            if (!fwd && !bwd) continue;
+            const unsigned long long kf = dist_key(d, j), kb = dist_key(d, (int)(0x7fffffffu - (unsigned)j));
+            if (MODE == 0) {
+                if (fwd && line > cid && line <= cid + 2) k[0] = min(k[0], kf);
+                if (bwd && line < cid && line >= cid - 2) k[1] = min(k[1], kb);
+            } else {
+                if (fwd && line == cid) k[0] = min(k[0], kf);
+                if (bwd && line == cid) k[1] = min(k[1], kb);
+                if (fwd && line > cid && line <= cid + 2) k[2] = min(k[2], kf);
+                if (bwd && line < cid && line >= cid - 2) k[3] = min(k[3], kb);
+            }
+        }
+    }
+    int res[2] = {-1, -1};
+#pragma unroll
+    for (int s = 0; s < (MODE == 0 ? 1 : 2); s++) {
+        const unsigned long long f = wave_min_u64(k[2 * s]), b = wave_min_u64(k[2 * s + 1]);
+        float best = 25.0f;
+        int idx = -1;
+        if (f != ~0ull) { best = __uint_as_float((unsigned)(f >> 32)); idx = (int)(f & 0xffffffffu); }
+        if (b != ~0ull && __uint_as_float((unsigned)(b >> 32)) < best) idx = (int)(0x7fffffffu - (unsigned)(b & 0xffffffffu));
+        res[s] = idx;
+    }
+    *ind2 = res[0];
+    *ind3 = res[1];
+}
+
+// 1 if the cloud's scan line (int(intensity)) never decreases with the index
+__global__ void k_line_sorted(const float4* __restrict__ a, const int* na, const float4* __restrict__ b, const int* nb_,
+                              int* flag) {
+    const float4* cl = blockIdx.y == 0 ? a : b;
+    const int n = blockIdx.y == 0 ? *na : *nb_;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j + 1 < n; j += gridDim.x * blockDim.x)
+        if (line_of(cl[j + 1].w) < line_of(cl[j].w)) flag[blockIdx.y] = 0;
+}
+
 __global__ void __launch_bounds__(256) k_odom_search(
     const float4* __restrict__ sharp, int n_sharp, const float4* __restrict__ flat, int n_flat,
     const float4* __restrict__ corner_last, int n_cl, const float4* __restrict__ surf_last, int n_sl,
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt) {
+    const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
+    const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
+    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s) {
     __shared__ RowSet<9> rows9[256 / WAVE];
     __shared__ RowSet<25> rows25[256 / WAVE];
+    __shared__ RowSet<128> rows128[256 / WAVE];
     const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
     const int lane = lane_id();
     if (qi >= n_sharp + n_flat) return;
@@ -162,8 +287,10 @@ __global__ void __launch_bounds__(256) k_odom_search(
     if (found) {
         const int cid = line_of(cl[closest].w);
         int i2, i3;
+        const bool by_grid = line_sorted[is_corner ? 0 : 1] != 0;
         if (is_corner) {
-            window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+            if (by_grid) grid_window<0>(*wdc, ws_c, wp_c, wi_c, closest, cid, sx, sy, sz, &i2, &i3, rows128[threadIdx.x / WAVE]);
+            else window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
             if (i2 >= 0) {
                 const float4 a = cl[closest], b = cl[i2];
                 f.type = 0;
@@ -171,7 +298,8 @@ __global__ void __launch_bounds__(256) k_odom_search(
                 f.b[0] = b.x; f.b[1] = b.y; f.b[2] = b.z;
             }
         } else {
-            window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+            if (by_grid) grid_window<1>(*wds, ws_s, wp_s, wi_s, closest, cid, sx, sy, sz, &i2, &i3, rows128[threadIdx.x / WAVE]);
+            else window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
             if (i2 >= 0 && i3 >= 0) {
                 const float4 pj = cl[closest], pl = cl[i2], pm = cl[i3];
                 // LidarPlaneFactor ctor (lidarFactor.hpp:64-65)
@@ -210,7 +338,16 @@ void odom_round_search(Ctx& C, int round) {
         C.d_sharp, C.n_sharp, C.d_flat, C.n_flat, C.d_corner_last, C.n_corner_last, C.d_surf_last, C.n_surf_last,
         C.g_corner_last.desc, C.g_corner_last.cell_start, C.g_corner_last.pts, C.g_corner_last.idx,
         C.g_surf_last.desc, C.g_surf_last.cell_start, C.g_surf_last.pts, C.g_surf_last.idx,
-        C.d_odom, C.d_factors, C.d_round_cnt + 2 * round);
+        C.d_odom, C.d_factors, C.d_round_cnt + 2 * round, C.d_last_sorted,
+        C.g_corner_win.desc, C.g_corner_win.cell_start, C.g_corner_win.pts, C.g_corner_win.idx,
+        C.g_surf_win.desc, C.g_surf_win.cell_start, C.g_surf_win.pts, C.g_surf_win.idx);
+    HIPCHK(hipGetLastError());
+}
+
+// after the last clouds change: whether each is ordered by scan line (selects grid_window)
+void odom_last_sorted(Ctx& C) {
+    set_counts2(C, C.d_last_sorted, 1, 1);
+    k_line_sorted<<<dim3(64, 2), 256, 0, C.stream>>>(C.d_corner_last, C.d_last_n + 0, C.d_surf_last, C.d_last_n + 1, C.d_last_sorted);
     HIPCHK(hipGetLastError());
 }
 

@@ -174,10 +174,17 @@ def teacher_forced_odometry_inputs(name, k):
     return prev, cur
 
 
-@pytest.mark.parametrize("name,k", [("vlp16", 3), ("hdl64", 2)])
-def test_odometry_frame_teacher_forced(gpu_ctx_factory, name, k):
+@pytest.mark.parametrize("name,k,shuffled", [("vlp16", 3, False), ("hdl64", 2, False), ("vlp16", 4, True)])
+def test_odometry_frame_teacher_forced(gpu_ctx_factory, name, k, shuffled):
+    """shuffled: last clouds not ordered by scan line -> the device must fall back from the grid
+    window search to the literal forward/backward scan and still match the reference loop."""
     lines = synth.SCAN_LINES[name]
     prev, cur = teacher_forced_odometry_inputs(name, k)
+    if shuffled:
+        rng = np.random.default_rng(5)
+        prev = dict(prev)
+        prev["less_sharp"] = prev["less_sharp"][rng.permutation(len(prev["less_sharp"]))]
+        prev["less_flat"] = prev["less_flat"][rng.permutation(len(prev["less_flat"]))]
     q0 = np.array([0.001, -0.002, 0.003, 1.0]); q0 /= np.linalg.norm(q0)
     t0 = np.array([0.9, 0.02, 0.01])
     qw = np.array([0, 0, 0, 1.0]); tw = np.zeros(3)
