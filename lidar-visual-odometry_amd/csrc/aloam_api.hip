@@ -195,6 +195,18 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     C.features_swapped = false;
 }
 
+// the odometry's kd-tree rebuild (laserOdometry.cpp:640-641): 1-NN grids + scan-line-layered
+// window grids of the last clouds, one batched build, and whether the clouds are line-ordered
+static void build_last_grids(Ctx& C) {
+    const GridBuild b[4] = {
+        {&C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
+        {&C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr},
+        {&C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
+        {&C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr}};
+    grid_build_multi(C, b, 4);
+    odom_last_sorted(C);
+}
+
 static void do_odometry(Ctx& C, aloam_odom_result* R) {
     if (!C.have_features) throw ApiError{ALOAM_E_STATE, "odometry before any features"};
     aloam_odom_result r{};
@@ -224,11 +236,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     C.n_corner_last = C.n_lsharp;
     C.n_surf_last = C.n_lflat;
     set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);
-    grid_build(C, C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
-    grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
-    grid_build(C, C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
-    grid_build(C, C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
-    odom_last_sorted(C);
+    build_last_grids(C);
     const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
     r.publish_to_mapping = (C.odom_frame_count % skip == 0);
     if (r.publish_to_mapping) C.odom_frame_count = 0;
@@ -476,11 +484,7 @@ int aloam_set_odom_state(aloam_ctx* ctx, const double q[4], const double t[3], c
     if (ns > 0) HIPCHK(hipMemcpyAsync(C.d_surf_last, surf_last, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
     C.n_corner_last = nc; C.n_surf_last = ns;
     set_counts2(C, C.d_last_n, nc, ns);
-    grid_build(C, C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(nc, 1), nullptr, nullptr);
-    grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(ns, 1), nullptr, nullptr);
-    grid_build(C, C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr);
-    grid_build(C, C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
-    odom_last_sorted(C);
+    build_last_grids(C);
     sync(C);
     C.odom_inited = true;
     API_END

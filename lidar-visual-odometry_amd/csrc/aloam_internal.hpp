@@ -31,6 +31,7 @@ struct GridDesc {
     float ox, oy, oz, cell, inv_cell;
     int dx, dy, dz, ncells, n;
     int nlayers;                   // > 1: cells also split by scan line (layer = int(intensity))
+    int n_acc;                     // build-time counter (published to n by the scatter)
 };
 struct Grid {
     GridDesc* desc = nullptr;      // device
@@ -200,6 +201,8 @@ struct ApiError {
 // ---- launch entry points (defined in the k_*.hip files) ----
 void scan_registration_launch(Ctx& C, const float4* in, int n);
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of, const unsigned char* cube_valid);
+struct GridBuild { Grid* g; const float4* pts; const int* d_n; int cap_n; const int* cube_of; const unsigned char* cube_valid; };
+void grid_build_multi(Ctx& C, const GridBuild* b, int n);   // up to 4 grids in one set of launches
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);

@@ -43,7 +43,7 @@ __device__ inline int cell_coord(float v, float o, float inv) { return (int)floo
 
 __global__ void k_grid_init(GridDesc* d) {
     if (threadIdx.x < 6) d->bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    if (threadIdx.x == 0) { d->n = 0; d->ncells = 0; }
+    if (threadIdx.x == 0) { d->n = 0; d->n_acc = 0; d->ncells = 0; }
 }
 
 __device__ inline bool grid_include(int i, const int* cube_of, const unsigned char* cube_valid) {
@@ -52,62 +52,11 @@ __device__ inline bool grid_include(int i, const int* cube_of, const unsigned ch
     return c >= 0 && cube_valid[c];
 }
 
-__global__ void k_grid_bbox(const float4* __restrict__ pts, const int* d_n, const int* cube_of,
-                            const unsigned char* cube_valid, GridDesc* d) {
-    __shared__ unsigned sh[6];
-    if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    __syncthreads();
-    const int n = *d_n;
-    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-    int cnt = 0;
-    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
-        if (!grid_include(i, cube_of, cube_valid)) continue;
-        float4 p = pts[i];
-        unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
-        for (int a = 0; a < 3; a++) { mn[a] = min(mn[a], v[a]); mx[a] = max(mx[a], v[a]); }
-        cnt++;
-    }
-    for (int a = 0; a < 3; a++) {
-        unsigned long long lo = wave_min_u64(mn[a]), hi = wave_max_u64(mx[a]);
-        if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
-    }
-    cnt = wave_sum_i(cnt);
-    if (lane_id() == 0 && cnt) atomicAdd(&d->n, cnt);
-    __syncthreads();
-    if (threadIdx.x < 3) { atomicMin(&d->bb[threadIdx.x], sh[threadIdx.x]); atomicMax(&d->bb[3 + threadIdx.x], sh[3 + threadIdx.x]); }
-}
 
-__global__ void k_grid_count(const float4* __restrict__ pts, const int* d_n, const int* cube_of,
-                             const unsigned char* cube_valid, GridDesc* d, float min_cell, int nlayers, int* cell_count, int* pcell) {
-    __shared__ GridDesc gd;
-    if (threadIdx.x == 0) {
-        unsigned bb[6];
-        for (int a = 0; a < 6; a++) bb[a] = d->bb[a];
-        gd.n = d->n;
-        grid_params(bb, min_cell, nlayers, &gd);
-        if (blockIdx.x == 0) {
-            d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
-            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers;
-        }
-    }
-    __syncthreads();
-    const int n = *d_n;
-    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
-        if (!grid_include(i, cube_of, cube_valid)) { pcell[i] = -1; continue; }
-        float4 p = pts[i];
-        int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
-        int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
-        int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
-        const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
-        int c = ((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx;
-        pcell[i] = c;
-        atomicAdd(&cell_count[c], 1);
-    }
-}
 
 // three-phase exclusive scan of cell_count[0, ncells) into cell_start
 constexpr int SCAN_CHUNK = 4096;
-__global__ void k_grid_scan1(const int* __restrict__ cnt, const GridDesc* d, int* blk) {
+__device__ __forceinline__ void k_grid_scan1_body(const int* __restrict__ cnt, const GridDesc* d, int* blk) {
     __shared__ int sh[GB / WAVE];
     const int nc = d->ncells;
     const int base = blockIdx.x * SCAN_CHUNK;
@@ -119,7 +68,7 @@ __global__ void k_grid_scan1(const int* __restrict__ cnt, const GridDesc* d, int
     __syncthreads();
     if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < GB / WAVE; w++) t += sh[w]; blk[blockIdx.x] = t; }
 }
-__global__ void k_grid_scan2(int* blk, const GridDesc* d) {
+__device__ __forceinline__ void k_grid_scan2_body(int* blk, const GridDesc* d) {
     __shared__ int sh[1024];
     const int nb = (d->ncells + SCAN_CHUNK - 1) / SCAN_CHUNK;
     // nb <= GRID_MAX_CELLS / SCAN_CHUNK = 2048: two entries per thread
@@ -138,7 +87,7 @@ __global__ void k_grid_scan2(int* blk, const GridDesc* d) {
     if (i0 < nb) blk[i0] = ex;
     if (i1 < nb) blk[i1] = ex + v0;
 }
-__global__ void k_grid_scan3(const int* __restrict__ cnt, const GridDesc* d, const int* blk, int* start) {
+__device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, const GridDesc* d, const int* blk, int* start) {
     __shared__ int sh[SCAN_CHUNK];
     const int nc = d->ncells;
     const int base = blockIdx.x * SCAN_CHUNK;
@@ -170,17 +119,6 @@ __global__ void k_grid_scan3(const int* __restrict__ cnt, const GridDesc* d, con
     if (base + len == nc && threadIdx.x == GB - 1) start[nc] = off + s;
 }
 
-__global__ void k_grid_scatter(const float4* __restrict__ pts, const int* d_n, const int* __restrict__ pcell,
-                               const int* __restrict__ start, int* cell_count, float4* __restrict__ spts, int* __restrict__ sidx) {
-    const int n = *d_n;
-    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
-        int c = pcell[i];
-        if (c < 0) continue;
-        int pos = start[c] + atomicSub(&cell_count[c], 1) - 1;
-        spts[pos] = pts[i];
-        sidx[pos] = i;
-    }
-}
 
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers) {
     g.cap = cap;
@@ -193,20 +131,129 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers) {
     g.pts = (float4*)dalloc(C, sizeof(float4) * cap);
     g.idx = (int*)dalloc(C, sizeof(int) * cap);
     g.pcell = (int*)dalloc(C, sizeof(int) * cap);
+    k_grid_init<<<1, 64, 0, C.stream>>>(g.desc);      // bbox armed for the first build
+    HIPCHK(hipGetLastError());
 }
 
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of,
                 const unsigned char* cube_valid) {
+    const GridBuild b{&g, pts, d_n, cap_n, cube_of, cube_valid};
+    grid_build_multi(C, &b, 1);
+}
+
+// ------------------------------------------------------------------------------------------
+// Batched builds: up to 4 grids in the same 6 launches (blockIdx.y = grid). The bbox is reset by the
+// scatter of the previous build (and once at allocation), so no init launch is needed.
+struct GridJob {
+    GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx; int* pcell;
+    const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
+    float min_cell; int nlayers;
+};
+struct GridJobs { GridJob j[4]; };
+
+__global__ void k_gm_bbox(GridJobs J) {
+    const GridJob& g = J.j[blockIdx.y];
+    __shared__ unsigned sh[6];
+    if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    const int n = *g.d_n;
+    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    int cnt = 0;
+    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
+        if (!grid_include(i, g.cube_of, g.cube_valid)) continue;
+        float4 p = g.pts[i];
+        unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
+        for (int a = 0; a < 3; a++) { mn[a] = min(mn[a], v[a]); mx[a] = max(mx[a], v[a]); }
+        cnt++;
+    }
+    for (int a = 0; a < 3; a++) {
+        unsigned long long lo = wave_min_u64(mn[a]), hi = wave_max_u64(mx[a]);
+        if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
+    }
+    cnt = wave_sum_i(cnt);
+    if (lane_id() == 0 && cnt) atomicAdd(&g.desc->n_acc, cnt);
+    __syncthreads();
+    if (threadIdx.x < 3) { atomicMin(&g.desc->bb[threadIdx.x], sh[threadIdx.x]); atomicMax(&g.desc->bb[3 + threadIdx.x], sh[3 + threadIdx.x]); }
+}
+__global__ void k_gm_count(GridJobs J) {
+    const GridJob& g = J.j[blockIdx.y];
+    __shared__ GridDesc gd;
+    if (threadIdx.x == 0) {
+        unsigned bb[6];
+        for (int a = 0; a < 6; a++) bb[a] = g.desc->bb[a];
+        grid_params(bb, g.min_cell, g.nlayers, &gd);
+        if (blockIdx.x == 0) {
+            GridDesc* d = g.desc;
+            d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
+            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers;
+        }
+    }
+    __syncthreads();
+    const int n = *g.d_n;
+    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
+        if (!grid_include(i, g.cube_of, g.cube_valid)) { g.pcell[i] = -1; continue; }
+        float4 p = g.pts[i];
+        int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
+        int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
+        int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
+        const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
+        int c = ((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx;
+        g.pcell[i] = c;
+        atomicAdd(&g.cell_count[c], 1);
+    }
+}
+__global__ void k_gm_scan1(GridJobs J) {
+    const GridJob& g = J.j[blockIdx.y];
+    if (blockIdx.x * SCAN_CHUNK >= g.desc->ncells) return;
+    k_grid_scan1_body(g.cell_count, g.desc, g.blk);
+}
+__global__ void k_gm_scan2(GridJobs J) {
+    const GridJob& g = J.j[blockIdx.y];
+    k_grid_scan2_body(g.blk, g.desc);
+}
+__global__ void k_gm_scan3(GridJobs J) {
+    const GridJob& g = J.j[blockIdx.y];
+    if (blockIdx.x * SCAN_CHUNK >= g.desc->ncells) return;
+    k_grid_scan3_body(g.cell_count, g.desc, g.blk, g.cell_start);
+}
+__global__ void k_gm_scatter(GridJobs J) {
+    const GridJob& g = J.j[blockIdx.y];
+    const int n = *g.d_n;
+    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
+        int c = g.pcell[i];
+        if (c < 0) continue;
+        int pos = g.cell_start[c] + atomicSub(&g.cell_count[c], 1) - 1;
+        g.spts[pos] = g.pts[i];
+        g.sidx[pos] = i;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {            // publish n, re-arm bbox/counter for the next build
+        GridDesc* d = g.desc;
+        d->n = d->n_acc;
+        d->n_acc = 0;
+        for (int a = 0; a < 3; a++) { d->bb[a] = 0xffffffffu; d->bb[3 + a] = 0u; }
+    }
+}
+
+void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
+    if (nj <= 0) return;
+    if (nj > 4) throw ApiError{ALOAM_E_ARG, "grid_build_multi: at most 4 grids"};
     hipStream_t st = C.stream;
-    const int nb = std::max(1, std::min(1024, (cap_n + GB - 1) / GB));
-    k_grid_init<<<1, 64, 0, st>>>(g.desc);
-    k_grid_bbox<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc);
-    k_grid_count<<<nb, GB, 0, st>>>(pts, d_n, cube_of, cube_valid, g.desc, g.min_cell, g.nlayers, g.cell_count, g.pcell);
+    GridJobs J{};
+    int cap = 1;
+    for (int k = 0; k < nj; k++) {
+        const Grid& g = *b[k].g;
+        J.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell,
+                         b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid, g.min_cell, g.nlayers};
+        cap = std::max(cap, b[k].cap_n);
+    }
+    const int nb = std::max(1, std::min(1024, (cap + GB - 1) / GB));
     const int nsb = GRID_MAX_CELLS / SCAN_CHUNK;
-    k_grid_scan1<<<nsb, GB, 0, st>>>(g.cell_count, g.desc, g.blk);
-    k_grid_scan2<<<1, 1024, 0, st>>>(g.blk, g.desc);
-    k_grid_scan3<<<nsb, GB, 0, st>>>(g.cell_count, g.desc, g.blk, g.cell_start);
-    k_grid_scatter<<<nb, GB, 0, st>>>(pts, d_n, g.pcell, g.cell_start, g.cell_count, g.pts, g.idx);
+    k_gm_bbox<<<dim3(nb, nj), GB, 0, st>>>(J);
+    k_gm_count<<<dim3(nb, nj), GB, 0, st>>>(J);
+    k_gm_scan1<<<dim3(nsb, nj), GB, 0, st>>>(J);
+    k_gm_scan2<<<dim3(1, nj), 1024, 0, st>>>(J);
+    k_gm_scan3<<<dim3(nsb, nj), GB, 0, st>>>(J);
+    k_gm_scatter<<<dim3(nb, nj), GB, 0, st>>>(J);
     HIPCHK(hipGetLastError());
 }
 

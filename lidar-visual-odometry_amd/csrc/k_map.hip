@@ -549,8 +549,9 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
     k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid);
     k_map_shift<<<nblk(C.n_mc), MB, 0, st>>>(C.d_mc_cube, C.d_map_n + 0, C.d_map);
     k_map_shift<<<nblk(C.n_ms), MB, 0, st>>>(C.d_ms_cube, C.d_map_n + 1, C.d_map);
-    grid_build(C, C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid);
-    grid_build(C, C.g_map_surf, C.d_ms, C.d_map_n + 1, std::max(C.n_ms, 1), C.d_ms_cube, C.d_cube_valid);
+    const GridBuild gb[2] = {{&C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid},
+                             {&C.g_map_surf, C.d_ms, C.d_map_n + 1, std::max(C.n_ms, 1), C.d_ms_cube, C.d_cube_valid}};
+    grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
     // stacks (:542-550)
     voxel_grid_sorted(C, C.d_map_corner_in, C.d_map_in_n + 0, ub_c, C.P.mapping_line_resolution, C.d_cstack, C.d_stack_n + 0);
