@@ -144,8 +144,37 @@ static void allocate(Ctx& C) {
     C.d_ins_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_voxel);
     C.d_ins_val = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     C.d_ins_val2 = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    // lane scratch: lane 0 aliases the buffers above, lane 1 is a second set for stream2
+    KindScratch& k0 = C.ks[0];
+    k0.vkeys = C.d_vkeys; k0.vkeys2 = C.d_vkeys2; k0.vvals = C.d_vvals; k0.vvals2 = C.d_vvals2;
+    k0.sort_tmp = C.d_sort_tmp; k0.ins_pts = C.d_ins_pts; k0.ins_val = C.d_ins_val; k0.ins_val2 = C.d_ins_val2;
+    k0.seg_keys = C.d_seg_keys; k0.blk = C.d_blk; k0.map_tmp = C.d_map_tmp;
+    KindScratch& k1 = C.ks[1];
+    k1.vkeys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)C.cap_voxel);
+    k1.vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
+    k1.vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    k1.vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
+    k1.sort_tmp = dalloc(C, C.sort_tmp_bytes);
+    k1.ins_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_voxel);
+    k1.ins_val = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    k1.ins_val2 = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    k1.seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (4 * (size_t)M + 32768));
+    k1.blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, M / 256 + 1) + 4096));
+    k1.map_tmp = (float4*)dalloc(C, sizeof(float4) * M);
+    HIPCHK(hipStreamCreateWithFlags(&C.stream2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
     C.ev_ready = true;
+}
+
+void fork_lane1(Ctx& C) {
+    HIPCHK(hipEventRecord(C.ev_fork, C.stream));
+    HIPCHK(hipStreamWaitEvent(C.stream2, C.ev_fork, 0));
+}
+void join_lane1(Ctx& C) {
+    HIPCHK(hipEventRecord(C.ev_join, C.stream2));
+    HIPCHK(hipStreamWaitEvent(C.stream, C.ev_join, 0));
 }
 
 static void sync(Ctx& C) {
@@ -391,6 +420,8 @@ aloam_ctx* aloam_create(const aloam_params* p, int device) {
         g_create_err = e.msg;
         for (auto& b : C->bufs) (void)hipFree(b.p);
         if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
+        if (C->stream2) (void)hipStreamDestroy(C->stream2);
+        if (C->stream) (void)hipStreamDestroy(C->stream);
         delete C;
         return nullptr;
     }
@@ -403,9 +434,13 @@ void aloam_destroy(aloam_ctx* ctx) {
     Ctx* C = (Ctx*)ctx;
     (void)hipSetDevice(C->device);
     if (C->stream) (void)hipStreamSynchronize(C->stream);
+    if (C->stream2) (void)hipStreamSynchronize(C->stream2);
     if (C->ev_ready) for (int i = 0; i < Ctx::NEV; i++) (void)hipEventDestroy(C->ev[i]);
+    if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
+    if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     for (auto& b : C->bufs) (void)hipFree(b.p);
     if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
+    if (C->stream2) (void)hipStreamDestroy(C->stream2);
     if (C->stream) (void)hipStreamDestroy(C->stream);
     delete C;
 }

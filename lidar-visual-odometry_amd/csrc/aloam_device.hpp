@@ -393,6 +393,49 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
     }
     return found;
 }
+// Exclusive scan of one int per thread over a whole workgroup of NT threads (NT/64 waves):
+// wave shuffle scans + one LDS round for the wave totals. Returns the exclusive prefix; *total =
+// the workgroup sum (all threads). Two barriers.
+template <int NT>
+__device__ __forceinline__ int block_exscan(int v, int* total) {
+    __shared__ int wsum[NT / WAVE];
+    __shared__ int wtot;
+    const int lane = lane_id(), w = threadIdx.x / WAVE;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int t = __shfl_up(incl, o, WAVE);
+        if (lane >= o) incl += t;
+    }
+    if (lane == WAVE - 1) wsum[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        const int x = lane < NT / WAVE ? wsum[lane] : 0;
+        int xi = x;
+#pragma unroll
+        for (int o = 1; o < NT / WAVE; o <<= 1) {
+            const int t = __shfl_up(xi, o, WAVE);
+            if (lane >= o) xi += t;
+        }
+        if (lane < NT / WAVE) wsum[lane] = xi - x;
+        if (lane == NT / WAVE - 1) wtot = xi;
+    }
+    __syncthreads();
+    *total = wtot;
+    return wsum[w] + incl - v;
+}
+// In-place exclusive scan of a[0, n) by one workgroup of 1024 threads (each owns a contiguous
+// chunk); *total = sum. For the small "per-block count" scans.
+__device__ __forceinline__ void block_scan_array(int* a, int n, int* total) {
+    const int per = (n + 1023) / 1024;
+    const int b0 = threadIdx.x * per, b1 = min(n, b0 + per);
+    int s = 0;
+    for (int i = b0; i < b1; i++) s += a[i];
+    int tot;
+    int run = block_exscan<1024>(s, &tot);
+    for (int i = b0; i < b1; i++) { const int v = a[i]; a[i] = run; run += v; }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
 // PCL 1.8 VoxelGrid leaf grid from an ordered-int bbox (voxel_grid.cpp applyFilter)
 __device__ inline void voxel_params(const unsigned* bb, float leaf, bool* overflow, int minb[3], int* mul1, int* mul2) {
     const float inv = 1.0f / leaf;

@@ -80,11 +80,23 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+struct KindScratch {               // per-lane scratch for the map kinds' concurrent work
+    unsigned long long *vkeys = nullptr, *vkeys2 = nullptr;   // 2 x cap_voxel, cap_voxel
+    int *vvals = nullptr, *vvals2 = nullptr;                  // cap_voxel, cap_voxel + 64 (+ VoxHdr)
+    void* sort_tmp = nullptr;
+    float4* ins_pts = nullptr;
+    int *ins_val = nullptr, *ins_val2 = nullptr;
+    unsigned long long* seg_keys = nullptr;                   // 4 x cap_map + 32768
+    int* blk = nullptr;
+    float4* map_tmp = nullptr;
+};
 struct Ctx {
     aloam_params P;
     int device = 0;
     std::string err;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;   // mapping: the surf half of the per-kind work runs here (fork/join)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool profiling = false;
     aloam_timing timing{};
     std::vector<DevBuf> bufs;
@@ -178,6 +190,7 @@ struct Ctx {
     // profiling events: [0..1] scan, [2..3] odom, [4..5] map, search pairs after that
     static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS;
     hipEvent_t ev[NEV];
+    KindScratch ks[2];
     bool ev_ready = false;
 };
 
@@ -215,7 +228,11 @@ void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int
 void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2);
 size_t voxel_sort_tmp_bytes(int cap);
 size_t cube_sort_tmp_bytes(int cap);
-void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout);
+// lane 0: C.stream + the primary scratch; lane 1: C.stream2 + the second scratch set
+void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane = 0);
+void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit, int lane = 0);
+void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so far
+void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
 void map_frame_launch(Ctx& C, aloam_map_result* R);
 void* dalloc(Ctx& C, size_t bytes);
 

@@ -25,7 +25,6 @@
 namespace aloam {
 
 void prof_mark(Ctx& C, int idx);
-void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit);
 void segment_voxel_launch(Ctx& C, const float4* pts, const int* off, const int* seg_list, const int* nseg_p, int max_seg,
                           float leaf, float4* out, int* seg_nout, unsigned long long* gkeys);
 
@@ -278,34 +277,29 @@ __global__ void k_cube_count_new(const unsigned* __restrict__ skey, int ub, Cube
     }
 }
 // single block: exclusive scan over cubes of v(c); mode 0: cnt_old+cnt_new -> off ; mode 1: final counts -> final_off
-__global__ void k_cube_scan(CubeArrays a, const unsigned char* __restrict__ valid, int mode, int* total) {
-    __shared__ int sh[1024];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
+__global__ void __launch_bounds__(1024) k_cube_scan(CubeArrays a, const unsigned char* __restrict__ valid, int mode, int* total) {
+    constexpr int PER = (CUBE_N + 1023) / 1024;
     int* dst = mode == 0 ? a.off : a.final_off;
-    for (int base = 0; base < CUBE_N; base += 1024) {
-        const int c = base + threadIdx.x;
-        int v = 0;
+    const int c0 = threadIdx.x * PER;
+    int v[PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int c = c0 + k;
+        v[k] = 0;
         if (c < CUBE_N) {
-            if (mode == 0) v = old_count(a, c) + new_count(a, c);
-            else v = valid[c] ? a.seg_nout[c] : old_count(a, c) + new_count(a, c);
+            if (mode == 0) v[k] = old_count(a, c) + new_count(a, c);
+            else v[k] = valid[c] ? a.seg_nout[c] : old_count(a, c) + new_count(a, c);
         }
-        sh[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += t;
-            __syncthreads();
-        }
-        const int incl = sh[threadIdx.x];
-        if (c < CUBE_N) dst[c] = carry + incl - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += incl;
-        __syncthreads();
+        s += v[k];
     }
-    if (threadIdx.x == 0) { dst[CUBE_N] = carry; if (total) *total = carry; }
+    int tot;
+    int run = block_exscan<1024>(s, &tot);
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        if (c0 + k < CUBE_N) dst[c0 + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 0) { dst[CUBE_N] = tot; if (total) *total = tot; }
 }
 __global__ void k_cube_scatter(const float4* __restrict__ old_pts, const int* __restrict__ old_cube, const int* d_n_old,
                                const float4* __restrict__ ins_pts, const unsigned* __restrict__ skey, const int* __restrict__ sval,
@@ -374,7 +368,10 @@ __global__ void k_cubevox_bbox(const float4* __restrict__ B, CubeArrays a, const
         const unsigned u[3] = {f2ord(q.x), f2ord(q.y), f2ord(q.z)};
         for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], u[d]); mx[d] = max(mx[d], u[d]); }
     }
-    for (int d = 0; d < 3; d++) { atomicMin(&sh[d], mn[d]); atomicMax(&sh[3 + d], mx[d]); }
+    for (int d = 0; d < 3; d++) {
+        const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
+        if (lane_id() == 0) { atomicMin(&sh[d], (unsigned)lo); atomicMax(&sh[3 + d], (unsigned)hi); }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int d = 0; d < 6; d++) v->bb[r][d] = sh[d];
@@ -463,35 +460,15 @@ size_t cube_sort_tmp_bytes(int cap) {
 }
 
 __global__ void k_scan_small_m(int* a, int nb, int* total) {
-    __shared__ int sh[1024];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < nb; base += 1024) {
-        int i = base + threadIdx.x;
-        int v = i < nb ? a[i] : 0;
-        sh[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += t;
-            __syncthreads();
-        }
-        int incl = sh[threadIdx.x];
-        if (i < nb) a[i] = carry + incl - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += incl;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && total) *total = carry;
+    block_scan_array(a, nb, total);
 }
 
 // ------------------------------------------------------------------------------------------
 static int nblk(int n) { return std::max(1, std::min(2048, (n + MB - 1) / MB)); }
 
 static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, const int* d_stack_n, float leaf) {
-    hipStream_t st = C.stream;
+    hipStream_t st = which ? C.stream2 : C.stream;          // the kinds rebuild concurrently
+    KindScratch& K = C.ks[which];
     float4* A = which == 0 ? C.d_mc : C.d_ms;
     int* Acube = which == 0 ? C.d_mc_cube : C.d_ms_cube;
     float4* B = which == 0 ? C.d_mc2 : C.d_ms2;
@@ -505,20 +482,20 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     a.last_new = base + 3 * (CUBE_N + 1); a.off = base + 4 * (CUBE_N + 1); a.seg_nout = base + 5 * (CUBE_N + 1);
     a.final_off = base + 6 * (CUBE_N + 1);
     if (C.n_mc + C.n_ms + 2 * ub_new > C.cap_map) throw ApiError{ALOAM_E_CAPACITY, "map capacity exceeded"};
-    unsigned* k1 = (unsigned*)C.d_vkeys;
-    unsigned* k2 = (unsigned*)C.d_vkeys2;
-    k_map_insert<<<nblk(ub_new), MB, 0, st>>>(stack, d_stack_n, ub_new, C.d_map, C.d_ins_pts, k1, C.d_ins_val);
-    if (ub_new > 0) stable_sort_pairs(C, k1, k2, C.d_ins_val, C.d_ins_val2, ub_new, 13);
+    unsigned* k1 = (unsigned*)K.vkeys;
+    unsigned* k2 = (unsigned*)K.vkeys2;
+    k_map_insert<<<nblk(ub_new), MB, 0, st>>>(stack, d_stack_n, ub_new, C.d_map, K.ins_pts, k1, K.ins_val);
+    if (ub_new > 0) stable_sort_pairs(C, k1, k2, K.ins_val, K.ins_val2, ub_new, 13, which);
     k_cube_reset<<<(CUBE_N + 1 + 255) / 256, 256, 0, st>>>(a);
     k_cube_count_old<<<nblk(n_old_ub), MB, 0, st>>>(Acube, d_n_old, a);
     k_cube_count_new<<<nblk(ub_new), MB, 0, st>>>(k2, ub_new, a);
     k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 0, nullptr);
-    k_cube_scatter<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(A, Acube, d_n_old, C.d_ins_pts, k2, C.d_ins_val2, ub_new, a, B, Bcube);
+    k_cube_scatter<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(A, Acube, d_n_old, K.ins_pts, k2, K.ins_val2, ub_new, a, B, Bcube);
     // per-cube VoxelGrid of the surrounding cubes into Cf at the same offsets (one stable radix sort)
-    float4* Cf = C.d_map_tmp;
+    float4* Cf = K.map_tmp;
     const int ub_tot = n_old_ub + ub_new;
-    CubeVox* cv = (CubeVox*)C.d_seg_keys;                         // scratch header
-    unsigned long long* vk1 = C.d_seg_keys + 32768;
+    CubeVox* cv = (CubeVox*)K.seg_keys;                         // scratch header
+    unsigned long long* vk1 = K.seg_keys + 32768;
     unsigned long long* vk2 = vk1 + (size_t)C.cap_map;
     int* vv1 = (int*)(vk2 + (size_t)C.cap_map);
     int* vv2 = vv1 + (size_t)C.cap_map;
@@ -529,10 +506,10 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     k_cubevox_keys<<<nblk(ub_tot), MB, 0, st>>>(B, Bcube, a, cv, leaf, ub_tot, vk1, vv1);
     if (ub_tot > 0) {
         size_t bytes = C.sort_tmp_bytes;
-        HIPCHK(rocprim::radix_sort_pairs(C.d_sort_tmp, bytes, vk1, vk2, vv1, vv2, (unsigned)ub_tot, 0, 39, st));
-        k_cubevox_flags<<<nbt, MB, 0, st>>>(vk2, ub_tot, C.d_blk);
-        k_scan_small_m<<<1, 1024, 0, st>>>(C.d_blk, nbt, &cv->nrun);
-        k_cubevox_heads<<<nbt, MB, 0, st>>>(vk2, ub_tot, C.d_blk, heads, cv);
+        HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, vk1, vk2, vv1, vv2, (unsigned)ub_tot, 0, 39, st));
+        k_cubevox_flags<<<nbt, MB, 0, st>>>(vk2, ub_tot, K.blk);
+        k_scan_small_m<<<1, 1024, 0, st>>>(K.blk, nbt, &cv->nrun);
+        k_cubevox_heads<<<nbt, MB, 0, st>>>(vk2, ub_tot, K.blk, heads, cv);
         k_cubevox_centroids<<<nbt, MB, 0, st>>>(B, vk2, vv2, heads, &cv->nrun, ub_tot, C.d_map, cv, a, Cf);
     }
     k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 1, d_n_old);
@@ -554,8 +531,10 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
     grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
     // stacks (:542-550)
-    voxel_grid_sorted(C, C.d_map_corner_in, C.d_map_in_n + 0, ub_c, C.P.mapping_line_resolution, C.d_cstack, C.d_stack_n + 0);
-    voxel_grid_sorted(C, C.d_map_surf_in, C.d_map_in_n + 1, ub_s, C.P.mapping_plane_resolution, C.d_sstack, C.d_stack_n + 1);
+    fork_lane1(C);
+    voxel_grid_sorted(C, C.d_map_corner_in, C.d_map_in_n + 0, ub_c, C.P.mapping_line_resolution, C.d_cstack, C.d_stack_n + 0, 0);
+    voxel_grid_sorted(C, C.d_map_surf_in, C.d_map_in_n + 1, ub_s, C.P.mapping_plane_resolution, C.d_sstack, C.d_stack_n + 1, 1);
+    join_lane1(C);
     const int nq = ub_c + ub_s;
     HIPCHK(hipMemsetAsync(C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, 0, sizeof(int) * 2 * ALOAM_MAX_ROUNDS, st));
     if (nq > 0) {
@@ -574,8 +553,10 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
         }
     }
     k_map_update<<<1, 1, 0, st>>>(C.d_map);
+    fork_lane1(C);
     rebuild_map(C, 0, ub_c, C.d_cstack, C.d_stack_n + 0, C.P.mapping_line_resolution);
     rebuild_map(C, 1, ub_s, C.d_sstack, C.d_stack_n + 1, C.P.mapping_plane_resolution);
+    join_lane1(C);
     if (C.n_map_full_in > 0)
         k_map_register<<<(C.n_map_full_in + MB - 1) / MB, MB, 0, st>>>(C.d_map_full_in, C.n_map_full_in, C.d_map, C.d_registered);
     HIPCHK(hipGetLastError());

@@ -57,28 +57,7 @@ __global__ void k_filter_count(const float4* __restrict__ in, int n, int dense, 
 
 // single block of 1024: exclusive scan of nb ints in place, total -> *total
 __global__ void k_scan_small(int* a, int nb, int* total) {
-    __shared__ int sh[1024];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < nb; base += 1024) {
-        int i = base + threadIdx.x;
-        int v = i < nb ? a[i] : 0;
-        sh[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += t;
-            __syncthreads();
-        }
-        int incl = sh[threadIdx.x];
-        if (i < nb) a[i] = carry + incl - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += incl;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && total) *total = carry;
+    block_scan_array(a, nb, total);
 }
 
 __global__ void k_filter_scatter(const float4* __restrict__ in, int n, int dense, float thres, const int* blk,

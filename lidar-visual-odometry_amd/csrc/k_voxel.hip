@@ -87,60 +87,48 @@ __global__ void k_vox_centroids(const float4* __restrict__ pts, const int* d_n, 
     if (r == 0) *d_nout = nrun;
     if (r >= nrun) return;
     const int h0 = heads[r], h1 = r + 1 < nrun ? heads[r + 1] : n;
+    // sequential fp32 sum in sorted order (PCL's accumulation order), 8 loads in flight per step
     float4 c = pts[vals[h0]];
-    for (int t = h0 + 1; t < h1; t++) {
-        float4 p = pts[vals[t]];
-        c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
+    for (int t0 = h0 + 1; t0 < h1; t0 += 8) {
+        int vi[8];
+        float4 p[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) vi[u] = t0 + u < h1 ? vals[t0 + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; u++) p[u] = vi[u] >= 0 ? pts[vi[u]] : make_float4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (vi[u] >= 0) { c.x += p[u].x; c.y += p[u].y; c.z += p[u].z; c.w += p[u].w; }
     }
     const float cnt = (float)(h1 - h0);
     out[r] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
 }
 
 __global__ void k_scan_small_v(int* a, int nb, int* total) {
-    __shared__ int sh[1024];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < nb; base += 1024) {
-        int i = base + threadIdx.x;
-        int v = i < nb ? a[i] : 0;
-        sh[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += t;
-            __syncthreads();
-        }
-        int incl = sh[threadIdx.x];
-        if (i < nb) a[i] = carry + incl - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += incl;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && total) *total = carry;
+    block_scan_array(a, nb, total);
 }
 
-void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout) {
-    hipStream_t st = C.stream;
+void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane) {
+    hipStream_t st = lane ? C.stream2 : C.stream;
+    KindScratch& K = C.ks[lane];
     if (cap_n <= 0) { HIPCHK(hipMemsetAsync(d_nout, 0, sizeof(int), st)); return; }
     if (cap_n > C.cap_voxel) throw ApiError{ALOAM_E_CAPACITY, "voxel grid capacity exceeded"};
-    VoxHdr* h = (VoxHdr*)(C.d_vvals2 + C.cap_voxel);   // header lives behind the value buffer
-    unsigned* k1 = (unsigned*)C.d_vkeys;
-    unsigned* k2 = (unsigned*)C.d_vkeys2;
-    int* blk = C.d_blk;
-    int* heads = (int*)(C.d_vkeys + C.cap_voxel);      // second half of the key scratch
+    VoxHdr* h = (VoxHdr*)(K.vvals2 + C.cap_voxel);   // header lives behind the value buffer
+    unsigned* k1 = (unsigned*)K.vkeys;
+    unsigned* k2 = (unsigned*)K.vkeys2;
+    int* blk = K.blk;
+    int* heads = (int*)(K.vkeys + C.cap_voxel);      // second half of the key scratch
     const int nb = (cap_n + VB - 1) / VB;
     const int nbr = std::min(nb, 1024);
     k_vox_init<<<1, 64, 0, st>>>(h);
     k_vox_bbox<<<nbr, VB, 0, st>>>(pts, d_n, h);
-    k_vox_keys<<<nbr, VB, 0, st>>>(pts, d_n, cap_n, h, leaf, k1, C.d_vvals);
+    k_vox_keys<<<nbr, VB, 0, st>>>(pts, d_n, cap_n, h, leaf, k1, K.vvals);
     size_t bytes = C.sort_tmp_bytes;
-    HIPCHK(rocprim::radix_sort_pairs(C.d_sort_tmp, bytes, k1, k2, C.d_vvals, C.d_vvals2, (unsigned)cap_n, 0, 32, st));
+    HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, k1, k2, K.vvals, K.vvals2, (unsigned)cap_n, 0, 32, st));
     k_vox_flags<<<nb, VB, 0, st>>>(k2, d_n, cap_n, blk);
     k_scan_small_v<<<1, 1024, 0, st>>>(blk, nb, &h->nrun);
     k_vox_heads<<<nb, VB, 0, st>>>(k2, d_n, blk, heads);
-    k_vox_centroids<<<nb, VB, 0, st>>>(pts, d_n, &h->nrun, heads, C.d_vvals2, out, d_nout);
+    k_vox_centroids<<<nb, VB, 0, st>>>(pts, d_n, &h->nrun, heads, K.vvals2, out, d_nout);
     HIPCHK(hipGetLastError());
 }
 
@@ -152,9 +140,10 @@ size_t voxel_sort_tmp_bytes(int cap) {
 }
 
 // stable sort of (unsigned key, int value) pairs — used to order inserted map points by cube
-void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit) {
+void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit, int lane) {
     size_t bytes = C.sort_tmp_bytes;
-    HIPCHK(rocprim::radix_sort_pairs(C.d_sort_tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0, end_bit, C.stream));
+    HIPCHK(rocprim::radix_sort_pairs(C.ks[lane].sort_tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0, end_bit,
+                                     lane ? C.stream2 : C.stream));
 }
 
 // ------------------------------------------------------------------------------------------
