@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ALOAM_ABI_VERSION 1
+#define ALOAM_ABI_VERSION 2
 
 /* error codes */
 #define ALOAM_OK             0
@@ -205,11 +205,17 @@ int aloam_eval_factors(aloam_ctx* ctx, const aloam_factor* f, int n, const doubl
 int aloam_lm_solve(aloam_ctx* ctx, const aloam_factor* f, int n, double x[7], aloam_lm_summary* s);
 /* PCL VoxelGrid (downsample_all_data, x,y,z,intensity centroids) on one cloud. */
 int aloam_voxel_grid(aloam_ctx* ctx, const float* pts, int n, float leaf, aloam_cloud* out);
-/* Exact k-NN (k <= 8) of each query in a point set by float L2 on x,y,z, sorted by distance,
- * ties by index; idx = -1 / d2 = +inf when fewer than k points exist within radius
- * (radius <= 0: unbounded). */
+/* Exact radius k-NN (k <= 8, radius > 0) of each query in a point set by float L2 on x,y,z,
+ * sorted by distance, ties by index; idx = -1 / d2 = +inf when fewer than k points lie within
+ * the radius — the KdTreeFLANN::nearestKSearch + distance gate of laserMapping.cpp:582-584,648-650
+ * (host buffers). */
 int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int nq, int k,
               float radius, int* idx, float* d2);
+/* The same search on device-resident data (~240k queries against a ~2M-point
+ * local map): d_pts / d_queries are device float4 (x, y, z, w) arrays, d_idx / d_d2 device arrays
+ * of nq * k; the index is built in context memory grown on demand. Synchronous. */
+int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k,
+                     float radius, int* d_idx, float* d_d2);
 
 /* Timing of the last pipeline call, measured with HIP events on the context's stream. */
 typedef struct aloam_timing {
@@ -222,6 +228,9 @@ typedef struct aloam_timing {
     int   map_search_launches;
     double map_search_bytes;  /* algorithmic bytes of the mapping searches     */
     double odom_search_bytes;
+    float knn_ms;             /* aloam_knn_device: search kernel time (HIP events)              */
+    int   knn_launches;
+    double knn_bytes;         /* its algorithmic bytes: sum_q (16 + 16 |C27(q)|) + 8 k Q         */
 } aloam_timing;
 int aloam_set_profiling(aloam_ctx* ctx, int enable);
 int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);

@@ -56,7 +56,8 @@ def _declare(L):
     L.aloam_set_profiling.argtypes = [vp, C.c_int]
     L.aloam_get_timing.argtypes = [vp, C.POINTER(abi.Timing)]
     L.aloam_forward_mapping_input.argtypes = [vp, vp]
-    for name in ("aloam_forward_mapping_input", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
+    L.aloam_knn_device.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_float, vp, vp]
+    for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
                  "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
                  "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
                  "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing"):
@@ -80,7 +81,7 @@ EXPORTED_SYMBOLS = [
     "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
     "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
     "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing",
-    "aloam_forward_mapping_input",
+    "aloam_forward_mapping_input", "aloam_knn_device",
 ]
 
 
@@ -239,6 +240,11 @@ class Context:
         d2 = np.zeros((len(q), k), np.float32)
         self._check(lib().aloam_knn(self.h, abi.fptr(pts), len(pts), abi.fptr(q), len(q), k, radius, abi.iptr(idx), abi.fptr(d2)))
         return idx, d2
+
+    def knn_device(self, d_pts, n, d_queries, nq, k, radius, d_idx, d_d2):
+        """aloam_knn_device on device pointers (ints, e.g. torch tensor .data_ptr())."""
+        self._check(lib().aloam_knn_device(self.h, C.c_void_p(d_pts), int(n), C.c_void_p(d_queries), int(nq), int(k),
+                                           float(radius), C.c_void_p(d_idx), C.c_void_p(d_d2)))
 
     def set_profiling(self, on):
         self._check(lib().aloam_set_profiling(self.h, int(on)))

@@ -23,7 +23,9 @@ void* dalloc(Ctx& C, size_t bytes) {
     void* p = nullptr;
     bytes = std::max<size_t>(bytes, 16);
     HIPCHK(hipMalloc(&p, bytes));
-    HIPCHK(hipMemset(p, 0, bytes));
+    // zeroed on the context's (non-blocking) stream, so every later kernel of the context is ordered
+    // after it; a plain hipMemset runs on the null stream, which a non-blocking stream does not wait for
+    HIPCHK(hipMemsetAsync(p, 0, bytes, C.stream));
     C.bufs.push_back({p, bytes});
     return p;
 }
@@ -83,7 +85,7 @@ static void allocate(Ctx& C) {
     std::memset(&C.h_odom, 0, sizeof(C.h_odom));
     C.h_odom.para[3] = 1.0;
     C.h_odom.q_w[3] = 1.0;
-    HIPCHK(hipMemcpy(C.d_odom, &C.h_odom, sizeof(OdomState), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(C.d_odom, &C.h_odom, sizeof(OdomState), hipMemcpyHostToDevice, C.stream));
     grid_alloc(C, C.g_corner_last, capLS, 2.5f * 1.025f);   // two-phase 1-NN, k_odom.hip
     grid_alloc(C, C.g_surf_last, N, 2.5f * 1.025f);
     const int layers = std::min(MAXL, std::max(P.scan_line, 1));
@@ -109,7 +111,7 @@ static void allocate(Ctx& C) {
     C.cap_map = M;
     C.d_map = (MapState*)dalloc(C, sizeof(MapState));
     init_map_state(C.h_map);
-    HIPCHK(hipMemcpy(C.d_map, &C.h_map, sizeof(MapState), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(C.d_map, &C.h_map, sizeof(MapState), hipMemcpyHostToDevice, C.stream));
     C.d_mc = (float4*)dalloc(C, sizeof(float4) * M);
     C.d_ms = (float4*)dalloc(C, sizeof(float4) * M);
     C.d_mc2 = (float4*)dalloc(C, sizeof(float4) * M);
@@ -123,8 +125,8 @@ static void allocate(Ctx& C) {
     C.d_map_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_cube_cnt = (int*)dalloc(C, sizeof(int) * 2 * 7 * (CUBE_N + 1));
     C.d_cube_valid = (unsigned char*)dalloc(C, CUBE_N);
-    grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f);     // 5-NN within 1 m, 3x3x3 cells
-    grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f);
+    grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f, 1, true);     // 5-NN within 1 m, 3x3x3 cells
+    grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f, 1, true);
     C.d_map_corner_in = (float4*)dalloc(C, sizeof(float4) * capLS);
     C.d_map_surf_in = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_map_full_in = (float4*)dalloc(C, sizeof(float4) * N);
@@ -166,6 +168,7 @@ static void allocate(Ctx& C) {
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
     C.ev_ready = true;
+    HIPCHK(hipStreamSynchronize(C.stream));   // all zero-fills and init kernels done
 }
 
 void fork_lane1(Ctx& C) {
@@ -180,7 +183,8 @@ void join_lane1(Ctx& C) {
 static void sync(Ctx& C) {
     HIPCHK(hipStreamSynchronize(C.stream));
     if (*(volatile int*)C.h_bar_err) {   // a solver grid barrier timed out: reset it and report (results void)
-        HIPCHK(hipMemset(C.d_bar, 0, sizeof(unsigned) * 4));
+        HIPCHK(hipMemsetAsync(C.d_bar, 0, sizeof(unsigned) * 4, C.stream));
+        HIPCHK(hipStreamSynchronize(C.stream));
         *(volatile int*)C.h_bar_err = 0;
         throw ApiError{ALOAM_E_HIP, "LM grid barrier timed out (workgroups not co-resident)"};
     }
@@ -702,6 +706,40 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
     grid_build(C, C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr);
     sync(C);
     C.have_map_input = false;
+    API_END
+}
+
+int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k, float radius,
+                     int* d_idx, float* d_d2) {
+    API_BEGIN(ctx)
+    if (n < 0 || nq < 0 || k < 1 || k > 8 || !(radius > 0) || (n > 0 && !d_pts) || (nq > 0 && (!d_queries || !d_idx || !d_d2)))
+        throw ApiError{ALOAM_E_ARG, "bad knn args (device pointers, radius > 0, 1 <= k <= 8)"};
+    if (!C.d_knn_n) C.d_knn_n = (int*)dalloc(C, sizeof(int) * 2);
+    if (C.g_knn.cap < std::max(n, 1)) {          // grow (old buffers are released with the context)
+        Grid g{};
+        grid_alloc(C, g, std::max(std::max(n, 1), C.g_knn.cap * 2), radius * 1.025f, 1, true);
+        C.g_knn = g;
+    }
+    C.g_knn.min_cell = radius * 1.025f;           // cells >= radius: the 27-cell block holds the ball
+    set_counts2(C, C.d_knn_n, n, 0);
+    grid_build(C, C.g_knn, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr);
+    if (C.profiling) {
+        HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long), C.stream));
+        HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 2], C.stream));
+    }
+    knn_device_launch(C, C.g_knn, (const float4*)d_queries, nq, k, radius, d_idx, d_d2, C.profiling ? C.d_cand : nullptr);
+    unsigned long long cand = 0;
+    if (C.profiling) {
+        HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 1], C.stream));
+        HIPCHK(hipMemcpyAsync(&cand, C.d_cand, sizeof(cand), hipMemcpyDeviceToHost, C.stream));
+    }
+    sync(C);
+    if (C.profiling) {
+        C.timing.knn_ms = ev_ms(C, Ctx::NEV - 2, Ctx::NEV - 1);
+        C.timing.knn_launches = 1;
+        // B = sum_q [16 + 16 |C27(q)|] + 8 k Q
+        C.timing.knn_bytes = 16.0 * nq + 16.0 * (double)cand + 8.0 * k * (double)nq;
+    }
     API_END
 }
 

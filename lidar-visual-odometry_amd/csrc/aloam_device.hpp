@@ -300,41 +300,50 @@ __device__ __forceinline__ int thread_knn27(const float ox, const float oy, cons
     return found;
 }
 // Exact radius k-NN of one query by a GROUP of GS aligned lanes (GS | 64) over the 3x3x3 cell
-// block: every lane loads the 9 row bounds (same addresses across the group: one coalesced round
-// trip), the rows are flattened through their prefix sums, lane l streams candidates l, l+GS, ...
-// (4 point + index loads in flight), keeps a sorted top-K by (d2, index), and K rounds of a group
-// min over 64-bit keys merge the lanes' lists. Same total order as the wave / thread versions.
-// Every lane returns the same result.
-template <int K, int GS>
+// block. The 9 row bounds are loaded together (same addresses across the group: one coalesced
+// round trip) into a per-group LDS table tab[20] (row base - prefix, prefix); the rows are
+// flattened, lane l streams candidates l, l+GS, ... tracking its row incrementally (candidates
+// only move forward), 4 loads in flight, and keeps a sorted top-K by (d2, index); K rounds of a
+// group min over 64-bit keys merge the lanes' lists. IDXW: the grid stores each point's original
+// index in w (no second load per candidate). Same total order as the wave / thread versions;
+// every lane returns the same result.
+template <int K, int GS, bool IDXW>
 __device__ __forceinline__ int group_knn27(const float ox, const float oy, const float oz, const float inv_cell,
                                            const int gdx, const int gdy, const int gdz,
                                            const int* __restrict__ start, const float4* __restrict__ spts,
                                            const int* __restrict__ sidx, float qx, float qy, float qz, float r2, bool active,
-                                           int* out_pos, float* out_d2, int* out_idx, int* ncand) {
+                                           int* out_pos, float* out_d2, int* out_idx, int* ncand, int* tab, int npts) {
     const int gl = lane_id() & (GS - 1);
-    int rb[9], pre[10];
-    pre[0] = 0;
+    int total;
     {
         const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
         const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gdx - 1);
-        int re[9];
+        int rb[9], pre[10];
+        pre[0] = 0;
 #pragma unroll
         for (int r = 0; r < 9; r++) {
             const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
             const bool ok = active && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
             const int c = (z * gdy + y) * gdx;
             rb[r] = ok ? start[c + x0] : 0;
-            re[r] = ok ? start[c + x1 + 1] : 0;
+            pre[r + 1] = pre[r] + (ok ? start[c + x1 + 1] - rb[r] : 0);
         }
+        total = pre[9];
+        __builtin_amdgcn_wave_barrier();
+        if (gl == 0) {
 #pragma unroll
-        for (int r = 0; r < 9; r++) pre[r + 1] = pre[r] + (re[r] - rb[r]);
+            for (int r = 0; r < 9; r++) { tab[r] = rb[r] - pre[r]; tab[10 + r] = pre[r + 1]; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const int total = pre[9];
     if (ncand) *ncand = total;
     float bd[K];
     int bi[K], bp[K];
 #pragma unroll
     for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    int row = 0, base = tab[0], nxt = tab[10];
     for (int t0 = gl; t0 < total; t0 += 4 * GS) {
         float4 v[4];
         int id[4], ps[4];
@@ -343,21 +352,21 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
             const int t = t0 + u * GS;
             int p = -1;
             if (t < total) {
-                int base = rb[0] - pre[0];
-#pragma unroll
-                for (int r = 1; r < 9; r++) if (t >= pre[r]) base = rb[r] - pre[r];
+                while (t >= nxt && row < 8) { row++; base = tab[row]; nxt = tab[10 + row]; }
                 p = base + t;
+                if ((unsigned)p >= (unsigned)npts) p = -1;                   // defensive: inconsistent index
             }
             ps[u] = p;
             v[u] = p >= 0 ? spts[p] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
-            id[u] = p >= 0 ? sidx[p] : 0x7fffffff;
+            if (!IDXW) id[u] = p >= 0 ? sidx[p] : 0x7fffffff;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
-            if (!(ps[u] >= 0 && d2 < r2)) continue;
-            if (d2 < bd[K - 1] || (d2 == bd[K - 1] && id[u] < bi[K - 1])) {
-                float nd = d2; int ni = id[u], np = ps[u];
+            if (!(d2 < r2) || d2 > bd[K - 1]) continue;
+            const int iu = IDXW ? __float_as_int(v[u].w) : id[u];
+            if (d2 < bd[K - 1] || iu < bi[K - 1]) {
+                float nd = d2; int ni = iu, np = ps[u];
 #pragma unroll
                 for (int k = 0; k < K; k++) {
                     const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);

@@ -42,6 +42,7 @@ struct Grid {
     int* idx = nullptr;            // original index of each sorted point
     int* pcell = nullptr;          // cell of each input point
     int nlayers = 1;
+    bool w_index = false;          // sorted copy carries the original index in w (search-only grids)
     int cap = 0;
     float min_cell = 1.f;
 };
@@ -138,6 +139,8 @@ struct Ctx {
     int n_corner_last = 0, n_surf_last = 0;
     Grid g_corner_last, g_surf_last;
     Grid g_corner_win, g_surf_win;  // scan-line-layered grids of the last clouds (window search)
+    Grid g_knn;                     // aloam_knn_device (grown on demand)
+    int* d_knn_n = nullptr;
     aloam_factor* d_factors = nullptr;
     int cap_factors = 0;
     LMState* d_lm = nullptr;
@@ -188,7 +191,7 @@ struct Ctx {
     unsigned long long* d_cand = nullptr;                // [2] candidate counters (profiling)
 
     // profiling events: [0..1] scan, [2..3] odom, [4..5] map, search pairs after that
-    static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS;
+    static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS + 2;   // last two: aloam_knn_device
     hipEvent_t ev[NEV];
     KindScratch ks[2];
     bool ev_ready = false;
@@ -216,7 +219,9 @@ void scan_registration_launch(Ctx& C, const float4* in, int n);
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of, const unsigned char* cube_valid);
 struct GridBuild { Grid* g; const float4* pts; const int* d_n; int cap_n; const int* cube_of; const unsigned char* cube_valid; };
 void grid_build_multi(Ctx& C, const GridBuild* b, int n);   // up to 4 grids in one set of launches
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1);
+void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2,
+                       unsigned long long* cand);
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);
 void odom_compose(Ctx& C);

@@ -120,10 +120,11 @@ __device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, c
 }
 
 
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers) {
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_index) {
     g.cap = cap;
     g.min_cell = min_cell;
     g.nlayers = nlayers;
+    g.w_index = w_index;
     g.desc = (GridDesc*)dalloc(C, sizeof(GridDesc));
     g.cell_count = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
     g.cell_start = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
@@ -147,7 +148,7 @@ void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, c
 struct GridJob {
     GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx; int* pcell;
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
-    float min_cell; int nlayers;
+    float min_cell; int nlayers; int w_index;
 };
 struct GridJobs { GridJob j[4]; };
 
@@ -222,8 +223,11 @@ __global__ void k_gm_scatter(GridJobs J) {
     for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
         int c = g.pcell[i];
         if (c < 0) continue;
-        int pos = g.cell_start[c] + atomicSub(&g.cell_count[c], 1) - 1;
-        g.spts[pos] = g.pts[i];
+        const int left = atomicSub(&g.cell_count[c], 1);
+        int pos = g.cell_start[c] + left - 1;
+        if (left <= 0 || pos >= g.cell_start[c + 1]) continue;     // defensive: never write outside the cell
+        const float4 p = g.pts[i];
+        g.spts[pos] = g.w_index ? make_float4(p.x, p.y, p.z, __int_as_float(i)) : p;
         g.sidx[pos] = i;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {            // publish n, re-arm bbox/counter for the next build
@@ -243,7 +247,7 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     for (int k = 0; k < nj; k++) {
         const Grid& g = *b[k].g;
         J.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell,
-                         b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid, g.min_cell, g.nlayers};
+                         b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0};
         cap = std::max(cap, b[k].cap_n);
     }
     const int nb = std::max(1, std::min(1024, (cap + GB - 1) / GB));
@@ -275,6 +279,63 @@ __global__ void k_knn(const GridDesc* __restrict__ gdp, const int* __restrict__ 
             idx[wq * k + j] = j < f ? oi[j] : -1;
             d2[wq * k + j] = j < f ? od[j] : INFINITY;
         }
+}
+
+// Large searches (aloam_knn_device, C4): a GS-lane group per query (group_knn27 in
+// aloam_device.hpp) over the radius-edge grid; candidates counted per wave when profiling.
+template <int K, int GS>
+__global__ void __launch_bounds__(256) k_knn_group(const GridDesc* __restrict__ gdp, const int* __restrict__ start,
+                                                   const float4* __restrict__ spts, const int* __restrict__ sidx,
+                                                   const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
+                                                   float* __restrict__ d2, unsigned long long* cand) {
+    __shared__ int tabs[256 / GS][20];
+    // natural order (measured: an XCD-contiguous remap of the ring-ordered queries was 20% slower —
+    // all XCDs sweeping the same neighbourhood share it through the MALL)
+    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+    const bool live = qi < nq;
+    if (!__ballot(live)) return;
+    const GridDesc gd = *gdp;
+    const float4 qq = q[live ? qi : 0];
+    int pos[K], oi[K], nc = 0;
+    float od[K];
+    const int f = group_knn27<K, GS, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, spts, sidx,
+                                           qq.x, qq.y, qq.z, r2, live, pos, od, oi, &nc, tabs[threadIdx.x / GS], gd.n);
+    const int gl = lane_id() & (GS - 1);
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if (j < k && j % GS == gl) {
+                idx[(size_t)qi * k + j] = j < f ? oi[j] : -1;
+                d2[(size_t)qi * k + j] = j < f ? od[j] : INFINITY;
+            }
+    }
+    if (cand) {
+        const int t = wave_sum_i(live && gl == 0 ? nc : 0);
+        if (lane_id() == 0 && t) atomicAdd(cand, (unsigned long long)t);
+    }
+}
+
+template <int GS>
+static void knn_group_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float r2, int* idx, float* d2,
+                             unsigned long long* cand) {
+    const int blocks = (int)(((long long)nq * GS + 255) / 256);
+    if (k <= 5) k_knn_group<5, GS><<<blocks, 256, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2, cand);
+    else k_knn_group<8, GS><<<blocks, 256, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2, cand);
+}
+
+void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2,
+                       unsigned long long* cand) {
+    if (nq <= 0) return;
+    const float r2 = radius * radius;
+    static const int gs = getenv("ALOAM_KNN_GS") ? atoi(getenv("ALOAM_KNN_GS")) : 8;   // tuning knob
+    if (gs == 64) knn_group_launch<64>(C, g, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 32) knn_group_launch<32>(C, g, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 16) knn_group_launch<16>(C, g, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 4) knn_group_launch<4>(C, g, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 2) knn_group_launch<2>(C, g, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 1) knn_group_launch<1>(C, g, q, nq, k, r2, idx, d2, cand);
+    else knn_group_launch<8>(C, g, q, nq, k, r2, idx, d2, cand);
+    HIPCHK(hipGetLastError());
 }
 
 void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2) {

@@ -168,6 +168,7 @@ __global__ void __launch_bounds__(256) k_map_assoc(
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp) {
+    __shared__ int tabs[256 / AG][20];
     // slots are compact: corner stack at [0, nc), surf stack at [nc, nc + ns) — the reference's
     // AddResidualBlock order; the solver reads nc + ns from the device
     // every independent load is issued up front (one round trip before the grid walk)
@@ -192,8 +193,9 @@ __global__ void __launch_bounds__(256) k_map_assoc(
     float d2[5];
     int found = 5;
     if (exp & 1) { for (int k = 0; k < 5; k++) pos[k] = (li * 7 + k) % 64; }
-    else found = group_knn27<5, AG>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
-                                    corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand);
+    else found = group_knn27<5, AG, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
+                                          corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand,
+                                          tabs[threadIdx.x / AG], gd.n);
     if (live && lead) {
         aloam_factor f;
         f.type = -1; f.pad = 0;
