@@ -131,7 +131,7 @@ def main():
 
     W, K = max(args.warmup, 5), args.steps
     # independent replica per rank: a different stretch of the synthetic street
-    start = 1000 * rank
+    start = lvo.replicas.replica_start_frame(rank)
     frames = lvo.synth.sequence("hdl64", W + K, start=start)
     n_pts = [len(f) for f in frames]
     dev = torch.device("cuda", local_rank)
@@ -201,8 +201,7 @@ def main():
     else:
         pipe.set_profiling(False)
 
-    total_scans = K * world
-    value = total_scans / elapsed
+    value = lvo.replicas.aggregate_rate(K, world, elapsed)
     ms_per_step = elapsed / K * 1000.0
     rounds = 10 + 10
     stage /= K

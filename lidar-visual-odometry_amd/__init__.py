@@ -17,6 +17,7 @@ import os
 import numpy as np
 
 from . import _abi as abi  # noqa: F401
+from . import replicas  # noqa: F401
 from . import synth  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))

@@ -1,0 +1,50 @@
+"""Multi-GPU execution of the per-scan path.
+
+One process per GPU (torchrun; backend "nccl" = RCCL on the GPU box, "gloo" in CPU tests).
+* Across scans the path is a pose chain — scan k's odometry and mapping need scan k-1's — so N GPUs
+  run N independent replica sequences ("scaling": "weak"); torch.distributed carries only the start /
+  stop barriers and the max-over-ranks elapsed time, no data-path collective.
+* Within one search (C4: one sweep against a large local map) queries are independent given the map:
+  shard_range splits them into contiguous (scan-ordered, hence spatially coherent) chunks, map
+  replicated, again without a collective.
+"""
+import time
+
+
+def replica_start_frame(rank, stride=1000):
+    """First frame of rank's replica sequence: a different stretch of the synthetic street."""
+    return stride * int(rank)
+
+
+def shard_range(n, rank, world):
+    """Contiguous [lo, hi) share of n items for rank (sizes differ by at most one)."""
+    base, extra = divmod(int(n), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def timed_region(fn, dist=None, sync=None, device=None):
+    """Runs fn() between barrier + sync pairs and returns the max over ranks of the elapsed seconds
+    (the contract of bench.py: every rank's time counts, the slowest one defines the job)."""
+    if dist is not None:
+        dist.barrier()
+    if sync is not None:
+        sync()
+    t0 = time.perf_counter()
+    out = fn()
+    if sync is not None:
+        sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
+
+
+def aggregate_rate(units_per_rank, world, elapsed):
+    """Whole-job throughput: all ranks' units over the max-over-ranks time."""
+    return units_per_rank * world / elapsed if elapsed > 0 else 0.0

@@ -243,3 +243,34 @@ def test_pipeline_sequence_ate(gpu_ctx_factory):
         to.append(mo["t_w_curr"])
     ate = np.sqrt(np.mean(np.sum((np.array(tg) - np.array(to)) ** 2, axis=1)))
     assert ate <= 1e-4, ate
+
+
+@pytest.mark.gpu
+def test_knn_device_c4_scale(gpu_ctx_factory):
+    """C4: a 128-line sweep against a dense ~1.1M-point local map through
+    aloam_knn_device; 3000 sampled queries must equal the oracle's kd-tree 5-NN (indices exact,
+    distance bits exact) and every query's 5th distance must be < 1 when found."""
+    import torch
+    m = synth.dense_map(4, 0.0, 0.0, step=0.15)
+    R, o = synth.pose("l128", 0)
+    s = synth.scan("l128", 0)
+    q = s.copy()
+    q[:, :3] = (s[:, :3].astype(np.float64) @ R.T + o).astype(np.float32)
+    dm, dq = torch.from_numpy(m).cuda(), torch.from_numpy(q).cuda()
+    idx = torch.full((len(q), 5), -7, dtype=torch.int32, device="cuda")
+    d2 = torch.empty((len(q), 5), dtype=torch.float32, device="cuda")
+    ctx = gpu_ctx_factory(128)
+    ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), 5, 1.0, idx.data_ptr(), d2.data_ptr())
+    gi, gd = idx.cpu().numpy(), d2.cpu().numpy()
+    assert (gi >= -1).all()                                   # every slot written
+    sel = np.random.default_rng(1).choice(len(q), 3000, replace=False)
+    oi, od = ob.knn(m, q[sel], 5, 1.0)
+    assert np.array_equal(gi[sel], oi)
+    ok = oi >= 0
+    assert np.array_equal(gd[sel][ok].view(np.uint32), od[ok].view(np.uint32))
+    assert (gd[gi[:, 4] >= 0, 4] < 1.0).all()
+    # k < 5 through the same kernel: prefixes of the 5-NN lists
+    idx3 = torch.empty((len(q), 3), dtype=torch.int32, device="cuda")
+    d3 = torch.empty((len(q), 3), dtype=torch.float32, device="cuda")
+    ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), 3, 1.0, idx3.data_ptr(), d3.data_ptr())
+    assert np.array_equal(idx3.cpu().numpy(), gi[:, :3])
