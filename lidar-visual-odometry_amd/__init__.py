@@ -72,6 +72,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ALOAMError(f"HIP extension not built: {LIB_PATH} (run __graft_entry__.build())")
+        # One HIP runtime per process: the PyTorch wheel bundles its own libamdhip64.so.7, which
+        # libtorch_hip requests under a different name; if our library loaded /opt/rocm's copy first,
+        # torch would load a second runtime that then sees no device. Importing torch first makes
+        # our NEEDED libamdhip64.so.7 resolve to the copy already in the process.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = _declare(C.CDLL(LIB_PATH))
     return _lib
 

@@ -105,6 +105,9 @@ static void allocate(Ctx& C) {
     C.d_round_cnt = (int*)dalloc(C, sizeof(int) * 4 * ALOAM_MAX_ROUNDS);
     C.d_last_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_last_sorted = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_odom_nq = (int*)dalloc(C, sizeof(int) * 2);
+    lm_init(C);
+    C.use_graphs = getenv("ALOAM_NO_GRAPHS") == nullptr;
     C.d_cand = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2);
     // mapping
     const int M = std::max(P.max_map_points, 1024);
@@ -169,6 +172,28 @@ static void allocate(Ctx& C) {
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
     C.ev_ready = true;
     HIPCHK(hipStreamSynchronize(C.stream));   // all zero-fills and init kernels done
+}
+
+void run_graph(Ctx& C, int slot, const void* k0, const void* k1, int n, const std::function<void()>& issue) {
+    Ctx::GraphSlot& g = C.graphs[slot];
+    if (!g.exec || g.key[0] != k0 || g.key[1] != k1 || g.n != n) {
+        if (g.exec) { (void)hipGraphExecDestroy(g.exec); g.exec = nullptr; }
+        hipGraph_t graph = nullptr;
+        HIPCHK(hipStreamBeginCapture(C.stream, hipStreamCaptureModeThreadLocal));
+        try {
+            issue();
+        } catch (...) {
+            (void)hipStreamEndCapture(C.stream, &graph);
+            if (graph) (void)hipGraphDestroy(graph);
+            throw;
+        }
+        HIPCHK(hipStreamEndCapture(C.stream, &graph));
+        const hipError_t e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        HIPCHK(e);
+        g.key[0] = k0; g.key[1] = k1; g.n = n;
+    }
+    HIPCHK(hipGraphLaunch(g.exec, C.stream));
 }
 
 void fork_lane1(Ctx& C) {
@@ -254,11 +279,25 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         HIPCHK(hipMemsetAsync(C.d_round_cnt, 0, sizeof(int) * 2 * ALOAM_MAX_ROUNDS, st));
         const int nslots = C.n_sharp + C.n_flat;
         if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
-        for (int it = 0; it < rounds; it++) {
-            prof_mark(C, 6 + 2 * it);
-            odom_round_search(C, it);
-            prof_mark(C, 7 + 2 * it);
-            lm_run(C, C.d_factors, nslots, C.d_odom->para, it, nullptr);
+        set_counts2(C, C.d_odom_nq, C.n_sharp, C.n_flat);
+        // the rounds read every size from the device, so the same launches serve every scan
+        const int cap_slots = MAXL * (LINE_SHARP_CAP + LINE_FLAT_CAP);
+        const int hint = nslots;
+        auto issue = [&C, rounds, cap_slots](bool marks, int live_hint) {
+            for (int it = 0; it < rounds; it++) {
+                if (marks) prof_mark(C, 6 + 2 * it);
+                odom_round_search(C, it);
+                if (marks) prof_mark(C, 7 + 2 * it);
+                lm_run(C, C.d_factors, cap_slots, C.d_odom->para, it, nullptr, C.d_odom_nq, live_hint);
+            }
+        };
+        if (C.profiling || !C.use_graphs) {
+            issue(true, hint);
+        } else {   // two cached graphs: the last-cloud buffers alternate between scans
+            int slot = (C.graphs[0].key[0] == C.d_corner_last && C.graphs[0].key[1] == C.d_surf_last) ? 0
+                     : (C.graphs[1].key[0] == C.d_corner_last && C.graphs[1].key[1] == C.d_surf_last) ? 1
+                     : (C.graphs[0].exec ? 1 : 0);
+            run_graph(C, slot, C.d_corner_last, C.d_surf_last, rounds, [&] { issue(false, hint); });
         }
         odom_compose(C);
     }
@@ -440,6 +479,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->stream) (void)hipStreamSynchronize(C->stream);
     if (C->stream2) (void)hipStreamSynchronize(C->stream2);
     if (C->ev_ready) for (int i = 0; i < Ctx::NEV; i++) (void)hipEventDestroy(C->ev[i]);
+    for (auto& g : C->graphs) if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     for (auto& b : C->bufs) (void)hipFree(b.p);

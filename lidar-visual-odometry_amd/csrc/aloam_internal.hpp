@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -194,6 +195,10 @@ struct Ctx {
     static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS + 2;   // last two: aloam_knn_device
     hipEvent_t ev[NEV];
     KindScratch ks[2];
+    struct GraphSlot { const void* key[2] = {nullptr, nullptr}; int n = -1; hipGraphExec_t exec = nullptr; };
+    GraphSlot graphs[3];             // 0,1: odometry rounds (last-cloud buffer parity), 2: mapping rounds
+    bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling
+    int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
 };
 
@@ -227,6 +232,9 @@ void set_counts2(Ctx& C, int* dst, int a, int b);
 void odom_compose(Ctx& C);
 // nslots = host upper bound; d_nslots2 (optional, device int[2]) = live slots as a sum of two counts
 void odom_last_sorted(Ctx& C);
+// runs issue() through a cached HIP graph of C.stream keyed by (k0, k1, n) in slot
+void run_graph(Ctx& C, int slot, const void* k0, const void* k1, int n, const std::function<void()>& issue);
+void lm_init(Ctx& C);   // one-time kernel attributes (before any graph capture)
 void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2 = nullptr,
             int live_hint = 0);
 void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq);

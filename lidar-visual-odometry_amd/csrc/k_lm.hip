@@ -469,6 +469,12 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
     }
 }
 
+void lm_init(Ctx& C) {
+    (void)C;   // static rows (59 KB) + up to 80 KB of cached slots: above the default dynamic limit
+    HIPCHK(hipFuncSetAttribute((const void*)k_lm_coop, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(aloam_factor) * LM_CACHE)));
+}
+
 // one Ceres Solve over nslots factor slots; `gate` (device int, may be null) disables the solve.
 void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2,
             int live_hint) {
@@ -483,12 +489,6 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
     G = std::max(1, std::min(LM_COOP_MAX, G));
     const int cap = std::min(LM_CACHE, (nslots + G - 1) / G);          // LDS slots per workgroup
     const size_t lds = sizeof(aloam_factor) * (size_t)cap;
-    static bool attr = false;
-    if (!attr) {   // static rows (59 KB) + up to 80 KB of cached slots: above the default dynamic limit
-        HIPCHK(hipFuncSetAttribute((const void*)k_lm_coop, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)(sizeof(aloam_factor) * LM_CACHE)));
-        attr = true;
-    }
     k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_coop_part, C.d_bar, C.d_bar_err, out,
                                       C.P.max_solver_iterations, gate, d_nslots2, cap);
     HIPCHK(hipGetLastError());

@@ -163,54 +163,58 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
 // and writes the factor record. Correspondence counts and (profiling) candidate counts are
 // aggregated per wave before the atomics.
 constexpr int AG = 8;     // lanes per query (measured best of 4 / 8 / 16 at C3)
+constexpr int ASSOC_BLOCKS = 512;   // fixed launch (graph-replayable); waves stride over the stacks
 __global__ void __launch_bounds__(256) k_map_assoc(
-    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n, int ub_c, int ub_s,
+    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n,
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp) {
     __shared__ int tabs[256 / AG][20];
     // slots are compact: corner stack at [0, nc), surf stack at [nc, nc + ns) — the reference's
     // AddResidualBlock order; the solver reads nc + ns from the device
-    // every independent load is issued up front (one round trip before the grid walk)
-    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / AG;
-    const bool corner = qi < ub_c;
-    const int li = corner ? qi : qi - ub_c;
-    const int opt = m->optimize;
+    if (!m->optimize) return;
     const int nc = stack_n[0], ns = stack_n[1];
     double par[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
-    const float4 po = corner ? cstack[min(li, max(ub_c - 1, 0))] : sstack[min(li, max(ub_s - 1, 0))];
-    const GridDesc gd = corner ? *gdc : *gds;
-    if (!opt) return;
     const bool lead = (lane_id() & (AG - 1)) == 0;
-    const bool live = qi < ub_c + ub_s && li < (corner ? nc : ns);
-    if (!__ballot(live)) return;                    // whole wave past the (downsampled) stacks
-    int type = -1, ncand = 0;
-    const float4 sel = associate_to_map(par, po);
-    const float4* sp = corner ? sp_c : sp_s;
-    int pos[5], idx[5];
-    float d2[5];
-    int found = 5;
-    if (exp & 1) { for (int k = 0; k < 5; k++) pos[k] = (li * 7 + k) % 64; }
-    else found = group_knn27<5, AG, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
-                                          corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand,
-                                          tabs[threadIdx.x / AG], gd.n);
-    if (live && lead) {
-        aloam_factor f;
-        f.type = -1; f.pad = 0;
-        if (found == 5 && !(exp & 2)) fit_factor(corner, po, sp, pos, f);
-        out[corner ? li : nc + li] = f;
-        type = f.type;
+    const int per_wave = WAVE / AG;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
+    int cnt_c = 0, cnt_s = 0;
+    unsigned long long ncand_sum = 0;
+    for (int base = wave * per_wave; base < nc + ns; base += nwaves * per_wave) {   // wave-uniform trip count
+        const int qi = base + (lane_id() / AG);
+        const bool live = qi < nc + ns;
+        const bool corner = qi < nc;
+        const int li = corner ? qi : qi - nc;
+        const float4 po = live ? (corner ? cstack[li] : sstack[li]) : make_float4(0, 0, 0, 0);
+        const GridDesc gd = corner ? *gdc : *gds;
+        const float4 sel = associate_to_map(par, po);
+        const float4* sp = corner ? sp_c : sp_s;
+        int pos[5], idx[5], ncand = 0;
+        float d2[5];
+        int found = 5;
+        if (exp & 1) { for (int k = 0; k < 5; k++) pos[k] = (li * 7 + k) % 64; }
+        else found = group_knn27<5, AG, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
+                                              corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand,
+                                              tabs[threadIdx.x / AG], gd.n);
+        if (live && lead) {
+            aloam_factor f;
+            f.type = -1; f.pad = 0;
+            if (found == 5 && !(exp & 2)) fit_factor(corner, po, sp, pos, f);
+            out[qi] = f;
+            if (f.type >= 0) { if (corner) cnt_c++; else cnt_s++; }
+            ncand_sum += ncand;
+        }
     }
     // wave-aggregated counters
-    const unsigned long long vc = __ballot(type >= 0 && corner), vs = __ballot(type >= 0 && !corner);
+    const int tc = wave_sum_i(cnt_c), ts = wave_sum_i(cnt_s);
     if (lane_id() == 0) {
-        if (vc) atomicAdd(&round_cnt[0], __popcll(vc));
-        if (vs) atomicAdd(&round_cnt[1], __popcll(vs));
+        if (tc) atomicAdd(&round_cnt[0], tc);
+        if (ts) atomicAdd(&round_cnt[1], ts);
     }
     if (cand_count) {
-        const int t = wave_sum_i(lead ? ncand : 0);
+        const int t = wave_sum_i((int)ncand_sum);
         if (lane_id() == 0 && t) atomicAdd(cand_count, (unsigned long long)t);
     }
 }
@@ -542,17 +546,23 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
     if (nq > 0) {
         if (nq > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity exceeded"};
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
-        for (int it = 0; it < rounds; it++) {
-            prof_mark(C, 6 + 2 * (ALOAM_MAX_ROUNDS + it));
-            k_map_assoc<<<(nq * AG + 255) / 256, 256, 0, st>>>(
-                C.d_cstack, C.d_sstack, C.d_stack_n, ub_c, ub_s,
-                C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
-                C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
-                C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it, C.profiling ? C.d_cand : nullptr, g_exp);
-            prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
-            lm_run(C, C.d_factors, nq, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize, C.d_stack_n,
-                   C.map_slots_hint);
-        }
+        // every size comes from the device (stack counts, grids, gate): one fixed launch sequence
+        auto issue = [&C, st, rounds](bool marks, int live_hint) {
+            for (int it = 0; it < rounds; it++) {
+                if (marks) prof_mark(C, 6 + 2 * (ALOAM_MAX_ROUNDS + it));
+                k_map_assoc<<<ASSOC_BLOCKS, 256, 0, st>>>(
+                    C.d_cstack, C.d_sstack, C.d_stack_n,
+                    C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
+                    C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
+                    C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it, C.profiling ? C.d_cand : nullptr, g_exp);
+                if (marks) prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
+                lm_run(C, C.d_factors, C.cap_factors, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize,
+                       C.d_stack_n, live_hint);
+            }
+        };
+        const int hint = C.map_slots_hint > 0 ? C.map_slots_hint : 4096;
+        if (C.profiling || !C.use_graphs) issue(true, hint);
+        else run_graph(C, 2, nullptr, nullptr, rounds, [&] { issue(false, hint); });
     }
     k_map_update<<<1, 1, 0, st>>>(C.d_map);
     fork_lane1(C);

@@ -249,22 +249,16 @@ __global__ void k_line_sorted(const float4* __restrict__ a, const int* na, const
         if (line_of(cl[j + 1].w) < line_of(cl[j].w)) flag[blockIdx.y] = 0;
 }
 
-__global__ void __launch_bounds__(256) k_odom_search(
-    const float4* __restrict__ sharp, int n_sharp, const float4* __restrict__ flat, int n_flat,
+__device__ __forceinline__ void odom_query(int qi, int n_sharp,
+    const float4* __restrict__ sharp, const float4* __restrict__ flat,
     const float4* __restrict__ corner_last, int n_cl, const float4* __restrict__ surf_last, int n_sl,
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
     const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
-    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s) {
-    __shared__ RowSet<9> rows9[256 / WAVE];
-    __shared__ RowSet<25> rows25[256 / WAVE];
-    __shared__ RowSet<128> rows128[256 / WAVE];
-    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s,
+    RowSet<9>& r9, RowSet<25>& r25, RowSet<128>& r128) {
     const int lane = lane_id();
-    if (qi >= n_sharp + n_flat) return;
-    RowSet<9>& r9 = rows9[threadIdx.x / WAVE];
-    RowSet<25>& r25 = rows25[threadIdx.x / WAVE];
     const bool is_corner = qi < n_sharp;
     const float4 pi = is_corner ? sharp[qi] : flat[qi - n_sharp];
     // TransformToStart (:154-172)
@@ -289,7 +283,7 @@ __global__ void __launch_bounds__(256) k_odom_search(
         int i2, i3;
         const bool by_grid = line_sorted[is_corner ? 0 : 1] != 0;
         if (is_corner) {
-            if (by_grid) grid_window<0>(*wdc, ws_c, wp_c, wi_c, closest, cid, sx, sy, sz, &i2, &i3, rows128[threadIdx.x / WAVE]);
+            if (by_grid) grid_window<0>(*wdc, ws_c, wp_c, wi_c, closest, cid, sx, sy, sz, &i2, &i3, r128);
             else window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
             if (i2 >= 0) {
                 const float4 a = cl[closest], b = cl[i2];
@@ -298,7 +292,7 @@ __global__ void __launch_bounds__(256) k_odom_search(
                 f.b[0] = b.x; f.b[1] = b.y; f.b[2] = b.z;
             }
         } else {
-            if (by_grid) grid_window<1>(*wds, ws_s, wp_s, wi_s, closest, cid, sx, sy, sz, &i2, &i3, rows128[threadIdx.x / WAVE]);
+            if (by_grid) grid_window<1>(*wds, ws_s, wp_s, wi_s, closest, cid, sx, sy, sz, &i2, &i3, r128);
             else window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
             if (i2 >= 0 && i3 >= 0) {
                 const float4 pj = cl[closest], pl = cl[i2], pm = cl[i3];
@@ -319,6 +313,28 @@ __global__ void __launch_bounds__(256) k_odom_search(
     }
 }
 
+// One wave per feature point, grid-stride over the points: the counts come from the device
+// (n_q[0] sharp, n_q[1] flat; n_last[0..1] last-cloud sizes), so the launch configuration is
+// fixed and the round loop can be replayed as a graph.
+__global__ void __launch_bounds__(256) k_odom_search(
+    const float4* __restrict__ sharp, const float4* __restrict__ flat, const int* __restrict__ n_q,
+    const float4* __restrict__ corner_last, const float4* __restrict__ surf_last, const int* __restrict__ n_last,
+    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
+    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
+    const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
+    const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
+    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s) {
+    __shared__ RowSet<9> rows9[256 / WAVE];
+    __shared__ RowSet<25> rows25[256 / WAVE];
+    __shared__ RowSet<128> rows128[256 / WAVE];
+    const int n_sharp = n_q[0], nq = n_q[0] + n_q[1];
+    const int n_cl = n_last[0], n_sl = n_last[1];
+    const int w = threadIdx.x / WAVE;
+    for (int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; qi < nq; qi += gridDim.x * (blockDim.x / WAVE))
+        odom_query(qi, n_sharp, sharp, flat, corner_last, n_cl, surf_last, n_sl, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s,
+                   odom, out, round_cnt, line_sorted, wdc, ws_c, wp_c, wi_c, wds, ws_s, wp_s, wi_s, rows9[w], rows25[w], rows128[w]);
+}
+
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582)
 __global__ void k_odom_compose(OdomState* o) {
     dquat qw{o->q_w[0], o->q_w[1], o->q_w[2], o->q_w[3]};
@@ -329,13 +345,13 @@ __global__ void k_odom_compose(OdomState* o) {
     o->q_w[0] = n.x; o->q_w[1] = n.y; o->q_w[2] = n.z; o->q_w[3] = n.w;
 }
 
+// fixed launch: one wave per possible feature point (caps 12 sharp + 24 flat per line); waves past
+// the device-side count exit at once
 void odom_round_search(Ctx& C, int round) {
-    const int nq = C.n_sharp + C.n_flat;
-    if (nq == 0) return;
     const int threads = 256;
-    const int nb = (nq * WAVE + threads - 1) / threads;
+    const int nb = (MAXL * (LINE_SHARP_CAP + LINE_FLAT_CAP) * WAVE + threads - 1) / threads;
     k_odom_search<<<nb, threads, 0, C.stream>>>(
-        C.d_sharp, C.n_sharp, C.d_flat, C.n_flat, C.d_corner_last, C.n_corner_last, C.d_surf_last, C.n_surf_last,
+        C.d_sharp, C.d_flat, C.d_odom_nq, C.d_corner_last, C.d_surf_last, C.d_last_n,
         C.g_corner_last.desc, C.g_corner_last.cell_start, C.g_corner_last.pts, C.g_corner_last.idx,
         C.g_surf_last.desc, C.g_surf_last.cell_start, C.g_surf_last.pts, C.g_surf_last.idx,
         C.d_odom, C.d_factors, C.d_round_cnt + 2 * round, C.d_last_sorted,

@@ -18,9 +18,10 @@ def lvo():
     return mod
 
 
-@pytest.fixture(scope="session")
+@pytest.fixture
 def gpu_ctx_factory(lvo):
-    """Creates HIP contexts; fails (never skips silently) when the HIP library or GPU is missing."""
+    """Creates HIP contexts for one test (destroyed at its end); fails (never skips silently) when
+    the HIP library or GPU is missing."""
     ctxs = []
 
     def make(scan_line=64, **over):
