@@ -81,7 +81,10 @@ static void allocate(Ctx& C) {
     C.d_lsharp_idx = (int*)dalloc(C, sizeof(int) * capLS);
     C.d_flat_idx = (int*)dalloc(C, sizeof(int) * capF);
     // odometry
-    C.d_odom = (OdomState*)dalloc(C, sizeof(OdomState));
+    C.d_out = (DevOut*)dalloc(C, sizeof(DevOut));
+    HIPCHK(hipHostMalloc((void**)&C.h_out, sizeof(DevOut), hipHostMallocDefault));
+    std::memset(C.h_out, 0, sizeof(DevOut));
+    C.d_odom = &C.d_out->odom;
     std::memset(&C.h_odom, 0, sizeof(C.h_odom));
     C.h_odom.para[3] = 1.0;
     C.h_odom.q_w[3] = 1.0;
@@ -101,18 +104,18 @@ static void allocate(Ctx& C) {
     HIPCHK(hipHostMalloc((void**)&C.h_bar_err, sizeof(int) * 4, hipHostMallocMapped));   // read at every sync, no copy
     std::memset(C.h_bar_err, 0, sizeof(int) * 4);
     HIPCHK(hipHostGetDevicePointer((void**)&C.d_bar_err, C.h_bar_err, 0));
-    C.d_lm_sum = (aloam_lm_summary*)dalloc(C, sizeof(aloam_lm_summary) * 2 * ALOAM_MAX_ROUNDS);
-    C.d_round_cnt = (int*)dalloc(C, sizeof(int) * 4 * ALOAM_MAX_ROUNDS);
+    C.d_lm_sum = C.d_out->lm_sum;
+    C.d_round_cnt = C.d_out->round_cnt;
     C.d_last_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_last_sorted = (int*)dalloc(C, sizeof(int) * 2);
     C.d_odom_nq = (int*)dalloc(C, sizeof(int) * 2);
     lm_init(C);
     C.use_graphs = getenv("ALOAM_NO_GRAPHS") == nullptr;
-    C.d_cand = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2);
+    C.d_cand = C.d_out->cand;
     // mapping
     const int M = std::max(P.max_map_points, 1024);
     C.cap_map = M;
-    C.d_map = (MapState*)dalloc(C, sizeof(MapState));
+    C.d_map = &C.d_out->map;
     init_map_state(C.h_map);
     HIPCHK(hipMemcpyAsync(C.d_map, &C.h_map, sizeof(MapState), hipMemcpyHostToDevice, C.stream));
     C.d_mc = (float4*)dalloc(C, sizeof(float4) * M);
@@ -125,7 +128,7 @@ static void allocate(Ctx& C) {
     C.d_ms2_cube = (int*)dalloc(C, sizeof(int) * M);
     C.d_map_tmp = (float4*)dalloc(C, sizeof(float4) * M);
     C.d_seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (4 * (size_t)M + 32768));
-    C.d_map_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_map_n = C.d_out->map_n;
     C.d_cube_cnt = (int*)dalloc(C, sizeof(int) * 2 * 7 * (CUBE_N + 1));
     C.d_cube_valid = (unsigned char*)dalloc(C, CUBE_N);
     grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f, 1, true);     // 5-NN within 1 m, 3x3x3 cells
@@ -136,7 +139,7 @@ static void allocate(Ctx& C) {
     C.d_map_in_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_cstack = (float4*)dalloc(C, sizeof(float4) * capLS);
     C.d_sstack = (float4*)dalloc(C, sizeof(float4) * N);
-    C.d_stack_n = (int*)dalloc(C, sizeof(int) * 2);
+    C.d_stack_n = C.d_out->stack_n;
     C.d_registered = (float4*)dalloc(C, sizeof(float4) * N);
     // voxel / sort scratch
     C.cap_voxel = std::max(N, capLS) + 64;
@@ -325,11 +328,12 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     }
     prof_mark(C, 3);
     // results
-    int cnt[2 * ALOAM_MAX_ROUNDS];
-    HIPCHK(hipMemcpyAsync(&C.h_odom, C.d_odom, sizeof(OdomState), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(cnt, C.d_round_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(r.lm, C.d_lm_sum, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS, hipMemcpyDeviceToHost, st));
+    // odom state, round counts and LM summaries: one copy into the pinned mirror
+    HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, offsetof(DevOut, map_n), hipMemcpyDeviceToHost, st));
     sync(C);
+    C.h_odom = C.h_out->odom;
+    const int* cnt = C.h_out->round_cnt;
+    std::memcpy(r.lm, C.h_out->lm_sum, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
     if (!r.optimized) std::memset(r.lm, 0, sizeof(r.lm));
     for (int i = 0; i < r.rounds; i++) { r.corner_correspondence[i] = cnt[2 * i]; r.plane_correspondence[i] = cnt[2 * i + 1]; }
     for (int k = 0; k < 4; k++) { r.q_w_curr[k] = C.h_odom.q_w[k]; r.q_last_curr[k] = C.h_odom.para[k]; }
@@ -359,17 +363,15 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
     prof_mark(C, 4);
     map_frame_launch(C, &r);
     prof_mark(C, 5);
-    int cnt[2 * ALOAM_MAX_ROUNDS];
-    int mapn[2];
-    unsigned long long cand[2] = {0, 0};
-    int stackn[2];
-    HIPCHK(hipMemcpyAsync(&C.h_map, C.d_map, sizeof(MapState), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(cnt, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, sizeof(cnt), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(r.lm, C.d_lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(mapn, C.d_map_n, sizeof(mapn), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(stackn, C.d_stack_n, sizeof(stackn), hipMemcpyDeviceToHost, st));
-    if (C.profiling) HIPCHK(hipMemcpyAsync(cand, C.d_cand, sizeof(cand), hipMemcpyDeviceToHost, st));
+    // map state, counts, summaries, sizes: one copy of the results block into the pinned mirror
+    HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, sizeof(DevOut), hipMemcpyDeviceToHost, st));
     sync(C);
+    C.h_map = C.h_out->map;
+    const int* cnt = C.h_out->round_cnt + 2 * ALOAM_MAX_ROUNDS;
+    std::memcpy(r.lm, C.h_out->lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
+    const int* mapn = C.h_out->map_n;
+    const int* stackn = C.h_out->stack_n;
+    const unsigned long long* cand = C.h_out->cand;
     C.n_mc = mapn[0];
     C.n_ms = mapn[1];
     C.n_registered = C.n_map_full_in;
@@ -463,6 +465,7 @@ aloam_ctx* aloam_create(const aloam_params* p, int device) {
         g_create_err = e.msg;
         for (auto& b : C->bufs) (void)hipFree(b.p);
         if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
+        if (C->h_out) (void)hipHostFree(C->h_out);
         if (C->stream2) (void)hipStreamDestroy(C->stream2);
         if (C->stream) (void)hipStreamDestroy(C->stream);
         delete C;
@@ -484,6 +487,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     for (auto& b : C->bufs) (void)hipFree(b.p);
     if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
+    if (C->h_out) (void)hipHostFree(C->h_out);
     if (C->stream2) (void)hipStreamDestroy(C->stream2);
     if (C->stream) (void)hipStreamDestroy(C->stream);
     delete C;

@@ -82,6 +82,17 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// Per-frame results in ONE device block, so each stage returns them with a single D2H copy into a
+// pinned mirror (odometry: [odom .. lm_sum], mapping: the whole block).
+struct DevOut {
+    OdomState odom;
+    int round_cnt[4 * ALOAM_MAX_ROUNDS];
+    aloam_lm_summary lm_sum[2 * ALOAM_MAX_ROUNDS];
+    int map_n[2];
+    int stack_n[2];
+    unsigned long long cand[2];
+    MapState map;
+};
 struct KindScratch {               // per-lane scratch for the map kinds' concurrent work
     unsigned long long *vkeys = nullptr, *vkeys2 = nullptr;   // 2 x cap_voxel, cap_voxel
     int *vvals = nullptr, *vvals2 = nullptr;                  // cap_voxel, cap_voxel + 64 (+ VoxHdr)
@@ -195,6 +206,8 @@ struct Ctx {
     static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS + 2;   // last two: aloam_knn_device
     hipEvent_t ev[NEV];
     KindScratch ks[2];
+    DevOut* d_out = nullptr;         // device results block (d_odom, d_round_cnt, ... point into it)
+    DevOut* h_out = nullptr;         // pinned host mirror
     struct GraphSlot { const void* key[2] = {nullptr, nullptr}; int n = -1; hipGraphExec_t exec = nullptr; };
     GraphSlot graphs[3];             // 0,1: odometry rounds (last-cloud buffer parity), 2: mapping rounds
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling

@@ -65,6 +65,10 @@ int main(int argc, char** argv) {
     for (int p = 0; p < 5; p++)
         printf("pass %d: eval %.2f blockreduce %.2f us, barrier %.2f us, reduce %.2f us, tail %.2f us\n", p,
                p ? (ts[p][4] - ts[p - 1][3]) / 100.0 : 0.0, (ts[p][0] - ts[p][4]) / 100.0, (ts[p][1] - ts[p][0]) / 100.0, (ts[p][2] - ts[p][1]) / 100.0, (ts[p][3] - ts[p][2]) / 100.0);
+    unsigned long long tt[8];
+    hipMemcpyFromSymbol(tt, HIP_SYMBOL(aloam::g_tail_ts), sizeof(tt));
+    printf("next_step: build M %.2f us, chol %.2f, model cost %.2f, plus7 %.2f, norm %.2f\n", (tt[1]-tt[0])/100.0,
+           (tt[2]-tt[1])/100.0, (tt[3]-tt[2])/100.0, (tt[4]-tt[3])/100.0, (tt[5]-tt[4])/100.0);
     aloam_lm_summary s; hipMemcpy(&s, C.d_lm_sum, sizeof(s), hipMemcpyDeviceToHost);
     printf("iters %d succ %d term %d cost %g -> %g\n", s.iterations, s.successful_steps, s.termination, s.initial_cost, s.final_cost);
     return 0;
