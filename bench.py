@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=24, help="frames of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", choices=("pipeline", "serial"), default="pipeline")
+    ap.add_argument("--stages", type=int, choices=(2, 3), default=3, help="pipeline contexts (3 = one per node)")
     ap.add_argument("--profile-json", default="", help="also dump per-frame stage timings here")
     ap.add_argument("--c4-launches", type=int, default=20, help="timed launches of the C4 search (0 = skip)")
     ap.add_argument("--prof-frames", type=int, default=8,
@@ -147,16 +148,22 @@ def main():
     launches = 0
     stage = np.zeros(3)
 
-    def account(tm_front, tm_back):
-        nonlocal search_ms, search_bytes, launches, stage
+    stage_n = np.zeros(3)
+
+    def account(tm_scan=None, tm_odom=None, tm_back=None):
+        nonlocal search_ms, search_bytes, launches
         if tm_back is not None:
             search_ms += tm_back["map_search_ms"]
             search_bytes += tm_back["map_search_bytes"]
             launches += tm_back["map_search_launches"]
             stage[2] += tm_back["mapping_ms"]
-        if tm_front is not None:
-            stage[0] += tm_front["scan_registration_ms"]
-            stage[1] += tm_front["odometry_ms"]
+            stage_n[2] += 1
+        if tm_scan is not None:
+            stage[0] += tm_scan["scan_registration_ms"]
+            stage_n[0] += 1
+        if tm_odom is not None:
+            stage[1] += tm_odom["odometry_ms"]
+            stage_n[1] += 1
 
     if args.mode == "serial":
         ctx = lvo.Context(params, device=local_rank)
@@ -164,12 +171,12 @@ def main():
             od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
             traj.append(mp["t_w_curr"])
     else:
-        pipe = lvo.Pipeline(params, device=local_rank)
+        pipe = lvo.Pipeline(params, device=local_rank, stages=args.stages)
         for k in range(W):
             od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
             if mp is not None:
                 traj.append(mp["t_w_curr"])
-        traj.append(pipe.flush()["t_w_curr"])
+        traj += [mp["t_w_curr"] for _, mp in pipe.flush() if mp is not None]
 
     if dist:
         dist.barrier()
@@ -185,7 +192,7 @@ def main():
             od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
             if mp is not None:
                 traj.append(mp["t_w_curr"])
-        traj.append(pipe.flush()["t_w_curr"])
+        traj += [mp["t_w_curr"] for _, mp in pipe.flush() if mp is not None]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -201,26 +208,27 @@ def main():
         for k in range(W + K, W + K + P):
             od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
             tm = ctx.timing()
-            account(tm, tm)
+            account(tm, tm, tm)
             traj.append(mp["t_w_curr"])
         ctx.set_profiling(False)
     else:
         pipe.set_profiling(True)
         for k in range(W + K, W + K + P):
             od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
-            tf = pipe.front.timing()
-            account(tf, pipe.last_back_timing if mp is not None else None)
+            account(tm_scan=pipe.last_front_timing, tm_odom=pipe.last_odom_timing if od is not None else None,
+                    tm_back=pipe.last_back_timing if mp is not None else None)
             if mp is not None:
                 traj.append(mp["t_w_curr"])
-        mp = pipe.flush()
-        account(None, pipe.last_back_timing)
-        traj.append(mp["t_w_curr"])
+        for od, mp in pipe.flush():
+            account(tm_back=pipe.last_back_timing if mp is not None else None)
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
         pipe.set_profiling(False)
 
     value = lvo.replicas.aggregate_rate(K, world, elapsed)
     ms_per_step = elapsed / K * 1000.0
     rounds = 10 + 10
-    stage /= P
+    stage = stage / np.maximum(stage_n, 1)
     avg_launch_ms = search_ms / max(launches, 1)
     bytes_per_launch = search_bytes / max(launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -246,7 +254,9 @@ def main():
             "stage_ms": {"scan_registration": round(stage[0], 4), "odometry": round(stage[1], 4),
                          "mapping": round(stage[2], 4)},
             "parallelism": f"replicas x{world}",
-            "mode": args.mode + (" (front end scan k+1 || mapping scan k, 2 HIP streams)" if args.mode == "pipeline" else ""),
+            "mode": args.mode + ((" (scanRegistration k+2 || laserOdometry k+1 || laserMapping k, one context/stream each)"
+                                  if args.stages == 3 else " (front end k+1 || mapping k, 2 contexts)")
+                                 if args.mode == "pipeline" else ""),
         },
         "roofline": {
             "kernel": "k_map_assoc (mapping 5-NN search + line/plane fit, 8 lanes per query)",

@@ -192,6 +192,12 @@ int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags,
  * Lets the two stages of consecutive scans run concurrently on two streams, as the reference's
  * separate ROS nodes do. */
 int aloam_forward_mapping_input(aloam_ctx* src, aloam_ctx* dst);
+/* The scanRegistration -> laserOdometry topics (/velodyne_cloud_2, /laser_cloud_sharp,
+ * /laser_cloud_less_sharp, /laser_cloud_flat, /laser_cloud_less_flat: scanRegistration.cpp:413-449
+ * -> laserOdometry.cpp:280-292) between two contexts, device to device: `src` ran
+ * aloam_scan_registration, `dst` then runs aloam_odometry. With it the three stages of three
+ * consecutive scans run concurrently, like the reference's three nodes. */
+int aloam_forward_features(aloam_ctx* src, aloam_ctx* dst);
 
 /* ---- lower-level entry points (tests, tools) -------------------------------------- */
 /* Residuals (3 per factor; plane types fill 1) and the tangent-space Jacobian

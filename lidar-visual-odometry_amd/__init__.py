@@ -58,7 +58,8 @@ def _declare(L):
     L.aloam_get_timing.argtypes = [vp, C.POINTER(abi.Timing)]
     L.aloam_forward_mapping_input.argtypes = [vp, vp]
     L.aloam_knn_device.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_float, vp, vp]
-    for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
+    L.aloam_forward_features.argtypes = [vp, vp]
+    for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
                  "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
                  "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
                  "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing"):
@@ -90,7 +91,7 @@ EXPORTED_SYMBOLS = [
     "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
     "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
     "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing",
-    "aloam_forward_mapping_input", "aloam_knn_device",
+    "aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features",
 ]
 
 
@@ -215,6 +216,10 @@ class Context:
             self._check(lib().aloam_process_scan(self.h, pts.ctypes.data_as(C.c_void_p), len(pts), fl, C.byref(o), C.byref(m)))
         return abi.odom_to_dict(o), abi.map_to_dict(m)
 
+    def forward_features(self, dst):
+        """Hand this context's scanRegistration output to `dst`'s laserOdometry (device to device)."""
+        self._check(lib().aloam_forward_features(self.h, dst.h))
+
     def forward_mapping_input(self, dst):
         """Hand this context's published odometry output to `dst`'s laserMapping (device to device)."""
         self._check(lib().aloam_forward_mapping_input(self.h, dst.h))
@@ -265,50 +270,103 @@ class Context:
 
 
 class Pipeline:
-    """The reference's node split on one GPU: scanRegistration + laserOdometry on a front-end context
-    and laserMapping on a back-end context (each with its own HIP stream), so scan k's mapping runs
-    while scan k+1 goes through the front end — what the three ROS processes do concurrently
-    (src/scanRegistration.cpp, src/laserOdometry.cpp, src/laserMapping.cpp:934 `process` thread).
-    Results are the same as Context.process_scan's, one mapping result behind."""
+    """The reference's node split on one GPU. stages=3 (default): scanRegistration, laserOdometry and
+    laserMapping each own a context (own HIP stream), and scan k+2's feature extraction, scan k+1's
+    odometry and scan k's mapping run concurrently — the three ROS processes of the reference
+    (src/scanRegistration.cpp, src/laserOdometry.cpp, src/laserMapping.cpp:934 `process` thread),
+    handing over device to device (aloam_forward_features / aloam_forward_mapping_input).
+    stages=2: scanRegistration + laserOdometry share the front context.
+    Every scan still goes through all three stages, in order; results equal Context.process_scan's."""
 
-    def __init__(self, params=None, device=0):
+    def __init__(self, params=None, device=0, stages=3):
         from concurrent.futures import ThreadPoolExecutor
-        self.front = Context(params, device)
-        self.back = Context(params, device)
-        self._pool = ThreadPoolExecutor(max_workers=1)   # ctypes calls release the GIL
-        self._pending = None
+        self.stages = stages
+        self.front = Context(params, device)                       # scanRegistration (+ odometry if 2 stages)
+        self.odom = Context(params, device) if stages == 3 else self.front
+        self.back = Context(params, device)                        # laserMapping
+        self._pool = ThreadPoolExecutor(max_workers=2)             # ctypes calls release the GIL
+        self._pending_map = None
+        self._pending_odom = None
         self._profiling = False
         self.last_back_timing = None
+        self.last_odom_timing = None
+        self.last_front_timing = None
+
+    def _contexts(self):
+        return list({id(x): x for x in (self.front, self.odom, self.back)}.values())
 
     def set_profiling(self, on):
-        self.front.set_profiling(on)
-        self.back.set_profiling(on)
+        for c in self._contexts():
+            c.set_profiling(on)
         self._profiling = bool(on)
 
     def _map_job(self):
         mp = self.back.mapping()
         return mp, (self.back.timing() if self._profiling else None)
 
+    def _odom_job(self):
+        od = self.odom.odometry()
+        return od, (self.odom.timing() if self._profiling else None)
+
     def push(self, pts=None, device_ptr=None, n=None):
-        """Front end of the new scan, overlapped with the previous scan's mapping.
-        Returns (odometry result of this scan, mapping result of the previous published scan or None)."""
-        od, _ = self.front.process_scan(pts, device_ptr, n, mapping=False)
-        mp = self.flush()
-        if od["publish_to_mapping"]:
-            self.front.forward_mapping_input(self.back)
-            self._pending = self._pool.submit(self._map_job)
+        """Feed one scan. Returns (odometry result, mapping result) of the scans that completed those
+        stages during this step (None while the pipeline fills)."""
+        if self.stages == 2:
+            od, _ = self.front.process_scan(pts, device_ptr, n, mapping=False)
+            self.last_front_timing = self.front.timing() if self._profiling else None
+            self.last_odom_timing = self.last_front_timing
+            mp = self._join_map()
+            if od["publish_to_mapping"]:
+                self.front.forward_mapping_input(self.back)
+                self._pending_map = self._pool.submit(self._map_job)
+            return od, mp
+        # three stages: scanRegistration here, odometry and mapping of earlier scans in the workers
+        if device_ptr is not None:
+            self.front.scan_registration(int(n), device_ptr=device_ptr)
+        else:
+            self.front.scan_registration(pts)
+        self.last_front_timing = self.front.timing() if self._profiling else None
+        od = self._join_odom()
+        mp = self._join_map()
+        if od is not None and od["publish_to_mapping"]:
+            self.odom.forward_mapping_input(self.back)
+            self._pending_map = self._pool.submit(self._map_job)
+        self.front.forward_features(self.odom)
+        self._pending_odom = self._pool.submit(self._odom_job)
         return od, mp
 
-    def flush(self):
-        """Mapping result of the last pushed scan (or None)."""
-        if self._pending is None:
+    def _join_odom(self):
+        if self._pending_odom is None:
             return None
-        mp, self.last_back_timing = self._pending.result()
-        self._pending = None
+        od, self.last_odom_timing = self._pending_odom.result()
+        self._pending_odom = None
+        return od
+
+    def _join_map(self):
+        if self._pending_map is None:
+            return None
+        mp, self.last_back_timing = self._pending_map.result()
+        self._pending_map = None
         return mp
+
+    def flush(self):
+        """Drain the pipeline: the (odometry, mapping) results that complete while draining."""
+        out = []
+        od = self._join_odom() if self.stages == 3 else None
+        mp = self._join_map()
+        if mp is not None:
+            out.append((None, mp))
+        if od is not None:
+            if od["publish_to_mapping"]:
+                self.odom.forward_mapping_input(self.back)
+                out.append((od, self.back.mapping()))
+                self.last_back_timing = self.back.timing() if self._profiling else None
+            else:
+                out.append((od, None))
+        return out
 
     def close(self):
         self.flush()
         self._pool.shutdown()
-        self.front.close()
-        self.back.close()
+        for c in self._contexts():
+            c.close()

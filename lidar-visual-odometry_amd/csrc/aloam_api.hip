@@ -555,6 +555,33 @@ int aloam_set_features(aloam_ctx* ctx, const float* sharp, int ns, const float* 
     API_END
 }
 
+int aloam_forward_features(aloam_ctx* src, aloam_ctx* dst) {
+    if (!src || src == dst) return ALOAM_E_ARG;
+    Ctx& S = *(Ctx*)src;
+    API_BEGIN(dst)
+    if (S.device != C.device) throw ApiError{ALOAM_E_ARG, "contexts on different devices"};
+    if (!S.have_features || S.features_swapped || S.features_from_host)
+        throw ApiError{ALOAM_E_STATE, "source has no fresh scanRegistration output"};
+    if (S.n_full > C.cap_in || S.n_lflat > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "feature cloud too large"};
+    hipStream_t st = C.stream;   // the source's stream is idle: its API calls return synchronised
+    auto cp = [&](float4* d, const float4* s_, int n) {
+        if (n > 0) HIPCHK(hipMemcpyAsync(d, s_, sizeof(float4) * n, hipMemcpyDeviceToDevice, st));
+    };
+    cp(C.d_cloud, S.d_cloud, S.n_full);
+    cp(C.d_sharp, S.d_sharp, S.n_sharp);
+    cp(C.d_lsharp, S.d_lsharp, S.n_lsharp);
+    cp(C.d_flat, S.d_flat, S.n_flat);
+    cp(C.d_lflat, S.d_lflat, S.n_lflat);
+    C.n_full = S.n_full; C.n_sharp = S.n_sharp; C.n_lsharp = S.n_lsharp; C.n_flat = S.n_flat; C.n_lflat = S.n_lflat;
+    C.h_meta = S.h_meta;
+    C.have_features = true;
+    C.features_from_host = false;
+    C.features_swapped = false;
+    sync(C);
+    S.have_features = false;
+    API_END
+}
+
 int aloam_set_odom_state(aloam_ctx* ctx, const double q[4], const double t[3], const double qw[4], const double tw[3],
                          const float* corner_last, int nc, const float* surf_last, int ns) {
     API_BEGIN(ctx)

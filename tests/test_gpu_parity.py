@@ -274,3 +274,36 @@ def test_knn_device_c4_scale(gpu_ctx_factory):
     d3 = torch.empty((len(q), 3), dtype=torch.float32, device="cuda")
     ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), 3, 1.0, idx3.data_ptr(), d3.data_ptr())
     assert np.array_equal(idx3.cpu().numpy(), gi[:, :3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stages", [2, 3])
+def test_pipeline_matches_single_context(lvo, stages):
+    """The node-split pipelines (aloam_forward_features / aloam_forward_mapping_input between
+    contexts) produce the single-context trajectory: same correspondences, poses to 1e-9."""
+    p = abi.default_params(16)
+    frames = [synth.scan("vlp16", k) for k in range(7)]
+    ref = lvo.Context(p)
+    ro = [ref.process_scan(f) for f in frames]
+    ref.close()
+    pipe = lvo.Pipeline(p, stages=stages)
+    ods, mps = [], []
+    for f in frames:
+        od, mp = pipe.push(f)
+        if od is not None:
+            ods.append(od)
+        if mp is not None:
+            mps.append(mp)
+    for od, mp in pipe.flush():
+        if od is not None:
+            ods.append(od)
+        if mp is not None:
+            mps.append(mp)
+    pipe.close()
+    assert len(ods) == len(frames) and len(mps) == len(frames)
+    for (o_ref, m_ref), o, m in zip(ro, ods, mps):
+        assert o["corner_correspondence"] == o_ref["corner_correspondence"]
+        assert o["plane_correspondence"] == o_ref["plane_correspondence"]
+        np.testing.assert_allclose(o["t_w_curr"], o_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(m["t_w_curr"], m_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(m["q_w_curr"], m_ref["q_w_curr"], rtol=1e-9, atol=1e-12)
