@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=24, help="frames of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", choices=("pipeline", "serial"), default="pipeline")
-    ap.add_argument("--stages", type=int, choices=(2, 3), default=3, help="pipeline contexts (3 = one per node)")
+    ap.add_argument("--stages", type=int, choices=(2, 3), default=2,
+                    help="pipeline contexts: 2 = front end + mapping (measured faster), 3 = one per node")
     ap.add_argument("--profile-json", default="", help="also dump per-frame stage timings here")
     ap.add_argument("--c4-launches", type=int, default=20, help="timed launches of the C4 search (0 = skip)")
     ap.add_argument("--prof-frames", type=int, default=8,

@@ -270,15 +270,16 @@ class Context:
 
 
 class Pipeline:
-    """The reference's node split on one GPU. stages=3 (default): scanRegistration, laserOdometry and
+    """The reference's node split on one GPU. stages=3: scanRegistration, laserOdometry and
     laserMapping each own a context (own HIP stream), and scan k+2's feature extraction, scan k+1's
     odometry and scan k's mapping run concurrently — the three ROS processes of the reference
     (src/scanRegistration.cpp, src/laserOdometry.cpp, src/laserMapping.cpp:934 `process` thread),
     handing over device to device (aloam_forward_features / aloam_forward_mapping_input).
-    stages=2: scanRegistration + laserOdometry share the front context.
+    stages=2 (default; measured faster on one MI355X — three concurrent contexts contend): scanRegistration
+    + laserOdometry share the front context.
     Every scan still goes through all three stages, in order; results equal Context.process_scan's."""
 
-    def __init__(self, params=None, device=0, stages=3):
+    def __init__(self, params=None, device=0, stages=2):
         from concurrent.futures import ThreadPoolExecutor
         self.stages = stages
         self.front = Context(params, device)                       # scanRegistration (+ odometry if 2 stages)
