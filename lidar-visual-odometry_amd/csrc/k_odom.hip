@@ -257,7 +257,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
     const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
     const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s,
-    RowSet<9>& r9, RowSet<25>& r25, RowSet<128>& r128) {
+    RowSet<9>& r9, RowSet<25>& r25, RowSet<128>& r128, int exp) {
     const int lane = lane_id();
     const bool is_corner = qi < n_sharp;
     const float4 pi = is_corner ? sharp[qi] : flat[qi - n_sharp];
@@ -276,8 +276,10 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     int closest = -1;
     float d2 = 0.f;
     int found;
-    if (is_corner) found = n > 0 ? wave_nn1(*gdc, cs_c, sp_c, si_c, sx, sy, sz, &closest, &d2, r9, r25) : 0;
+    if (exp & 1) { found = n > 0; closest = (qi * 37) % max(n, 1); }
+    else if (is_corner) found = n > 0 ? wave_nn1(*gdc, cs_c, sp_c, si_c, sx, sy, sz, &closest, &d2, r9, r25) : 0;
     else found = n > 0 ? wave_nn1(*gds, cs_s, sp_s, si_s, sx, sy, sz, &closest, &d2, r9, r25) : 0;
+    if (exp & 2) found = 0;
     if (found) {
         const int cid = line_of(cl[closest].w);
         int i2, i3;
@@ -323,7 +325,8 @@ __global__ void __launch_bounds__(256) k_odom_search(
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
     const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
-    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s) {
+    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s,
+    int exp) {
     __shared__ RowSet<9> rows9[256 / WAVE];
     __shared__ RowSet<25> rows25[256 / WAVE];
     __shared__ RowSet<128> rows128[256 / WAVE];
@@ -332,7 +335,8 @@ __global__ void __launch_bounds__(256) k_odom_search(
     const int w = threadIdx.x / WAVE;
     for (int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; qi < nq; qi += gridDim.x * (blockDim.x / WAVE))
         odom_query(qi, n_sharp, sharp, flat, corner_last, n_cl, surf_last, n_sl, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s,
-                   odom, out, round_cnt, line_sorted, wdc, ws_c, wp_c, wi_c, wds, ws_s, wp_s, wi_s, rows9[w], rows25[w], rows128[w]);
+                   odom, out, round_cnt, line_sorted, wdc, ws_c, wp_c, wi_c, wds, ws_s, wp_s, wi_s, rows9[w], rows25[w], rows128[w],
+                   exp);
 }
 
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582)
@@ -345,6 +349,7 @@ __global__ void k_odom_compose(OdomState* o) {
     o->q_w[0] = n.x; o->q_w[1] = n.y; o->q_w[2] = n.z; o->q_w[3] = n.w;
 }
 
+static const int g_odom_exp = getenv("ALOAM_ODOM_EXP") ? atoi(getenv("ALOAM_ODOM_EXP")) : 0;   // profiling experiments only
 // fixed launch: one wave per possible feature point (caps 12 sharp + 24 flat per line); waves past
 // the device-side count exit at once
 void odom_round_search(Ctx& C, int round) {
@@ -356,7 +361,7 @@ void odom_round_search(Ctx& C, int round) {
         C.g_surf_last.desc, C.g_surf_last.cell_start, C.g_surf_last.pts, C.g_surf_last.idx,
         C.d_odom, C.d_factors, C.d_round_cnt + 2 * round, C.d_last_sorted,
         C.g_corner_win.desc, C.g_corner_win.cell_start, C.g_corner_win.pts, C.g_corner_win.idx,
-        C.g_surf_win.desc, C.g_surf_win.cell_start, C.g_surf_win.pts, C.g_surf_win.idx);
+        C.g_surf_win.desc, C.g_surf_win.cell_start, C.g_surf_win.pts, C.g_surf_win.idx, g_odom_exp);
     HIPCHK(hipGetLastError());
 }
 
