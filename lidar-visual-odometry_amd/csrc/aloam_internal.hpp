@@ -157,8 +157,8 @@ struct Ctx {
     int cap_factors = 0;
     LMState* d_lm = nullptr;
     double* d_partials = nullptr;
-    double* d_coop_part = nullptr;  // 2 x 64 x 29 doubles (LM pass partials, double-buffered)
-    unsigned* d_bar = nullptr;       // grid barrier {count, generation}
+    unsigned long long* d_lm_recs = nullptr;  // 2 x 64 x 32 u64: LM pass partial records + tags (double-buffered)
+    unsigned long long* d_lm_seq = nullptr;   // LM launch sequence number (record tags = seq*256 + pass + 1)
     int map_slots_hint = 0;
     int* d_last_sorted = nullptr;    // [2]: corner_last / surf_last ordered by scan line          // last mapping frame's stack sizes (LM grid sizing only)
     int* d_bar_err = nullptr;        // set if a grid barrier timed out (device view of h_bar_err)

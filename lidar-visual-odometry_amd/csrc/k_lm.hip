@@ -20,11 +20,14 @@ constexpr int LB = 256;          // threads per LM workgroup
 constexpr int NACC = 29;         // 21 JtJ + 6 Jtr + cost + residual-block count
 
 // residual and 6-column tangent Jacobian of one factor at (q, t). Returns #residuals (0 = invalid).
-__device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
-    if (f.type < 0) return 0;
+// One factor type per instantiation: every branch is resolved at compile time, so r/J stay in
+// registers (a run-time type switch over shared r/J arrays made the compiler sink their stores into
+// dynamically indexed scratch).
+template <int TY>
+__device__ __forceinline__ int eval_factor_t(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
     const dvec3 cp{f.cp[0], f.cp[1], f.cp[2]};
     dvec3 pr, lp;
-    if (f.type == 0 || f.type == 1) {
+    if constexpr (TY == 0 || TY == 1) {
         dquat ql = qslerp_identity(1.0, q);          // lidarFactor.hpp:29,81 (s = 1)
         pr = qrot(ql, cp);
         lp = {pr.x + 1.0 * t[0], pr.y + 1.0 * t[1], pr.z + 1.0 * t[2]};
@@ -32,7 +35,7 @@ __device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q
         pr = qrot(q, cp);                            // lidarFactor.hpp:120,154
         lp = {pr.x + t[0], pr.y + t[1], pr.z + t[2]};
     }
-    if (f.type == 0) {                               // LidarEdgeFactor (lidarFactor.hpp:19-43)
+    if constexpr (TY == 0) {                         // LidarEdgeFactor (lidarFactor.hpp:19-43)
         const dvec3 a{f.a[0], f.a[1], f.a[2]}, b{f.b[0], f.b[1], f.b[2]};
         const dvec3 u{lp.x - a.x, lp.y - a.y, lp.z - a.z}, v{lp.x - b.x, lp.y - b.y, lp.z - b.z};
         const dvec3 nu = dcross(u, v);
@@ -55,9 +58,9 @@ __device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q
         J[2][3] = w.y * inv;   J[2][4] = -w.x * inv; J[2][5] = 0.0;
         return 3;
     }
-    if (f.type == 1 || f.type == 2) {
+    if constexpr (TY == 1 || TY == 2) {
         dvec3 nrm;
-        if (f.type == 1) {                           // LidarPlaneFactor (lidarFactor.hpp:69-90)
+        if constexpr (TY == 1) {                           // LidarPlaneFactor (lidarFactor.hpp:69-90)
             nrm = {f.b[0], f.b[1], f.b[2]};
             r[0] = (lp.x - f.a[0]) * nrm.x + (lp.y - f.a[1]) * nrm.y + (lp.z - f.a[2]) * nrm.z;
         } else {                                     // LidarPlaneNormFactor (lidarFactor.hpp:113-125)
@@ -68,17 +71,28 @@ __device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q
         J[0][0] = -2.0 * np.x; J[0][1] = -2.0 * np.y; J[0][2] = -2.0 * np.z;
         J[0][3] = nrm.x; J[0][4] = nrm.y; J[0][5] = nrm.z;
         return 1;
+    } else {
+        // LidarDistanceFactor (lidarFactor.hpp:147-161): J_rot = -2 [pr]x, J_t = I
+        r[0] = lp.x - f.a[0]; r[1] = lp.y - f.a[1]; r[2] = lp.z - f.a[2];
+        J[0][0] = 0.0;           J[0][1] = 2.0 * pr.z;   J[0][2] = -2.0 * pr.y;
+        J[1][0] = -2.0 * pr.z;   J[1][1] = 0.0;          J[1][2] = 2.0 * pr.x;
+        J[2][0] = 2.0 * pr.y;    J[2][1] = -2.0 * pr.x;  J[2][2] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) J[i][3 + k] = (i == k) ? 1.0 : 0.0;
+        return 3;
     }
-    // LidarDistanceFactor (lidarFactor.hpp:147-161): J_rot = -2 [pr]x, J_t = I
-    r[0] = lp.x - f.a[0]; r[1] = lp.y - f.a[1]; r[2] = lp.z - f.a[2];
-    J[0][0] = 0.0;           J[0][1] = 2.0 * pr.z;   J[0][2] = -2.0 * pr.y;
-    J[1][0] = -2.0 * pr.z;   J[1][1] = 0.0;          J[1][2] = 2.0 * pr.x;
-    J[2][0] = 2.0 * pr.y;    J[2][1] = -2.0 * pr.x;  J[2][2] = 0.0;
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int k = 0; k < 3; k++) J[i][3 + k] = (i == k) ? 1.0 : 0.0;
-    return 3;
+}
+
+__device__ __forceinline__ int eval_factor(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
+    switch (f.type) {
+        case 0: return eval_factor_t<0>(f, q, t, r, J);
+        case 1: return eval_factor_t<1>(f, q, t, r, J);
+        case 2: return eval_factor_t<2>(f, q, t, r, J);
+        case 3: return eval_factor_t<3>(f, q, t, r, J);
+        default: return 0;
+    }
 }
 
 // ceres::HuberLoss(0.1) + Corrector (rho'' <= 0 => plain sqrt(rho') scaling)
@@ -107,12 +121,13 @@ __device__ __forceinline__ void add_row(const double* J, double r, double sc, do
     for (int a = 0; a < 6; a++) acc[21 + a] += Ji[a] * ri;
 }
 
-__device__ __forceinline__ void accumulate(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
+template <int TY>
+__device__ __forceinline__ void accumulate_t(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
     double r[3], J[3][6];
-    const int m = eval_factor(f, q, t, r, J);
-    if (!m) return;
+    constexpr int m = (TY == 1 || TY == 2) ? 1 : 3;
+    eval_factor_t<TY>(f, q, t, r, J);
     double rho0, sc;
-    if (m == 1) {
+    if constexpr (m == 1) {
         sc = huber_scale(r[0] * r[0], &rho0);
         add_row(J[0], r[0], sc, acc);
     } else {
@@ -127,15 +142,36 @@ __device__ __forceinline__ void accumulate(const aloam_factor& f, const dquat& q
     acc[27] += 0.5 * rho0;
     acc[28] += 1.0;
 }
+__device__ __forceinline__ void accumulate(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
+    switch (f.type) {
+        case 0: accumulate_t<0>(f, q, t, acc); break;
+        case 1: accumulate_t<1>(f, q, t, acc); break;
+        case 2: accumulate_t<2>(f, q, t, acc); break;
+        case 3: accumulate_t<3>(f, q, t, acc); break;
+        default: break;
+    }
+}
 
 // ---- host-side-free LM math (thread 0 of the last workgroup) -------------------------------
+// Plus of Ceres' EigenQuaternionParameterization: q' = [sin|d|/|d| d, cos|d|] * q, t' = t + d_t.
+// Steps are small (|d| < 0.25 rad), where sin(x)/x and cos(x) are evaluated as even Taylor
+// polynomials in |d|^2 (truncation < 1e-17; no sqrt, sincos or division on the solver's serial
+// tail); larger steps take the libm path.
 __device__ __forceinline__ void plus7(const double* x, const double* d, double* out) {
-    const double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    const double nd2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     dquat q{x[0], x[1], x[2], x[3]};
-    if (nd > 0.0) {
-        double sn, cs;
-        sincos(nd, &sn, &cs);
-        const double sdd = sn / nd;
+    if (nd2 > 0.0) {
+        double sdd, cs;
+        if (nd2 < 0.0625) {
+            const double y = nd2;
+            sdd = 1.0 + y * (-1.0 / 6 + y * (1.0 / 120 + y * (-1.0 / 5040 + y * (1.0 / 362880 + y * (-1.0 / 39916800 + y * (1.0 / 6227020800.0))))));
+            cs = 1.0 + y * (-0.5 + y * (1.0 / 24 + y * (-1.0 / 720 + y * (1.0 / 40320 + y * (-1.0 / 3628800 + y * (1.0 / 479001600.0 + y * (-1.0 / 87178291200.0)))))));
+        } else {
+            const double nd = sqrt(nd2);
+            double sn;
+            sincos(nd, &sn, &cs);
+            sdd = sn / nd;
+        }
         dquat dq{sdd * d[0], sdd * d[1], sdd * d[2], cs};
         dquat r = qmul(dq, q);
         out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
@@ -168,6 +204,18 @@ __device__ __forceinline__ double Aget(const double* A, int a, int b) {   // upp
     if (a > b) { int t = a; a = b; b = t; }
     return A[a * 6 - a * (a - 1) / 2 + (b - a)];
 }
+// 1/sqrt(s) from the hardware estimate plus three Newton steps (quadratic convergence to full
+// precision); the Cholesky pivots take this instead of a sqrt and a division each, which are the
+// longest latency chain of the serial solver tail.
+__device__ __forceinline__ double rsqrt_nr(double s) {
+    double r = __builtin_amdgcn_rsq(s);
+#pragma unroll
+    for (int it = 0; it < 3; it++) {
+        const double e = fma(-(s * r), r, 1.0);
+        r = fma(0.5 * r, e, r);
+    }
+    return r;
+}
 __device__ __forceinline__ bool chol_solve6(double M[6][6], const double* rhs, double* y) {
     double L[6][6], inv[6];
     bool ok = true;
@@ -177,8 +225,8 @@ __device__ __forceinline__ bool chol_solve6(double M[6][6], const double* rhs, d
 #pragma unroll
         for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
         ok = ok && (s > 0.0);
-        L[j][j] = sqrt(s);
-        inv[j] = 1.0 / L[j][j];            // one division per column; the rest multiply
+        inv[j] = rsqrt_nr(s);
+        L[j][j] = s * inv[j];
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
             double v = M[i][j];
@@ -236,12 +284,12 @@ __device__ __forceinline__ void lm_next_step(LMState* st, aloam_lm_summary* out,
             #pragma unroll
             for (int a = 0; a < 6; a++) st->diag[a] = fmin(fmax(As[a][a], 1e-6), 1e32);
         double M[6][6];
+        const double inv_radius = 1.0 / st->radius;
         #pragma unroll
         for (int a = 0; a < 6; a++) {
             #pragma unroll
             for (int b = 0; b < 6; b++) M[a][b] = As[a][b];
-            const double D = sqrt(st->diag[a] / st->radius);
-            M[a][a] += D * D;
+            M[a][a] += st->diag[a] * inv_radius;   // D^2 with D = sqrt(diag / radius)
         }
         double y[6];
         const bool ok = chol_solve6(M, gs, y);
@@ -329,6 +377,14 @@ __device__ __forceinline__ void lm_tail(LMState* st, const double* tot, int pass
     lm_next_step(st, out, max_iter);
 }
 
+// The same tail on a register copy of the state (one LDS read/write burst instead of dependent LDS
+// round trips inside the step computation).
+__device__ __forceinline__ void lm_tail_reg(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+    LMState L = *st;
+    lm_tail(&L, tot, pass, xp, out, max_iter);
+    *st = L;
+}
+
 // Sum of NACC doubles over `nrows` rows of an LDS table rows[r*NACC + i] into tot[] (fixed order =>
 // deterministic): 8 x NACC threads each add every 8th row of one column, then NACC threads add the
 // 8 partials. Independent LDS loads, no shuffle dependency chains (the 29 chained wave reductions
@@ -352,47 +408,70 @@ __device__ __forceinline__ void reduce_rows(const double* rows, int nrows, doubl
     }
     __syncthreads();
 }
-// block-wide sum of NACC doubles per thread (NT >= 8 * NACC threads); rows = NT*NACC LDS doubles
+// v[l] + v[l ^ 32] + v[l ^ 16] + v[l ^ 48] in every lane l, via the gfx950 cross-row lane swaps
+// (no LDS, no dependent shuffles): same summation order in every lane, so the result is deterministic.
+__device__ __forceinline__ double quad_row_sum(double v) {
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const double h = __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+    const unsigned lo2 = (unsigned)__double2loint(h), hi2 = (unsigned)__double2hiint(h);
+    const auto c = __builtin_amdgcn_permlane16_swap(lo2, lo2, false, false);
+    const auto d = __builtin_amdgcn_permlane16_swap(hi2, hi2, false, false);
+    return __hiloint2double((int)d[0], (int)c[0]) + __hiloint2double((int)d[1], (int)c[1]);
+}
+// block-wide sum of NACC doubles per thread (NT >= 8 * NACC threads): each wave first folds its 64
+// lanes to 16 with lane swaps, so only NT/4 rows go through LDS (rows = NT/4 * NACC doubles)
 template <int NT>
 __device__ __forceinline__ void block_reduce_acc(const double* acc, double* rows, double* part8, double* tot) {
     static_assert(NT >= 8 * NACC, "reduce_rows needs 8*NACC threads");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NACC; i++) rows[threadIdx.x * NACC + i] = acc[i];
-    __syncthreads();
-    reduce_rows(rows, NT, part8, tot);
-}
-
-// Grid barrier for the persistent multi-workgroup solver (count + generation; the last arriver
-// resets the count, so consecutive launches with different grid sizes need no re-initialisation).
-// Bounded spin: a barrier that does not complete flags an error instead of hanging the queue.
-__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned nblocks, int* err) {
-    // All cross-workgroup data (partials, counters) moves through agent-scope RELAXED atomics, which
-    // are coherent across XCDs on their own; ordering is by completion (s_waitcnt vmcnt(0) before
-    // the next access). Acquire/release here would add an L2 writeback + invalidate per poll.
-    __shared__ int ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ok = 1;
-        const unsigned gen = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (arrived == nblocks - 1) {
-            const unsigned r = __hip_atomic_fetch_sub(&bar[0], nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(&bar[1], 1u + 0u * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            int spins = 0;
-            while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1 << 22)) { ok = 0; atomicExch(err, 1); break; }
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < NACC; i++) {
+        const double v = quad_row_sum(acc[i]);
+        if (lane < 16) rows[(wave * 16 + lane) * NACC + i] = v;
     }
     __syncthreads();
-    return ok;
+    reduce_rows(rows, NT / 4, part8, tot);
+}
+
+// Cross-workgroup exchange for the persistent solver: a tagged all-gather instead of a counter
+// barrier. Workgroup b writes its NACC partials into record b of this pass's buffer, waits for the
+// stores to complete, then writes the record's tag = epoch; every workgroup polls the G tags (one
+// lane each) until all equal the epoch and then reads the G records. There is no read-modify-write
+// on a shared word, so arrivals do not serialise at one address. All cross-workgroup data moves
+// through agent-scope RELAXED atomics (coherent across XCDs on their own), ordered by completion
+// (s_waitcnt vmcnt(0)); acquire/release would add an L2 writeback + invalidate per poll.
+// Epochs are unique per (launch, pass): seq (read at kernel start, bumped by workgroup 0 at the end)
+// * 256 + pass + 1, so records left by earlier launches never match and nothing is re-initialised.
+// Bounded spin: an exchange that does not complete flags an error instead of hanging the queue.
+constexpr int LM_REC = 32;   // u64 per record: NACC partials, tag at [LM_REC - 1]
+__device__ __forceinline__ bool gather_partials(unsigned long long* buf, unsigned long long epoch, const double* tot,
+                                                double* rows, unsigned G, int* err) {
+    __shared__ int ok;
+    unsigned long long* mine = buf + (size_t)blockIdx.x * LM_REC;
+    if (threadIdx.x < 64) {   // wave 0: publish, then poll
+        if (threadIdx.x < NACC)
+            __hip_atomic_store(&mine[threadIdx.x], (unsigned long long)__double_as_longlong(tot[threadIdx.x]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) __hip_atomic_store(&mine[LM_REC - 1], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long* tag = buf + (size_t)threadIdx.x * LM_REC + (LM_REC - 1);
+        int spins = 0, good = 1;
+        while (!__all(threadIdx.x >= G || __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1 << 22)) { good = 0; break; }
+        }
+        if (threadIdx.x == 0) { ok = good; if (!good) atomicExch(err, 1); }
+    }
+    __syncthreads();
+    if (!ok) return false;
+    for (int i = threadIdx.x; i < (int)G * NACC; i += blockDim.x) {   // all records -> LDS in one round trip
+        const int b = i / NACC, c = i - b * NACC;
+        rows[i] = __longlong_as_double(__hip_atomic_load(&buf[(size_t)b * LM_REC + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();
+    return true;
 }
 
 // Whole Solve as ONE persistent launch over G workgroups: each pass evaluates its slice, publishes
@@ -409,9 +488,9 @@ __device__ unsigned long long g_lm_ts[8][5];   // micro-benchmark only: block-0 
 #define LM_TS(p, k) do { } while (0)
 #endif
 __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
-                                                double* partials, unsigned* bar, int* err, aloam_lm_summary* out,
+                                                unsigned long long* recs, unsigned long long* seq, int* err, aloam_lm_summary* out,
                                                 int max_iter, const int* gate, const int* dn, int cache_cap) {
-    __shared__ double rows[CB * NACC];
+    __shared__ double rows[(CB / 4 > LM_COOP_MAX ? CB / 4 : LM_COOP_MAX) * NACC];   // wave-folded rows, then the G records
     __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
     __shared__ double xl[7];
@@ -424,8 +503,11 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
     const int per = (nslots + G - 1) / G;
     const int f0 = blockIdx.x * per, f1 = min(nslots, f0 + per);
     const bool cached = per <= cache_cap;           // slots read from HBM once, then from LDS
+    __shared__ unsigned long long ep;
     if (threadIdx.x < 7) xl[threadIdx.x] = xp[threadIdx.x];
+    if (threadIdx.x == 0) ep = __hip_atomic_load(seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * 256 + 1;
     __syncthreads();
+    const unsigned long long epoch0 = ep;
     for (int pass = 0; pass <= max_iter; pass++) {
         const double* xs = pass == 0 ? xl : ls.cand;
         const dquat q{xs[0], xs[1], xs[2], xs[3]};
@@ -443,15 +525,8 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
         LM_TS(pass, 4);
         block_reduce_acc<CB>(acc, rows, part8, tot);
         LM_TS(pass, 0);
-        double* part = partials + (size_t)(pass & 1) * LM_COOP_MAX * NACC;
-        if (threadIdx.x < NACC)
-            __hip_atomic_store((unsigned long long*)&part[blockIdx.x * NACC + threadIdx.x], __double_as_longlong(tot[threadIdx.x]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!grid_barrier(bar, G, err)) return;
+        if (!gather_partials(recs + (size_t)(pass & 1) * LM_COOP_MAX * LM_REC, epoch0 + pass, tot, rows, G, err)) return;
         LM_TS(pass, 1);
-        for (int i = threadIdx.x; i < (int)G * NACC; i += CB)     // all partials -> LDS in one round trip
-            rows[i] = __longlong_as_double(__hip_atomic_load((unsigned long long*)&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        __syncthreads();
         reduce_rows(rows, G, part8, tot);
         LM_TS(pass, 2);
         if (threadIdx.x == 0) {
@@ -463,6 +538,8 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
         if (done) break;
     }
     if (blockIdx.x == 0) {
+        // every workgroup has read seq (it published a pass-0 record before workgroup 0 got here)
+        if (threadIdx.x == 0) __hip_atomic_store(seq, epoch0 / 256 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (threadIdx.x < 7) xp[threadIdx.x] = xl[threadIdx.x];
         const int nw = sizeof(LMState) / 8;
         for (int i = threadIdx.x; i < nw; i += CB) ((unsigned long long*)st)[i] = ((const unsigned long long*)&ls)[i];
@@ -489,15 +566,15 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
     G = std::max(1, std::min(LM_COOP_MAX, G));
     const int cap = std::min(LM_CACHE, (nslots + G - 1) / G);          // LDS slots per workgroup
     const size_t lds = sizeof(aloam_factor) * (size_t)cap;
-    k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_coop_part, C.d_bar, C.d_bar_err, out,
-                                      C.P.max_solver_iterations, gate, d_nslots2, cap);
+    k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_lm_recs, C.d_lm_seq, C.d_bar_err, out,
+                                      std::min(C.P.max_solver_iterations, 200), gate, d_nslots2, cap);
     HIPCHK(hipGetLastError());
 }
 
 // ---- test entry: per-factor residuals / Jacobians and the normal equations ----
 __global__ void k_eval_factors(const aloam_factor* __restrict__ f, int n, const double* x, int robust, double* res,
                                double* jac, double* neq) {
-    __shared__ double rows[LB * NACC];
+    __shared__ double rows[LB / 4 * NACC];
     __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
     const dquat q{x[0], x[1], x[2], x[3]};

@@ -21,6 +21,32 @@ __global__ void k_time_eval(const aloam_factor* f, int n, const double* x, doubl
     outv[i] = s;
     cyc[i] = c1 - c0;
 }
+template <int V>
+__global__ void __launch_bounds__(64) k_tail_bench(const LMState* snap, long long* cyc, int reps) {
+    __shared__ LMState ls;
+    __shared__ double tot[NACC];
+    __shared__ double xl[7];
+    if (threadIdx.x != 0) return;
+    long long sum = 0;
+    for (int r = 0; r < reps; r++) {
+        ls = *snap;
+        ls.done = 0; ls.iteration = 0;
+        for (int i = 0; i < 21; i++) tot[i] = ls.A[i] * (1.0 + 1e-3 * r);
+        for (int i = 0; i < 6; i++) tot[21 + i] = ls.g[i];
+        tot[27] = ls.cost * 0.5; tot[28] = ls.nres;
+        for (int i = 0; i < 7; i++) xl[i] = ls.x[i];
+        ls.mcc = ls.cost;  ls.step_norm = 1.0;
+        __builtin_amdgcn_s_waitcnt(0);
+        const long long c0 = clock64();
+        if (V == 0) lm_tail(&ls, tot, 1, xl, nullptr, 4);
+        else lm_tail_reg(&ls, tot, 1, xl, nullptr, 4);
+        __builtin_amdgcn_s_waitcnt(0);
+        const long long c1 = clock64();
+        sum += c1 - c0;
+    }
+    cyc[0] = sum / reps;
+    cyc[1] = ls.iteration;
+}
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 20000;
     const int mode = argc > 2 ? atoi(argv[2]) : -1;
@@ -39,7 +65,7 @@ int main(int argc, char** argv) {
     hipStreamCreate(&C.stream);
     aloam_factor* df; hipMalloc(&df, sizeof(aloam_factor) * n); hipMemcpy(df, f.data(), sizeof(aloam_factor) * n, hipMemcpyHostToDevice);
     hipMalloc(&C.d_lm_sum, sizeof(aloam_lm_summary) * 32); hipMalloc(&C.d_lm, sizeof(LMState));
-    hipMalloc(&C.d_coop_part, sizeof(double) * 2 * 64 * 32); hipMalloc(&C.d_bar, 16); hipMemset(C.d_bar, 0, 16);
+    hipMalloc(&C.d_lm_recs, 8 * 2 * 64 * 32); hipMemset(C.d_lm_recs, 0, 8 * 2 * 64 * 32); hipMalloc(&C.d_lm_seq, 16); hipMemset(C.d_lm_seq, 0, 16);
     hipMalloc(&C.d_bar_err, 16); hipMemset(C.d_bar_err, 0, 16);
     double x0[7] = {0.01, -0.02, 0.005, 1, 0.1, 0.2, -0.1}; double nq = sqrt(x0[0]*x0[0]+x0[1]*x0[1]+x0[2]*x0[2]+1); for (int i=0;i<4;i++) x0[i]/=nq;
     double* dx; hipMalloc(&dx, 7 * 8);
@@ -65,10 +91,13 @@ int main(int argc, char** argv) {
     for (int p = 0; p < 5; p++)
         printf("pass %d: eval %.2f blockreduce %.2f us, barrier %.2f us, reduce %.2f us, tail %.2f us\n", p,
                p ? (ts[p][4] - ts[p - 1][3]) / 100.0 : 0.0, (ts[p][0] - ts[p][4]) / 100.0, (ts[p][1] - ts[p][0]) / 100.0, (ts[p][2] - ts[p][1]) / 100.0, (ts[p][3] - ts[p][2]) / 100.0);
-    unsigned long long tt[8];
-    hipMemcpyFromSymbol(tt, HIP_SYMBOL(aloam::g_tail_ts), sizeof(tt));
-    printf("next_step: build M %.2f us, chol %.2f, model cost %.2f, plus7 %.2f, norm %.2f\n", (tt[1]-tt[0])/100.0,
-           (tt[2]-tt[1])/100.0, (tt[3]-tt[2])/100.0, (tt[4]-tt[3])/100.0, (tt[5]-tt[4])/100.0);
+    {
+        long long* cy; hipMalloc(&cy, 16); long long hc[2];
+        k_tail_bench<0><<<1, 64>>>(C.d_lm, cy, 50); hipMemcpy(hc, cy, 16, hipMemcpyDeviceToHost);
+        printf("tail (LDS state): %lld cycles, it %lld\n", hc[0], hc[1]);
+        k_tail_bench<1><<<1, 64>>>(C.d_lm, cy, 50); hipMemcpy(hc, cy, 16, hipMemcpyDeviceToHost);
+        printf("tail (register state): %lld cycles, it %lld\n", hc[0], hc[1]);
+    }
     aloam_lm_summary s; hipMemcpy(&s, C.d_lm_sum, sizeof(s), hipMemcpyDeviceToHost);
     printf("iters %d succ %d term %d cost %g -> %g\n", s.iterations, s.successful_steps, s.termination, s.initial_cost, s.final_cost);
     return 0;
