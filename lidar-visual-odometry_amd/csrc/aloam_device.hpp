@@ -57,21 +57,63 @@ __device__ inline dquat qslerp_identity(double t, const dquat& q) {
 // ---- wave64 helpers ------------------------------------------------------------------
 __device__ inline int lane_id() { return threadIdx.x & (WAVE - 1); }
 
-__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long t = __shfl_xor(v, o, WAVE);
-        v = t < v ? t : v;
-    }
+// Cross-lane exchange without LDS: DPP for partners inside a 16-lane row (quad_perm swaps, then
+// half-row and row mirrors — after the quad steps a mirror reaches exactly the other half), the
+// gfx950 row-pair and half-wave swaps for 16 and 32. A __shfl_xor is a ds_bpermute round trip
+// through the LDS unit per step; these are plain VALU ops.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned swap16_u32(unsigned v) {      // value of lane l ^ 16
+    const auto s = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((threadIdx.x >> 4) & 1) ? s[0] : s[1];
+}
+__device__ __forceinline__ unsigned swap32_u32(unsigned v) {      // value of lane l ^ 32
+    const auto s = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return ((threadIdx.x >> 5) & 1) ? s[0] : s[1];
+}
+// partner value at step k of a wave all-reduce (k = 0..5: quad xor 1, quad xor 2, half-row mirror,
+// row mirror, row pair, half wave)
+template <int K>
+__device__ __forceinline__ unsigned xstep_u32(unsigned v) {
+    if constexpr (K == 0) return dpp_u32<0xB1>(v);        // quad_perm [1,0,3,2]
+    else if constexpr (K == 1) return dpp_u32<0x4E>(v);   // quad_perm [2,3,0,1]
+    else if constexpr (K == 2) return dpp_u32<0x141>(v);  // row_half_mirror
+    else if constexpr (K == 3) return dpp_u32<0x140>(v);  // row_mirror
+    else if constexpr (K == 4) return swap16_u32(v);
+    else return swap32_u32(v);
+}
+template <int K>
+__device__ __forceinline__ unsigned long long xstep_u64(unsigned long long v) {
+    return ((unsigned long long)xstep_u32<K>((unsigned)(v >> 32)) << 32) | xstep_u32<K>((unsigned)v);
+}
+// all-reduce over the first 2^NS steps' lanes (NS = 6: whole wave; NS = 3: aligned groups of 8)
+template <int NS, typename F>
+__device__ __forceinline__ unsigned long long allreduce_u64(unsigned long long v, F op) {
+    if constexpr (NS > 0) v = op(v, xstep_u64<0>(v));
+    if constexpr (NS > 1) v = op(v, xstep_u64<1>(v));
+    if constexpr (NS > 2) v = op(v, xstep_u64<2>(v));
+    if constexpr (NS > 3) v = op(v, xstep_u64<3>(v));
+    if constexpr (NS > 4) v = op(v, xstep_u64<4>(v));
+    if constexpr (NS > 5) v = op(v, xstep_u64<5>(v));
     return v;
 }
-__device__ inline unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long t = __shfl_xor(v, o, WAVE);
-        v = t > v ? t : v;
-    }
+template <int NS, typename F>
+__device__ __forceinline__ unsigned allreduce_u32(unsigned v, F op) {
+    if constexpr (NS > 0) v = op(v, xstep_u32<0>(v));
+    if constexpr (NS > 1) v = op(v, xstep_u32<1>(v));
+    if constexpr (NS > 2) v = op(v, xstep_u32<2>(v));
+    if constexpr (NS > 3) v = op(v, xstep_u32<3>(v));
+    if constexpr (NS > 4) v = op(v, xstep_u32<4>(v));
+    if constexpr (NS > 5) v = op(v, xstep_u32<5>(v));
     return v;
+}
+__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
+    return allreduce_u64<6>(v, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
+}
+__device__ inline unsigned long long wave_max_u64(unsigned long long v) {
+    return allreduce_u64<6>(v, [](unsigned long long a, unsigned long long b) { return b > a ? b : a; });
 }
 __device__ inline double wave_sum_d(double v) {
 #pragma unroll
@@ -79,9 +121,7 @@ __device__ inline double wave_sum_d(double v) {
     return v;
 }
 __device__ inline int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
+    return (int)allreduce_u32<6>((unsigned)v, [](unsigned a, unsigned b) { return a + b; });
 }
 __device__ inline unsigned long long lanemask_lt64() {
     int l = lane_id();
@@ -91,6 +131,16 @@ __device__ inline unsigned long long lanemask_lt64() {
 // float >= 0 (or +inf) ordered as unsigned: key = (bits << 32) | index
 __device__ inline unsigned long long dist_key(float d2, int idx) {
     return ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)idx;
+}
+
+// Guarded load without control flow: the address is clamped to element 0 (valid in every buffer
+// this is used on) and the value replaced afterwards. A branch around each load of an unrolled
+// batch makes the compiler wait for the load inside the branch — one memory round trip per load
+// instead of one per batch.
+template <typename T>
+__device__ __forceinline__ T load_or(const T* __restrict__ a, int i, bool ok, T dflt) {
+    const T v = a[ok ? i : 0];
+    return ok ? v : dflt;
 }
 
 // ordered-int encoding of floats for atomic min/max
@@ -138,15 +188,11 @@ __device__ __forceinline__ int build_rows(const float ox, const float oy, const 
     const int x0 = max(cx - m, 0), x1 = min(cx + m, gdx - 1);
     const int w = 2 * m + 1;
     const int nrow = w * w;
-    int b = 0, len = 0;
-    if (lane < nrow && lane < MAXR) {
-        const int y = cy - m + lane % w, z = cz - m + lane / w;
-        if (x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz) {
-            const int c = (z * gdy + y) * gdx;
-            b = start[c + x0];
-            len = start[c + x1 + 1] - b;
-        }
-    }
+    const int y = cy - m + lane % w, z = cz - m + lane / w;
+    const bool ok = lane < nrow && lane < MAXR && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
+    const int c = (z * gdy + y) * gdx;
+    const int b = load_or(start, c + x0, ok, 0);
+    const int len = load_or(start, c + x1 + 1, ok, 0) - b;
     int incl = len;
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -164,14 +210,19 @@ __device__ __forceinline__ int build_rows(const float ox, const float oy, const 
     return total;
 }
 // flattened candidate t -> point position (binary search over the row offsets)
+constexpr int pow2_floor(int v) { int p = 1; while (p * 2 <= v) p *= 2; return p; }
+// Fixed-step binary search (last row r with pre[r] <= t): uniform trip count, so the searches of a
+// lane's several candidates interleave instead of running one data-dependent loop after another.
 template <int MAXR>
 __device__ __forceinline__ int row_pos(const RowSet<MAXR>& rs, int t) {
-    int lo = 0, hi = rs.nr - 1;          // last row r with pre[r] <= t
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (rs.pre[mid] <= t) lo = mid; else hi = mid - 1;
+    const int last = rs.nr - 1;
+    int r = 0;
+#pragma unroll
+    for (int step = pow2_floor(MAXR > 1 ? MAXR - 1 : 1); step >= 1; step >>= 1) {
+        const int c = min(r + step, last);
+        r = rs.pre[c] <= t ? c : r;
     }
-    return rs.b[lo] + (t - rs.pre[lo]);
+    return rs.b[r] + (t - rs.pre[r]);
 }
 }  // namespace aloam
 
@@ -199,8 +250,9 @@ __device__ __forceinline__ int wave_knn_rows(const float ox, const float oy, con
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int t = t0 + u * WAVE + lane;
-            pp[u] = t < total ? row_pos<MAXR>(rs, t) : -1;
-            vv[u] = pp[u] >= 0 ? spts[pp[u]] : make_float4(0, 0, 0, 0);
+            const int pos = row_pos<MAXR>(rs, min(t, total - 1));
+            pp[u] = t < total ? pos : -1;
+            vv[u] = load_or(spts, pp[u], pp[u] >= 0, make_float4(0, 0, 0, 0));
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -254,8 +306,8 @@ __device__ __forceinline__ int thread_knn27(const float ox, const float oy, cons
         const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
         const bool ok = x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
         const int c = (z * gdy + y) * gdx;
-        rb[r] = ok ? start[c + x0] : 0;
-        re[r] = ok ? start[c + x1 + 1] : 0;
+        rb[r] = load_or(start, c + x0, ok, 0);
+        re[r] = load_or(start, c + x1 + 1, ok, 0);
     }
     float bd[K];
     int bi[K], bp[K];
@@ -272,8 +324,8 @@ __device__ __forceinline__ int thread_knn27(const float ox, const float oy, cons
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const bool in = p + u < e;
-                v[u] = in ? spts[p + u] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
-                id[u] = in ? sidx[p + u] : 0x7fffffff;
+                v[u] = load_or(spts, p + u, in, make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+                id[u] = load_or(sidx, p + u, in, 0x7fffffff);
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -325,8 +377,8 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
             const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
             const bool ok = active && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
             const int c = (z * gdy + y) * gdx;
-            rb[r] = ok ? start[c + x0] : 0;
-            pre[r + 1] = pre[r] + (ok ? start[c + x1 + 1] - rb[r] : 0);
+            rb[r] = load_or(start, c + x0, ok, 0);
+            pre[r + 1] = pre[r] + (load_or(start, c + x1 + 1, ok, 0) - rb[r]);
         }
         total = pre[9];
         __builtin_amdgcn_wave_barrier();
@@ -357,8 +409,8 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
                 if ((unsigned)p >= (unsigned)npts) p = -1;                   // defensive: inconsistent index
             }
             ps[u] = p;
-            v[u] = p >= 0 ? spts[p] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
-            if (!IDXW) id[u] = p >= 0 ? sidx[p] : 0x7fffffff;
+            v[u] = load_or(spts, p, p >= 0, make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+            if (!IDXW) id[u] = load_or(sidx, p, p >= 0, 0x7fffffff);
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -383,17 +435,12 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
 #pragma unroll
         for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
         const unsigned long long key = hp < 0 ? ~0ull : dist_key(hd, hi);
-        unsigned long long mn = key;
-#pragma unroll
-        for (int o = 1; o < GS; o <<= 1) {
-            const unsigned long long t = __shfl_xor(mn, o, WAVE);
-            mn = t < mn ? t : mn;
-        }
+        constexpr int NS = GS >= 64 ? 6 : GS >= 32 ? 5 : GS >= 16 ? 4 : GS >= 8 ? 3 : GS >= 4 ? 2 : GS >= 2 ? 1 : 0;
+        const unsigned long long mn = allreduce_u64<NS>(key, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
         // the owner of the minimum (unique: indices are unique) publishes its position
         const bool mine = key == mn && mn != ~0ull;
         int pos = mine ? hp : -1;
-#pragma unroll
-        for (int o = 1; o < GS; o <<= 1) pos = max(pos, __shfl_xor(pos, o, WAVE));
+        pos = (int)allreduce_u32<NS>((unsigned)(pos + 1), [](unsigned a, unsigned b) { return a > b ? a : b; }) - 1;
         if (mine) head++;
         out_pos[k] = pos;
         out_d2[k] = mn == ~0ull ? INFINITY : __uint_as_float((unsigned)(mn >> 32));

@@ -53,7 +53,7 @@ __device__ inline void window_search(const float4* __restrict__ cl, int n, int c
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int j = base + u * WAVE + lane;
-            p[u] = j < n ? cl[j] : make_float4(0, 0, 0, 0);
+            p[u] = load_or(cl, j, j < n, make_float4(0, 0, 0, 0));
         }
         int first_brk = 0x7fffffff;
 #pragma unroll
@@ -92,7 +92,7 @@ __device__ inline void window_search(const float4* __restrict__ cl, int n, int c
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int j = base - u * WAVE - lane;
-            p[u] = j >= 0 ? cl[j] : make_float4(0, 0, 0, 0);
+            p[u] = load_or(cl, j, j >= 0, make_float4(0, 0, 0, 0));
         }
         int first_brk = -1;
 #pragma unroll

@@ -719,12 +719,10 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
             for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
         }
 #pragma unroll
-        for (int d = 0; d < 3; d++)
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                mn[d] = min(mn[d], (unsigned)__shfl_xor((int)mn[d], o, WAVE));
-                mx[d] = max(mx[d], (unsigned)__shfl_xor((int)mx[d], o, WAVE));
-            }
+        for (int d = 0; d < 3; d++) {
+            mn[d] = allreduce_u32<6>(mn[d], [](unsigned a, unsigned b) { return min(a, b); });
+            mx[d] = allreduce_u32<6>(mx[d], [](unsigned a, unsigned b) { return max(a, b); });
+        }
         if (lane_id() == 0)
             for (int d = 0; d < 3; d++) { atomicMin(&s_bb[d], mn[d]); atomicMax(&s_bb[3 + d], mx[d]); }
     }

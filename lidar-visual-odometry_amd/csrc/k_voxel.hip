@@ -95,7 +95,7 @@ __global__ void k_vox_centroids(const float4* __restrict__ pts, const int* d_n, 
 #pragma unroll
         for (int u = 0; u < 8; u++) vi[u] = t0 + u < h1 ? vals[t0 + u] : -1;
 #pragma unroll
-        for (int u = 0; u < 8; u++) p[u] = vi[u] >= 0 ? pts[vi[u]] : make_float4(0, 0, 0, 0);
+        for (int u = 0; u < 8; u++) p[u] = load_or(pts, vi[u], vi[u] >= 0, make_float4(0, 0, 0, 0));
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (vi[u] >= 0) { c.x += p[u].x; c.y += p[u].y; c.z += p[u].z; c.w += p[u].w; }
