@@ -109,6 +109,23 @@ __device__ __forceinline__ unsigned allreduce_u32(unsigned v, F op) {
     if constexpr (NS > 5) v = op(v, xstep_u32<5>(v));
     return v;
 }
+// Inclusive prefix sum over the wave with DPP (row shifts 1/2/4/8, then row broadcasts of lanes 15
+// and 31), no LDS round trips. Lanes a shift does not reach keep the 0 of the update's old value.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+// value of a wave-uniform lane (SGPR result, no LDS)
+__device__ __forceinline__ int readlane_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
     return allreduce_u64<6>(v, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
 }
@@ -194,16 +211,12 @@ __device__ __forceinline__ int build_rows(const float ox, const float oy, const 
     const int b = load_or(start, c + x0, ok, 0);
     const int len = load_or(start, c + x1 + 1, ok, 0) - b;
     int incl = len;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int v = __shfl_up(incl, o, WAVE);
-        if (lane >= o) incl += v;
-    }
+    incl = wave_incl_scan(incl);
     const int nr = min(nrow, MAXR);
     __builtin_amdgcn_wave_barrier();
     if (lane < nr) { rs.b[lane] = b; rs.pre[lane + 1] = incl; }
     if (lane == 0) { rs.pre[0] = 0; rs.nr = nr; }
-    const int total = __shfl(incl, nr - 1, WAVE);
+    const int total = readlane_i(incl, nr - 1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -280,7 +293,7 @@ __device__ __forceinline__ int wave_knn_rows(const float ox, const float oy, con
         if (mn == ~0ull) break;
         const unsigned long long won = __ballot(key == mn);
         if (key == mn) head++;
-        out_pos[k] = __shfl(hp, __ffsll((long long)won) - 1, WAVE);
+        out_pos[k] = readlane_i(hp, __ffsll((long long)won) - 1);
         out_d2[k] = __uint_as_float((unsigned)(mn >> 32));
         out_idx[k] = (int)(mn & 0xffffffffu);
         found++;
@@ -458,21 +471,13 @@ __device__ __forceinline__ int block_exscan(int v, int* total) {
     __shared__ int wtot;
     const int lane = lane_id(), w = threadIdx.x / WAVE;
     int incl = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int t = __shfl_up(incl, o, WAVE);
-        if (lane >= o) incl += t;
-    }
+    incl = wave_incl_scan(incl);
     if (lane == WAVE - 1) wsum[w] = incl;
     __syncthreads();
     if (w == 0) {
         const int x = lane < NT / WAVE ? wsum[lane] : 0;
         int xi = x;
-#pragma unroll
-        for (int o = 1; o < NT / WAVE; o <<= 1) {
-            const int t = __shfl_up(xi, o, WAVE);
-            if (lane >= o) xi += t;
-        }
+        xi = wave_incl_scan(xi);
         if (lane < NT / WAVE) wsum[lane] = xi - x;
         if (lane == NT / WAVE - 1) wtot = xi;
     }

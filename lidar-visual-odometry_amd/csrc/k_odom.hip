@@ -159,20 +159,15 @@ __device__ __forceinline__ int build_rows_layers(const GridDesc& gd, const int* 
             }
         }
     }
-    int inc0 = len[0], inc1 = len[1];
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int v0 = __shfl_up(inc0, o, WAVE), v1 = __shfl_up(inc1, o, WAVE);
-        if (lane >= o) { inc0 += v0; inc1 += v1; }
-    }
-    const int t0 = __shfl(inc0, WAVE - 1, WAVE);
+    int inc0 = wave_incl_scan(len[0]), inc1 = wave_incl_scan(len[1]);
+    const int t0 = readlane_i(inc0, WAVE - 1);
     inc1 += t0;
     const int nr = min(nrow, 128);
     __builtin_amdgcn_wave_barrier();
     if (lane < nr) { rs.b[lane] = b[0]; rs.pre[lane + 1] = inc0; }
     if (lane + WAVE < nr) { rs.b[lane + WAVE] = b[1]; rs.pre[lane + WAVE + 1] = inc1; }
     if (lane == 0) { rs.pre[0] = 0; rs.nr = nr; }
-    const int total = nr > WAVE ? __shfl(inc1, nr - WAVE - 1, WAVE) : __shfl(inc0, nr - 1, WAVE);
+    const int total = nr > WAVE ? readlane_i(inc1, nr - WAVE - 1) : readlane_i(inc0, nr - 1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -24,11 +24,7 @@ constexpr int SB = 256;  // threads per block for the per-point kernels
 __device__ inline int block_excl_scan_256(int v, int* sh, int* total) {
     const int lane = lane_id(), w = threadIdx.x / WAVE;
     int x = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        int t = __shfl_up(x, o, WAVE);
-        if (lane >= o) x += t;
-    }
+    x = wave_incl_scan(x);
     if (lane == WAVE - 1) sh[w] = x;
     __syncthreads();
     int base = 0;
@@ -166,21 +162,13 @@ __global__ void __launch_bounds__(BS_T) k_bucket_scan(int* hist, int nb, int N_S
         for (int k = 0; k < BS_E; k++) s += buf[bs_pad(t * BS_E + k)];
         // block exclusive scan of s
         int incl = s;
-#pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const int v = __shfl_up(incl, o, WAVE);
-            if (lane >= o) incl += v;
-        }
+        incl = wave_incl_scan(incl);
         if (lane == WAVE - 1) wsum[w] = incl;
         __syncthreads();
         if (w == 0) {
             int x = lane < BS_T / WAVE ? wsum[lane] : 0;
             int xi = x;
-#pragma unroll
-            for (int o = 1; o < BS_T / WAVE; o <<= 1) {
-                const int v = __shfl_up(xi, o, WAVE);
-                if (lane >= o) xi += v;
-            }
+            xi = wave_incl_scan(xi);
             if (lane < BS_T / WAVE) wsum[lane] = xi - x;               // exclusive wave offsets
             if (lane == BS_T / WAVE - 1) carry_sh = xi;                // chunk total
         }
@@ -223,7 +211,7 @@ __global__ void k_bucket_scatter(const float4* __restrict__ cl, const ScanMeta* 
     unsigned long long active = __ballot(s >= 0);
     while (active) {
         int leader = __ffsll((long long)active) - 1;
-        int ls = __shfl(s, leader, WAVE);
+        int ls = readlane_i(s, leader);
         unsigned long long m = __ballot(s == ls);
         if (s == ls) rank = __popcll(m & lanemask_lt64());
         if (lane == leader) wcnt[w][ls] = __popcll(m);
@@ -630,10 +618,10 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                     if (!mk) break;
                     const int f = __ffsll((long long)mk) - 1;
                     last = f;
-                    const int indf = __shfl(ind, f, WAVE);
+                    const int indf = readlane_i(ind, f);
                     largest++;
                     if (largest > 20) { stop = true; break; }
-                    const int pf = __shfl(nf, f, WAVE), pb = __shfl(nbk, f, WAVE);
+                    const int pf = readlane_i(nf, f), pb = readlane_i(nbk, f);
                     if (lane == 0) {
                         if (largest <= 2) {
                             label[indf - off0] = 2;
@@ -668,7 +656,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                     if (!mk) break;
                     const int f = __ffsll((long long)mk) - 1;
                     last = f;
-                    const int indf = __shfl(ind, f, WAVE);
+                    const int indf = readlane_i(ind, f);
                     if (lane == 0) {
                         label[indf - off0] = -1;
                         line_flat[line * LINE_FLAT_CAP + n_flat] = indf;
@@ -676,7 +664,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                     n_flat++;
                     smallest++;
                     if (smallest >= 4) { stop = true; break; }
-                    const int pf = __shfl(nf, f, WAVE), pb = __shfl(nbk, f, WAVE);
+                    const int pf = readlane_i(nf, f), pb = readlane_i(nbk, f);
                     if (lane == 0) picked[indf - off0] = 1;
                     mark(indf - off0, pf, pb);
                     __threadfence_block();
