@@ -92,8 +92,8 @@ static void allocate(Ctx& C) {
     grid_alloc(C, C.g_corner_last, capLS, 2.5f * 1.025f);   // two-phase 1-NN, k_odom.hip
     grid_alloc(C, C.g_surf_last, N, 2.5f * 1.025f);
     const int layers = std::min(MAXL, std::max(P.scan_line, 1));
-    grid_alloc(C, C.g_corner_win, capLS, 2.5f * 1.025f, layers);   // window search: cells x scan line
-    grid_alloc(C, C.g_surf_win, N, 2.5f * 1.025f, layers);
+    grid_alloc(C, C.g_corner_win, capLS, 2.5f * 1.025f, layers, false, true);   // window search: 2-D cells x scan line
+    grid_alloc(C, C.g_surf_win, N, 2.5f * 1.025f, layers, false, true);
     C.cap_factors = capLS + N;
     C.d_factors = (aloam_factor*)dalloc(C, sizeof(aloam_factor) * C.cap_factors);
     C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);

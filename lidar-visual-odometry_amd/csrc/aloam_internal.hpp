@@ -44,6 +44,7 @@ struct Grid {
     int* pcell = nullptr;          // cell of each input point
     int nlayers = 1;
     bool w_index = false;          // sorted copy carries the original index in w (search-only grids)
+    bool flat = false;             // one z cell (2-D cells per layer: a scan line is a thin cone)
     int cap = 0;
     float min_cell = 1.f;
 };
@@ -239,7 +240,7 @@ struct GridBuild { Grid* g; const float4* pts; const int* d_n; int cap_n; const 
 void grid_build_multi(Ctx& C, const GridBuild* b, int n);   // up to 4 grids in one set of launches
 void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2,
                        unsigned long long* cand);
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false);
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);
 void odom_compose(Ctx& C);

@@ -16,7 +16,7 @@ namespace aloam {
 
 constexpr int GB = 256;
 
-__device__ inline void grid_params(const unsigned bb[6], float min_cell, int nlayers, GridDesc* d) {
+__device__ inline void grid_params(const unsigned bb[6], float min_cell, int nlayers, int flat, GridDesc* d) {
     float mn[3], mx[3];
     for (int a = 0; a < 3; a++) { mn[a] = ord2f(bb[a]); mx[a] = ord2f(bb[3 + a]); }
     float cell = min_cell;
@@ -26,7 +26,7 @@ __device__ inline void grid_params(const unsigned bb[6], float min_cell, int nla
         for (int a = 0; a < 3; a++) {
             float ext = mx[a] - mn[a];
             if (!(ext >= 0.f)) ext = 0.f;
-            dims[a] = (int)(ext / cell) + 2;
+            dims[a] = (a == 2 && flat) ? 1 : (int)(ext / cell) + 2;
             prod *= dims[a];
         }
         if (prod <= GRID_MAX_CELLS) break;
@@ -44,6 +44,21 @@ __device__ inline int cell_coord(float v, float o, float inv) { return (int)floo
 __global__ void k_grid_init(GridDesc* d) {
     if (threadIdx.x < 6) d->bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     if (threadIdx.x == 0) { d->n = 0; d->n_acc = 0; d->ncells = 0; }
+}
+
+// Runs of equal cell ids among consecutive lanes (input clouds come line by line, so neighbours
+// mostly share a cell): one atomic per run instead of per point — same-address atomics serialise
+// at L2. Returns each lane's run length (valid at the head) and its run head lane. c < 0 = none.
+__device__ __forceinline__ void cell_runs(int c, int* len, int* head) {
+    const int lane = lane_id();
+    const int prev = __builtin_amdgcn_update_dpp(-2, c, 0x138, 0xF, 0xF, false);   // wave_shr:1 (lane - 1)
+    const bool hd = c >= 0 && (lane == 0 || prev != c);
+    const unsigned long long heads = __ballot(hd), brk = __ballot(hd || c < 0);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int h = 63 - __clzll(heads & upto | 1ull);                 // my run's head (0 if none)
+    const unsigned long long above = brk & ~(lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    *len = (above ? __ffsll((long long)above) - 1 : WAVE) - lane;   // at a head: distance to next break
+    *head = h;
 }
 
 __device__ inline bool grid_include(int i, const int* cube_of, const unsigned char* cube_valid) {
@@ -120,8 +135,9 @@ __device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, c
 }
 
 
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_index) {
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_index, bool flat) {
     g.cap = cap;
+    g.flat = flat;
     g.min_cell = min_cell;
     g.nlayers = nlayers;
     g.w_index = w_index;
@@ -148,7 +164,7 @@ void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, c
 struct GridJob {
     GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx; int* pcell;
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
-    float min_cell; int nlayers; int w_index;
+    float min_cell; int nlayers; int w_index; int flat;
 };
 struct GridJobs { GridJob j[4]; };
 
@@ -182,7 +198,7 @@ __global__ void k_gm_count(GridJobs J) {
     if (threadIdx.x == 0) {
         unsigned bb[6];
         for (int a = 0; a < 6; a++) bb[a] = g.desc->bb[a];
-        grid_params(bb, g.min_cell, g.nlayers, &gd);
+        grid_params(bb, g.min_cell, g.nlayers, g.flat, &gd);
         if (blockIdx.x == 0) {
             GridDesc* d = g.desc;
             d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
@@ -191,16 +207,22 @@ __global__ void k_gm_count(GridJobs J) {
     }
     __syncthreads();
     const int n = *g.d_n;
-    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
-        if (!grid_include(i, g.cube_of, g.cube_valid)) { g.pcell[i] = -1; continue; }
-        float4 p = g.pts[i];
-        int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
-        int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
-        int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
-        const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
-        int c = ((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx;
-        g.pcell[i] = c;
-        atomicAdd(&g.cell_count[c], 1);
+    // whole waves iterate together (the run aggregation below needs every lane in the ballot)
+    for (int i0 = blockIdx.x * GB + (threadIdx.x & ~(WAVE - 1)); i0 < n; i0 += gridDim.x * GB) {
+        const int i = i0 + lane_id();
+        int c = -1;
+        if (i < n && grid_include(i, g.cube_of, g.cube_valid)) {
+            const float4 p = g.pts[i];
+            const int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
+            const int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
+            const int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
+            const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
+            c = ((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx;
+        }
+        if (i < n) g.pcell[i] = c;
+        int len, h;
+        cell_runs(c, &len, &h);
+        if (c >= 0 && h == lane_id()) atomicAdd(&g.cell_count[c], len);
     }
 }
 __global__ void k_gm_scan1(GridJobs J) {
@@ -220,11 +242,17 @@ __global__ void k_gm_scan3(GridJobs J) {
 __global__ void k_gm_scatter(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
     const int n = *g.d_n;
-    for (int i = blockIdx.x * GB + threadIdx.x; i < n; i += gridDim.x * GB) {
-        int c = g.pcell[i];
+    for (int i0 = blockIdx.x * GB + (threadIdx.x & ~(WAVE - 1)); i0 < n; i0 += gridDim.x * GB) {
+        const int i = i0 + lane_id();
+        const int c = i < n ? g.pcell[i] : -1;
+        int len, h;
+        cell_runs(c, &len, &h);
+        // the run head claims len slots at the top of the cell's remaining range; members take theirs
+        int left = 0;
+        if (c >= 0 && h == lane_id()) left = atomicSub(&g.cell_count[c], len);
+        left = __shfl(left, h, WAVE) - (lane_id() - h);
         if (c < 0) continue;
-        const int left = atomicSub(&g.cell_count[c], 1);
-        int pos = g.cell_start[c] + left - 1;
+        const int pos = g.cell_start[c] + left - 1;
         if (left <= 0 || pos >= g.cell_start[c + 1]) continue;     // defensive: never write outside the cell
         const float4 p = g.pts[i];
         g.spts[pos] = g.w_index ? make_float4(p.x, p.y, p.z, __int_as_float(i)) : p;
@@ -247,7 +275,8 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     for (int k = 0; k < nj; k++) {
         const Grid& g = *b[k].g;
         J.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell,
-                         b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0};
+                         b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0,
+                         g.flat ? 1 : 0};
         cap = std::max(cap, b[k].cap_n);
     }
     const int nb = std::max(1, std::min(1024, (cap + GB - 1) / GB));

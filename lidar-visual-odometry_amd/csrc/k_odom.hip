@@ -131,43 +131,31 @@ __device__ inline void window_search(const float4* __restrict__ cl, int n, int c
 // built line by line: laserOdometry.cpp:627-641 takes scanRegistration's per-line output), the
 // scan from `closest` visits exactly: forward = {j > closest, line in [c, c+2]}, backward =
 // {j < closest, line in [c-2, c]} (the break fires at the first line outside). Only points with
-// d^2 < 25 can win (the running minimum starts at 25), and those lie in the 5x5x5 block of 2.56 m
-// cells. Per set, the first occurrence of the minimum in scan order is the (d^2, j) minimum going
+// d^2 < 25 can win (the running minimum starts at 25), and those lie in the 5x5 (x, y) block of
+// 2.56 m cells of their line's layer. Per set, the first occurrence of the minimum in scan order is the (d^2, j) minimum going
 // forward and the (d^2, -j) minimum going backward; backward replaces forward only when strictly
 // closer — the serial loop's result, without walking whole scan lines.
-// Rows of the scan-line-layered grid for the lines lo..hi around the query (5 z x 5 y rows of
-// 5 x-cells per line, <= 125 rows): lane r owns rows r and r + 64; two wave prefix sums.
+// Rows of the scan-line-layered grid (2-D cells per line: one z cell, a scan line being a thin
+// cone) for the lines lo..hi around the query: per line 5 y-rows of the x-cells cx-2..cx+2, so the
+// rows hold every point of those lines within the 2 cells (>= 5.1 m) of the query in x and y — a
+// superset of the d < 5 m candidates. <= 25 rows, one lane each, one round trip.
 __device__ __forceinline__ int build_rows_layers(const GridDesc& gd, const int* __restrict__ start, float qx, float qy,
-                                                 float qz, int lo, int hi, int skip, RowSet<128>& rs) {
+                                                 int lo, int hi, int skip, RowSet<32>& rs) {
     const int lane = lane_id();
-    const int cx = (int)floorf((qx - gd.ox) * gd.inv_cell), cy = (int)floorf((qy - gd.oy) * gd.inv_cell),
-              cz = (int)floorf((qz - gd.oz) * gd.inv_cell);
+    const int cx = (int)floorf((qx - gd.ox) * gd.inv_cell), cy = (int)floorf((qy - gd.oy) * gd.inv_cell);
     const int x0 = max(cx - 2, 0), x1 = min(cx + 2, gd.dx - 1);
-    const int nrow = (hi - lo + 1) * 25;
-    int b[2], len[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int r = lane + h * WAVE;
-        b[h] = 0; len[h] = 0;
-        if (r < nrow) {
-            const int L = lo + r / 25, rr = r % 25;
-            const int y = cy - 2 + rr % 5, z = cz - 2 + rr / 5;
-            if (L != skip && L >= 0 && L < gd.nlayers && x0 <= x1 && y >= 0 && y < gd.dy && z >= 0 && z < gd.dz) {
-                const int c = ((L * gd.dz + z) * gd.dy + y) * gd.dx;
-                b[h] = start[c + x0];
-                len[h] = start[c + x1 + 1] - b[h];
-            }
-        }
-    }
-    int inc0 = wave_incl_scan(len[0]), inc1 = wave_incl_scan(len[1]);
-    const int t0 = readlane_i(inc0, WAVE - 1);
-    inc1 += t0;
-    const int nr = min(nrow, 128);
+    const int nrow = (hi - lo + 1) * 5;
+    const int L = lo + lane / 5, y = cy - 2 + lane % 5;
+    const bool ok = lane < nrow && L != skip && L >= 0 && L < gd.nlayers && x0 <= x1 && y >= 0 && y < gd.dy;
+    const int c = (L * gd.dz * gd.dy + y) * gd.dx;
+    const int bb = load_or(start, c + x0, ok, 0);
+    const int len = load_or(start, c + x1 + 1, ok, 0) - bb;
+    const int inc = wave_incl_scan(len);
+    const int nr = min(nrow, 32);
     __builtin_amdgcn_wave_barrier();
-    if (lane < nr) { rs.b[lane] = b[0]; rs.pre[lane + 1] = inc0; }
-    if (lane + WAVE < nr) { rs.b[lane + WAVE] = b[1]; rs.pre[lane + WAVE + 1] = inc1; }
+    if (lane < nr) { rs.b[lane] = bb; rs.pre[lane + 1] = inc; }
     if (lane == 0) { rs.pre[0] = 0; rs.nr = nr; }
-    const int total = nr > WAVE ? readlane_i(inc1, nr - WAVE - 1) : readlane_i(inc0, nr - 1);
+    const int total = readlane_i(inc, nr - 1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -179,15 +167,15 @@ __device__ __forceinline__ int build_rows_layers(const GridDesc& gd, const int* 
 // per-line output), the serial scan from `closest` visits exactly: forward = {j > closest, line
 // in [c, c+2]}, backward = {j < closest, line in [c-2, c]} (its break fires at the first line
 // outside). Only points with d^2 < 25 can win (the running minimum starts at 25), and those lie in
-// the 5x5x5 block of >= 2.56 m cells of their own line's layer. Per set, the first occurrence of
+// the 5x5 (x, y) block of >= 2.56 m cells of their own line's layer. Per set, the first occurrence of
 // the minimum in scan order is the (d^2, j) minimum going forward and the (d^2, -j) minimum going
 // backward; backward replaces forward only when strictly closer — the serial loop's result.
 template <int MODE>
 __device__ inline void grid_window(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
                                    const int* __restrict__ sidx, int closest, int cid, float sx, float sy, float sz,
-                                   int* ind2, int* ind3, RowSet<128>& rs) {
+                                   int* ind2, int* ind3, RowSet<32>& rs) {
     const int lane = lane_id();
-    const int total = build_rows_layers(gd, start, sx, sy, sz, cid - 2, cid + 2, MODE == 0 ? cid : -1000, rs);
+    const int total = build_rows_layers(gd, start, sx, sy, cid - 2, cid + 2, MODE == 0 ? cid : -1000, rs);
     // sets: 0 = fwd ind2, 1 = bwd ind2, 2 = fwd ind3, 3 = bwd ind3 (corner: ind2 sets only)
     unsigned long long k[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
@@ -197,9 +185,10 @@ __device__ inline void grid_window(const GridDesc& gd, const int* __restrict__ s
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int t = t0 + u * WAVE + lane;
-            pp[u] = t < total ? row_pos<128>(rs, t) : -1;
-            vv[u] = pp[u] >= 0 ? spts[pp[u]] : make_float4(0, 0, 0, 0);
-            jj[u] = pp[u] >= 0 ? sidx[pp[u]] : 0;
+            const int pos = row_pos<32>(rs, min(t, total - 1));
+            pp[u] = t < total ? pos : -1;
+            vv[u] = load_or(spts, pp[u], pp[u] >= 0, make_float4(0, 0, 0, 0));
+            jj[u] = load_or(sidx, pp[u], pp[u] >= 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -252,7 +241,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
     const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
     const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s,
-    RowSet<9>& r9, RowSet<25>& r25, RowSet<128>& r128, int exp) {
+    RowSet<9>& r9, RowSet<25>& r25, RowSet<32>& r32, int exp) {
     const int lane = lane_id();
     const bool is_corner = qi < n_sharp;
     const float4 pi = is_corner ? sharp[qi] : flat[qi - n_sharp];
@@ -280,7 +269,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
         int i2, i3;
         const bool by_grid = line_sorted[is_corner ? 0 : 1] != 0;
         if (is_corner) {
-            if (by_grid) grid_window<0>(*wdc, ws_c, wp_c, wi_c, closest, cid, sx, sy, sz, &i2, &i3, r128);
+            if (by_grid) grid_window<0>(*wdc, ws_c, wp_c, wi_c, closest, cid, sx, sy, sz, &i2, &i3, r32);
             else window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
             if (i2 >= 0) {
                 const float4 a = cl[closest], b = cl[i2];
@@ -289,7 +278,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
                 f.b[0] = b.x; f.b[1] = b.y; f.b[2] = b.z;
             }
         } else {
-            if (by_grid) grid_window<1>(*wds, ws_s, wp_s, wi_s, closest, cid, sx, sy, sz, &i2, &i3, r128);
+            if (by_grid) grid_window<1>(*wds, ws_s, wp_s, wi_s, closest, cid, sx, sy, sz, &i2, &i3, r32);
             else window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
             if (i2 >= 0 && i3 >= 0) {
                 const float4 pj = cl[closest], pl = cl[i2], pm = cl[i3];
@@ -324,13 +313,13 @@ __global__ void __launch_bounds__(256) k_odom_search(
     int exp) {
     __shared__ RowSet<9> rows9[256 / WAVE];
     __shared__ RowSet<25> rows25[256 / WAVE];
-    __shared__ RowSet<128> rows128[256 / WAVE];
+    __shared__ RowSet<32> rows32[256 / WAVE];
     const int n_sharp = n_q[0], nq = n_q[0] + n_q[1];
     const int n_cl = n_last[0], n_sl = n_last[1];
     const int w = threadIdx.x / WAVE;
     for (int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; qi < nq; qi += gridDim.x * (blockDim.x / WAVE))
         odom_query(qi, n_sharp, sharp, flat, corner_last, n_cl, surf_last, n_sl, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s,
-                   odom, out, round_cnt, line_sorted, wdc, ws_c, wp_c, wi_c, wds, ws_s, wp_s, wi_s, rows9[w], rows25[w], rows128[w],
+                   odom, out, round_cnt, line_sorted, wdc, ws_c, wp_c, wi_c, wds, ws_s, wp_s, wi_s, rows9[w], rows25[w], rows32[w],
                    exp);
 }
 
