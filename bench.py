@@ -49,6 +49,10 @@ def parse():
                     help="frames after the timed region run with HIP-event profiling (stage_ms, roofline_c3)")
     ap.add_argument("--c4-only", action="store_true", help="run only the C4 search section (profiling)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 FETCH_SIZE pass for roofline.traffic")
+    ap.add_argument("--c4-reg-steps", type=int, default=10,
+                    help="timed C4 scan-to-map registrations, queries sharded over all ranks (0 = skip)")
+    ap.add_argument("--c4-reg-only", action="store_true", help="run only the C4 registration section (profiling)")
+    ap.add_argument("--c4-cpu-rounds", type=int, default=2, help="rounds of the oracle C4 registration sample")
     return ap.parse_args()
 
 
@@ -111,6 +115,59 @@ def c4_search(lvo, torch, dev, launches):
             "found5": found}
 
 
+def c4_registration(lvo, torch, dev, dist, rank, world, steps, cpu_rounds):
+    """BASELINE configs[3]: the laserMapping registration (10 rounds of 5-NN + line/plane fits + LM(4),
+    laserMapping.cpp:556-727) of a 128-line sweep (the whole sweep as the surf stack, every 8th point
+    as the corner stack) against a ~2.1M-point local map, query slots sharded over all ranks with one
+    RCCL all-gather of normal-equation records per LM pass. Strong scaling: every
+    registration is the same whole-job unit whatever the world size. Inputs resident in HBM."""
+    cm, sm, cq, sq, x0, x_true = lvo.synth.c4_registration()
+    d_m, d_cq, d_sq = (torch.from_numpy(a).to(dev) for a in (cm, cq, sq))
+    p = lvo.abi.default_params(128)
+    p.max_scan_points, p.max_map_points = 1024, 1024       # the s2m buffers are sized by its own calls
+    ctx = lvo.Context(p, device=dev.index or 0)
+    ctx.s2m_set_map(d_m.data_ptr(), d_m.data_ptr(), len(cm), len(sm))
+    ctx.s2m_set_queries(d_cq.data_ptr(), d_sq.data_ptr(), len(cq), len(sq))
+    lvo.replicas.init_shard(ctx, dist)
+    for _ in range(2):
+        g = ctx.s2m_register(x0)
+    elapsed, g = lvo.replicas.timed_region(lambda: [ctx.s2m_register(x0) for _ in range(steps)][-1], dist=dist,
+                                           sync=torch.cuda.synchronize, device=dev)
+    out = {
+        "config": f"C4: 128-line sweep, corner stack {len(cq)} + surf stack {len(sq)} queries vs "
+                  f"{len(cm)}-point local map (corner = surf map), 10 rounds x LM(4) (BASELINE configs[3])",
+        "value": round(steps / elapsed, 3), "unit": "registrations/s", "n_gpus": world, "steps": steps,
+        "ms_per_registration": round(elapsed / steps * 1e3, 4), "scaling": "strong",
+        "parallelism": f"query slots sharded x{world} ({g['slot_end'] - g['slot_begin']} on rank {rank}), map replicated",
+        "exchange": "RCCL all-gather of 256 x 32 fp64 normal-equation records per LM pass" if world > 1 else "none (1 rank)",
+        "pose_err_m": float(np.linalg.norm(g["x"][4:] - x_true[4:])),
+        "surf_correspondences_last_round": g["surf_num"][-1],
+    }
+    if rank == 0 and world == 1 and cpu_rounds > 0:
+        import oracle_binding as ob
+        pp = lvo.abi.default_params(128)
+        pp.map_rounds = cpu_rounds
+        pp.max_scan_points, pp.max_map_points = 1024, 1024
+        t1 = time.perf_counter()
+        o = ob.s2m_register(pp, cm, sm, cq, sq, x0)
+        t_cpu = time.perf_counter() - t1
+        c2 = lvo.Context(pp, device=dev.index or 0)
+        c2.s2m_set_map(d_m.data_ptr(), d_m.data_ptr(), len(cm), len(sm))
+        c2.s2m_set_queries(d_cq.data_ptr(), d_sq.data_ptr(), len(cq), len(sq))
+        g2 = c2.s2m_register(x0)
+        c2.close()
+        rel = float(np.linalg.norm(g2["x"] - o["x"]) / np.linalg.norm(o["x"]))
+        out["cpu_baseline"] = {
+            "value": round(cpu_rounds / 10.0 / t_cpu, 5), "unit": "registrations/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/liboracle.so, {cpu_rounds} of the 10 rounds (kd-tree builds + 5-NN + fits + LM), "
+                      "scaled to one 10-round registration",
+            "s_per_sample": round(t_cpu, 3)}
+        out["pose_rel_vs_oracle"] = rel
+        out["counts_match_oracle"] = (g2["corner_num"] == o["corner_num"] and g2["surf_num"] == o["surf_num"])
+    ctx.close()
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -126,6 +183,15 @@ def main():
     torch.cuda.set_device(local_rank)
 
     from lvo_amd_loader import lvo
+
+    if args.c4_reg_only:
+        dev = torch.device("cuda", local_rank)
+        r = c4_registration(lvo, torch, dev, dist, rank, world, max(args.c4_reg_steps, 1), 0)
+        if rank == 0:
+            print(json.dumps({"c4_registration": r}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     if args.c4_only:
         dev = torch.device("cuda", local_rank)
@@ -294,6 +360,14 @@ def main():
             "queries_per_s": round(c4["queries"] / (c4["ms"] * 1e-3), 0),
             "found5_frac": round(c4["found5"], 4),
         }
+
+    if args.c4_reg_steps > 0:
+        # collective over all ranks; a failure is reported in the line instead of losing the headline
+        try:
+            result["c4_registration"] = c4_registration(lvo, torch, dev, dist, rank, world, args.c4_reg_steps,
+                                                        0 if args.no_cpu else args.c4_cpu_rounds)
+        except Exception as e:  # noqa: BLE001
+            result["c4_registration"] = {"error": repr(e)}
 
     if rank == 0 and not args.no_cpu:
         import oracle_binding as ob

@@ -241,6 +241,54 @@ typedef struct aloam_timing {
 int aloam_set_profiling(aloam_ctx* ctx, int enable);
 int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);
 
+/* ---- scan-to-map registration, sharded over ranks (BASELINE configs[3]) ----
+ * The registration half of laserMapping::process (src/laserMapping.cpp:556-727: 10 rounds of
+ * pointAssociateToMap + 5-NN within 1 m + line / plane fit + one ceres::Solve) against a local map
+ * the caller supplies, for a corner / surf query stack of any size (the C4 stress set is a whole
+ * 240k-point sweep against a 2M-point map). The query slots (corner stack, then surf stack: the
+ * reference's AddResidualBlock order) are cut into ALOAM_S2M_RECORDS fixed blocks; a rank of a
+ * world of W associates and evaluates the contiguous run of blocks aloam_shard_slot_range() gives
+ * it, and every LM pass exchanges one record of 32 doubles per block (21 JtJ + 6 Jtr + cost +
+ * count + corner / surf correspondences) with an RCCL all-gather over xGMI; every rank reduces the
+ * ALOAM_S2M_RECORDS records in block order and runs the identical LM tail, so the pose is
+ * bit-identical for every world size and no broadcast is needed. The map is replicated (2M points
+ * = 32 MB of HBM per rank). */
+#define ALOAM_S2M_RECORDS 256
+
+typedef struct aloam_s2m_result {
+    double q_w_curr[4];          /* parameters after the last round (laserMapping.cpp:129)   */
+    double t_w_curr[3];
+    int    optimized;            /* 0: map too small, solve skipped (laserMapping.cpp:554)   */
+    int    rounds;
+    int    corner_num[ALOAM_MAX_ROUNDS];   /* correspondences per round, all ranks          */
+    int    surf_num[ALOAM_MAX_ROUNDS];
+    aloam_lm_summary lm[ALOAM_MAX_ROUNDS];
+    int    slot_begin, slot_end; /* this rank's query slots                                 */
+    int    world;
+} aloam_s2m_result;
+
+/* The local map (laserCloudCornerFromMap / laserCloudSurfFromMap, map frame): float4 arrays of
+ * nc / ns points, host memory or, with ALOAM_INPUT_DEVICE, device memory. Builds its search index. */
+int aloam_s2m_set_map(aloam_ctx* ctx, const float* corner, int nc, const float* surf, int ns, int flags);
+/* The query stacks (laserCloudCornerStack / laserCloudSurfStack, body frame, already downsampled;
+ * laserMapping.cpp:542-550). Every rank passes the same full stacks. */
+int aloam_s2m_set_queries(aloam_ctx* ctx, const float* corner, int ncq, const float* surf, int nsq, int flags);
+/* Runs the rounds from x = (qx,qy,qz,qw,tx,ty,tz) in place. With a shard communicator
+ * (aloam_shard_init) this is a collective: every rank calls it with the same x. */
+int aloam_s2m_register(aloam_ctx* ctx, double x[7], aloam_s2m_result* out);
+/* The same registration for `world` contexts driven from one thread (rank r = ctxs[r], one GPU or
+ * several): the record exchange is a peer copy between the contexts' streams instead of RCCL.
+ * out (may be NULL) receives world results. */
+int aloam_s2m_register_group(aloam_ctx** ctxs, int world, double x[7], aloam_s2m_result* out);
+/* RCCL communicator for the exchange (librccl.so.1 is loaded on first use). Rank 0 creates the
+ * 128-byte id, the caller distributes it (e.g. torch.distributed), then every rank calls
+ * aloam_shard_init (collective). world = 1 needs no id: with id NULL there is no exchange, with an
+ * id a one-rank communicator is created and the exchange still goes through RCCL. */
+int aloam_shard_unique_id(unsigned char id[128]);
+int aloam_shard_init(aloam_ctx* ctx, int rank, int world, const unsigned char* id);
+/* [begin, end) query slots of `rank` among n_slots (pure host function, no device needed). */
+int aloam_shard_slot_range(int n_slots, int rank, int world, int* begin, int* end);
+
 #ifdef __cplusplus
 }
 #endif

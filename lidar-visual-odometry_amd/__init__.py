@@ -59,6 +59,16 @@ def _declare(L):
     L.aloam_forward_mapping_input.argtypes = [vp, vp]
     L.aloam_knn_device.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_float, vp, vp]
     L.aloam_forward_features.argtypes = [vp, vp]
+    L.aloam_s2m_set_map.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int]
+    L.aloam_s2m_set_queries.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int]
+    L.aloam_s2m_register.argtypes = [vp, D, C.POINTER(abi.S2MResult)]
+    L.aloam_s2m_register_group.argtypes = [C.POINTER(vp), C.c_int, D, C.POINTER(abi.S2MResult)]
+    L.aloam_shard_unique_id.argtypes = [C.c_char_p]
+    L.aloam_shard_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
+    L.aloam_shard_slot_range.argtypes = [C.c_int, C.c_int, C.c_int, I, I]
+    for name in ("aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
+                 "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range"):
+        getattr(L, name).restype = C.c_int
     for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
                  "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
                  "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
@@ -92,6 +102,8 @@ EXPORTED_SYMBOLS = [
     "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
     "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing",
     "aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features",
+    "aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
+    "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range",
 ]
 
 
@@ -260,6 +272,48 @@ class Context:
         self._check(lib().aloam_knn_device(self.h, C.c_void_p(d_pts), int(n), C.c_void_p(d_queries), int(nq), int(k),
                                            float(radius), C.c_void_p(d_idx), C.c_void_p(d_d2)))
 
+    # ---- scan-to-map registration, sharded over ranks (laserMapping.cpp:556-727; BASELINE configs[3]) ----
+    @staticmethod
+    def _pts_arg(a, n):
+        """(pointer, n, flags) for a float4 cloud: a numpy (n, 4) float32 array, or an int device pointer."""
+        if isinstance(a, int):
+            return C.c_void_p(a), int(n), abi.ALOAM_INPUT_DEVICE
+        a = np.ascontiguousarray(a, np.float32).reshape(-1, 4)
+        return a, len(a), 0
+
+    def s2m_set_map(self, corner, surf, n_corner=None, n_surf=None):
+        """The local map (laserCloudCornerFromMap / SurfFromMap) as host arrays or device pointers."""
+        c, nc, fc = self._pts_arg(corner, n_corner)
+        s, ns, fs = self._pts_arg(surf, n_surf)
+        if fc != fs:
+            raise ALOAMError("corner and surf map must both be host arrays or both device pointers")
+        cp = c if fc else c.ctypes.data_as(C.c_void_p)
+        sp = s if fs else s.ctypes.data_as(C.c_void_p)
+        self._check(lib().aloam_s2m_set_map(self.h, cp, nc, sp, ns, fc))
+
+    def s2m_set_queries(self, corner, surf, n_corner=None, n_surf=None):
+        """The query stacks (laserCloudCornerStack / SurfStack, body frame)."""
+        c, nc, fc = self._pts_arg(corner, n_corner)
+        s, ns, fs = self._pts_arg(surf, n_surf)
+        if fc != fs:
+            raise ALOAMError("corner and surf stacks must both be host arrays or both device pointers")
+        cp = c if fc else c.ctypes.data_as(C.c_void_p)
+        sp = s if fs else s.ctypes.data_as(C.c_void_p)
+        self._check(lib().aloam_s2m_set_queries(self.h, cp, nc, sp, ns, fc))
+
+    def s2m_register(self, x):
+        """10 rounds of association + Solve from x = (qx,qy,qz,qw,tx,ty,tz); collective when sharded."""
+        x = np.array(x, np.float64)
+        r = abi.S2MResult()
+        self._check(lib().aloam_s2m_register(self.h, abi.dptr(x), C.byref(r)))
+        return abi.s2m_to_dict(r)
+
+    def shard_init(self, rank, world, uid=None):
+        """Attach this context to an RCCL communicator of `world` ranks (uid: 128 bytes from rank 0)."""
+        if world > 1 and (uid is None or len(uid) != 128):
+            raise ALOAMError("shard_init needs the 128-byte unique id for world > 1")
+        self._check(lib().aloam_shard_init(self.h, int(rank), int(world), bytes(uid) if uid is not None else None))
+
     def set_profiling(self, on):
         self._check(lib().aloam_set_profiling(self.h, int(on)))
 
@@ -267,6 +321,37 @@ class Context:
         t = abi.Timing()
         self._check(lib().aloam_get_timing(self.h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
+
+
+def s2m_register_group(contexts, x):
+    """aloam_s2m_register_group: ranks = contexts (same map and stacks set on each), exchange by peer
+    copies between their streams. Returns one result dict per rank."""
+    world = len(contexts)
+    arr = (C.c_void_p * world)(*[c.h for c in contexts])
+    x = np.array(x, np.float64)
+    res = (abi.S2MResult * world)()
+    rc = lib().aloam_s2m_register_group(arr, world, abi.dptr(x), res)
+    if rc != 0:
+        raise ALOAMError(f"rc={rc}: {lib().aloam_last_error(contexts[0].h).decode()}")
+    return [abi.s2m_to_dict(res[r]) for r in range(world)]
+
+
+def shard_unique_id():
+    """128-byte RCCL unique id (call on rank 0 only, then distribute)."""
+    buf = C.create_string_buffer(128)
+    rc = lib().aloam_shard_unique_id(buf)
+    if rc != 0:
+        raise ALOAMError(f"aloam_shard_unique_id rc={rc}: {lib().aloam_last_error(None).decode()}")
+    return buf.raw
+
+
+def shard_slot_range(n_slots, rank, world):
+    """[begin, end) query slots of `rank` (the library's own decomposition; no device needed)."""
+    b, e = C.c_int(), C.c_int()
+    rc = lib().aloam_shard_slot_range(int(n_slots), int(rank), int(world), C.byref(b), C.byref(e))
+    if rc != 0:
+        raise ALOAMError(f"aloam_shard_slot_range rc={rc}")
+    return b.value, e.value
 
 
 class Pipeline:

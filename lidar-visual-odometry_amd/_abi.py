@@ -100,6 +100,19 @@ class MapResult(C.Structure):
     ]
 
 
+ALOAM_S2M_RECORDS = 256
+
+
+class S2MResult(C.Structure):
+    _fields_ = [
+        ("q_w_curr", C.c_double * 4), ("t_w_curr", C.c_double * 3),
+        ("optimized", C.c_int), ("rounds", C.c_int),
+        ("corner_num", C.c_int * ALOAM_MAX_ROUNDS), ("surf_num", C.c_int * ALOAM_MAX_ROUNDS),
+        ("lm", LMSummary * ALOAM_MAX_ROUNDS),
+        ("slot_begin", C.c_int), ("slot_end", C.c_int), ("world", C.c_int),
+    ]
+
+
 class Factor(C.Structure):
     _fields_ = [("type", C.c_int), ("pad", C.c_int),
                 ("cp", C.c_double * 3), ("a", C.c_double * 3), ("b", C.c_double * 3)]
@@ -161,4 +174,17 @@ def map_to_dict(r):
         "lm": [(r.lm[i].iterations, r.lm[i].successful_steps, r.lm[i].termination,
                 r.lm[i].num_residual_blocks, r.lm[i].initial_cost, r.lm[i].final_cost) for i in range(n)],
         "map_total_points": r.map_total_points,
+    }
+
+
+def s2m_to_dict(r):
+    n = r.rounds
+    return {
+        "q_w_curr": np.array(r.q_w_curr[:]), "t_w_curr": np.array(r.t_w_curr[:]),
+        "x": np.array(r.q_w_curr[:] + r.t_w_curr[:]),
+        "optimized": r.optimized, "rounds": n,
+        "corner_num": list(r.corner_num[:n]), "surf_num": list(r.surf_num[:n]),
+        "lm": [(r.lm[i].iterations, r.lm[i].successful_steps, r.lm[i].termination,
+                r.lm[i].num_residual_blocks, r.lm[i].initial_cost, r.lm[i].final_cost) for i in range(n)],
+        "slot_begin": r.slot_begin, "slot_end": r.slot_end, "world": r.world,
     }

@@ -486,6 +486,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     for (auto& g : C->graphs) if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
+    s2m_release(*C);
     for (auto& b : C->bufs) (void)hipFree(b.p);
     if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
     if (C->h_out) (void)hipHostFree(C->h_out);
@@ -827,6 +828,56 @@ int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t) {
     if (!t) throw ApiError{ALOAM_E_ARG, "null timing"};
     *t = C.timing;
     API_END
+}
+
+int aloam_s2m_set_map(aloam_ctx* ctx, const float* corner, int nc, const float* surf, int ns, int flags) {
+    API_BEGIN(ctx)
+    if (nc < 0 || ns < 0 || (nc > 0 && !corner) || (ns > 0 && !surf)) throw ApiError{ALOAM_E_ARG, "bad map"};
+    s2m_set_map(C, corner, nc, surf, ns, flags);
+    API_END
+}
+
+int aloam_s2m_set_queries(aloam_ctx* ctx, const float* corner, int ncq, const float* surf, int nsq, int flags) {
+    API_BEGIN(ctx)
+    if (ncq < 0 || nsq < 0 || (ncq > 0 && !corner) || (nsq > 0 && !surf)) throw ApiError{ALOAM_E_ARG, "bad query stacks"};
+    s2m_set_queries(C, corner, ncq, surf, nsq, flags);
+    API_END
+}
+
+int aloam_s2m_register(aloam_ctx* ctx, double x[7], aloam_s2m_result* out) {
+    API_BEGIN(ctx)
+    if (!x) throw ApiError{ALOAM_E_ARG, "null pose"};
+    s2m_register(C, x, out);
+    API_END
+}
+
+int aloam_s2m_register_group(aloam_ctx** ctxs, int world, double x[7], aloam_s2m_result* out) {
+    if (!ctxs || world < 1 || world > ALOAM_S2M_RECORDS || !x) return ALOAM_E_ARG;
+    for (int r = 0; r < world; r++) if (!ctxs[r]) return ALOAM_E_ARG;
+    API_BEGIN(ctxs[0])
+    s2m_register_group((Ctx**)ctxs, world, x, out);
+    API_END
+}
+
+int aloam_shard_unique_id(unsigned char id[128]) {
+    if (!id) return ALOAM_E_ARG;
+    try {
+        shard_unique_id(id);
+    } catch (const ApiError& e) {
+        g_create_err = e.msg;
+        return e.code;
+    }
+    return ALOAM_OK;
+}
+
+int aloam_shard_init(aloam_ctx* ctx, int rank, int world, const unsigned char* id) {
+    API_BEGIN(ctx)
+    shard_init(C, rank, world, id);
+    API_END
+}
+
+int aloam_shard_slot_range(int n_slots, int rank, int world, int* begin, int* end) {
+    return shard_slot_range(n_slots, rank, world, begin, end);
 }
 
 }  // extern "C"

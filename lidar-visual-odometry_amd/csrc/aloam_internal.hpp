@@ -214,6 +214,11 @@ struct Ctx {
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling
     int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
+
+    // ---- scan-to-map registration (k_s2m.hip) and its shard communicator ----
+    struct S2M* s2m = nullptr;       // allocated by the first aloam_s2m_* call
+    int shard_rank = 0, shard_world = 1;
+    void* shard_comm = nullptr;      // ncclComm_t (world > 1)
 };
 
 // error helpers
@@ -262,5 +267,14 @@ void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so f
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
 void map_frame_launch(Ctx& C, aloam_map_result* R);
 void* dalloc(Ctx& C, size_t bytes);
+// scan-to-map registration + shard communicator (k_s2m.hip)
+void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns, int flags);
+void s2m_set_queries(Ctx& C, const float* corner, int ncq, const float* surf, int nsq, int flags);
+void s2m_register(Ctx& C, double* x, aloam_s2m_result* out);
+void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out);
+void s2m_release(Ctx& C);
+void shard_unique_id(unsigned char* id);
+void shard_init(Ctx& C, int rank, int world, const unsigned char* id);
+int shard_slot_range(int n_slots, int rank, int world, int* begin, int* end);
 
 }  // namespace aloam

@@ -571,6 +571,87 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
     HIPCHK(hipGetLastError());
 }
 
+// ---- scan-to-map registration across ranks (aloam_s2m_*) ----------------------------
+// A Solve is max_iter + 1 passes of {k_s2m_partials -> record exchange -> k_s2m_tail}. The slots are
+// cut into nrec fixed blocks of `per` slots; a rank's partials launch covers its run of blocks, one
+// workgroup per block, and writes one S2M_REC-double record per block (the block's 29 normal-equation
+// sums in the fixed block_reduce_acc order + its corner / surf correspondence counts). After the
+// exchange every rank holds all nrec records in block order; k_s2m_tail reduces them with the same
+// fixed-order reduce_rows and runs the LM tail on the LMState in HBM, so every rank computes the
+// bitwise-identical step whatever the world size. A pass after termination is a no-op on every rank.
+constexpr int S2M_REC = 32;
+static_assert(ALOAM_S2M_RECORDS * NACC * 8 <= 64 * 1024, "tail records must fit in LDS");
+
+__global__ void __launch_bounds__(CB) k_s2m_partials(const aloam_factor* __restrict__ f, int nslots, int per, int rec0, int nrec,
+                                                     const LMState* __restrict__ st, const double* __restrict__ x, int pass,
+                                                     double* __restrict__ send) {
+    __shared__ double rows[CB / 4 * NACC];
+    __shared__ double part8[8 * NACC];
+    __shared__ double tot[NACC];
+    __shared__ int cnt[2];
+    double* rec = send + (size_t)blockIdx.x * S2M_REC;
+    const int g = rec0 + blockIdx.x;
+    if ((pass > 0 && st->done) || g >= nrec) {          // uniform: the same state on every rank
+        if (threadIdx.x < S2M_REC) rec[threadIdx.x] = 0.0;
+        return;
+    }
+    const double* xs = pass == 0 ? x : st->cand;
+    const dquat q{xs[0], xs[1], xs[2], xs[3]};
+    const double t[3] = {xs[4], xs[5], xs[6]};
+    if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+    double acc[NACC];
+#pragma unroll
+    for (int i = 0; i < NACC; i++) acc[i] = 0;
+    int ne = 0, np = 0;
+    const int f0 = g * per, f1 = min(nslots, f0 + per);
+    for (int i = f0 + threadIdx.x; i < f1; i += CB) {
+        const aloam_factor fi = f[i];
+        ne += fi.type == 0;
+        np += fi.type == 1 || fi.type == 2;
+        accumulate(fi, q, t, acc);
+    }
+    __syncthreads();
+    const int se = wave_sum_i(ne), sp = wave_sum_i(np);
+    if ((threadIdx.x & 63) == 0 && (se | sp)) { atomicAdd(&cnt[0], se); atomicAdd(&cnt[1], sp); }
+    block_reduce_acc<CB>(acc, rows, part8, tot);
+    if (threadIdx.x < NACC) rec[threadIdx.x] = tot[threadIdx.x];
+    if (threadIdx.x == 0) { rec[NACC] = cnt[0]; rec[NACC + 1] = cnt[1]; rec[NACC + 2] = 0.0; }
+}
+
+__global__ void __launch_bounds__(CB) k_s2m_tail(const double* __restrict__ recs, int nrec, LMState* st, double* x, int pass,
+                                                 aloam_lm_summary* out, int max_iter, int* round_cnt) {
+    __shared__ double rows[ALOAM_S2M_RECORDS * NACC];
+    __shared__ double part8[8 * NACC];
+    __shared__ double tot[NACC];
+    if (pass > 0 && st->done) return;
+    for (int i = threadIdx.x; i < nrec * NACC; i += CB) {
+        const int b = i / NACC, c = i - b * NACC;
+        rows[i] = recs[(size_t)b * S2M_REC + c];
+    }
+    if (pass == 0 && round_cnt && threadIdx.x < 2) {
+        int s = 0;
+        for (int b = 0; b < nrec; b++) s += (int)recs[(size_t)b * S2M_REC + NACC + threadIdx.x];
+        round_cnt[threadIdx.x] = s;
+    }
+    __syncthreads();
+    reduce_rows(rows, nrec, part8, tot);
+    if (threadIdx.x == 0) {
+        LMState L = *st;
+        lm_tail(&L, tot, pass, x, out, max_iter);
+        *st = L;
+    }
+}
+
+void s2m_partials_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const LMState* st,
+                         const double* x, int pass, double* send) {
+    k_s2m_partials<<<nrec_local, CB, 0, C.stream>>>(f, nslots, per, rec0, nrec, st, x, pass, send);
+    HIPCHK(hipGetLastError());
+}
+void s2m_tail_launch(Ctx& C, const double* recs, int nrec, LMState* st, double* x, int pass, aloam_lm_summary* out, int* round_cnt) {
+    k_s2m_tail<<<1, CB, 0, C.stream>>>(recs, nrec, st, x, pass, out, std::min(C.P.max_solver_iterations, 200), round_cnt);
+    HIPCHK(hipGetLastError());
+}
+
 // ---- test entry: per-factor residuals / Jacobians and the normal equations ----
 __global__ void k_eval_factors(const aloam_factor* __restrict__ f, int n, const double* x, int robust, double* res,
                                double* jac, double* neq) {

@@ -164,27 +164,21 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
 // aggregated per wave before the atomics.
 constexpr int AG = 8;     // lanes per query (measured best of 4 / 8 / 16 at C3)
 constexpr int ASSOC_BLOCKS = 512;   // fixed launch (graph-replayable); waves stride over the stacks
-__global__ void __launch_bounds__(256) k_map_assoc(
-    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n,
+// slots [s0, s1) of the compact slot space (corner stack at [0, nc), surf stack at [nc, nc + ns) — the
+// reference's AddResidualBlock order), pose `par` (laserMapping.cpp:129 parameters)
+__device__ __forceinline__ void assoc_slots(
+    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int nc, const int s0, const int s1, const double* par,
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp) {
-    __shared__ int tabs[256 / AG][20];
-    // slots are compact: corner stack at [0, nc), surf stack at [nc, nc + ns) — the reference's
-    // AddResidualBlock order; the solver reads nc + ns from the device
-    if (!m->optimize) return;
-    const int nc = stack_n[0], ns = stack_n[1];
-    double par[7];
-#pragma unroll
-    for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
+    aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp, int (*tabs)[20]) {
     const bool lead = (lane_id() & (AG - 1)) == 0;
     const int per_wave = WAVE / AG;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
     int cnt_c = 0, cnt_s = 0;
     unsigned long long ncand_sum = 0;
-    for (int base = wave * per_wave; base < nc + ns; base += nwaves * per_wave) {   // wave-uniform trip count
+    for (int base = s0 + wave * per_wave; base < s1; base += nwaves * per_wave) {   // wave-uniform trip count
         const int qi = base + (lane_id() / AG);
-        const bool live = qi < nc + ns;
+        const bool live = qi < s1;
         const bool corner = qi < nc;
         const int li = corner ? qi : qi - nc;
         const float4 po = live ? (corner ? cstack[li] : sstack[li]) : make_float4(0, 0, 0, 0);
@@ -208,15 +202,56 @@ __global__ void __launch_bounds__(256) k_map_assoc(
         }
     }
     // wave-aggregated counters
-    const int tc = wave_sum_i(cnt_c), ts = wave_sum_i(cnt_s);
-    if (lane_id() == 0) {
-        if (tc) atomicAdd(&round_cnt[0], tc);
-        if (ts) atomicAdd(&round_cnt[1], ts);
+    if (round_cnt) {
+        const int tc = wave_sum_i(cnt_c), ts = wave_sum_i(cnt_s);
+        if (lane_id() == 0) {
+            if (tc) atomicAdd(&round_cnt[0], tc);
+            if (ts) atomicAdd(&round_cnt[1], ts);
+        }
     }
     if (cand_count) {
         const int t = wave_sum_i((int)ncand_sum);
         if (lane_id() == 0 && t) atomicAdd(cand_count, (unsigned long long)t);
     }
+}
+
+__global__ void __launch_bounds__(256) k_map_assoc(
+    const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n,
+    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
+    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
+    const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp) {
+    __shared__ int tabs[256 / AG][20];
+    // the solver reads nc + ns from the device
+    if (!m->optimize) return;
+    const int nc = stack_n[0], ns = stack_n[1];
+    double par[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
+    assoc_slots(cstack, sstack, nc, 0, nc + ns, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, round_cnt, cand_count,
+                exp, tabs);
+}
+
+// Scan-to-map registration (aloam_s2m_*): one rank's slots [s0, s1) of the stacks at pose x.
+__global__ void __launch_bounds__(256) k_s2m_assoc(
+    const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc, int s0, int s1, const double* __restrict__ x,
+    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
+    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
+    aloam_factor* __restrict__ out, unsigned long long* cand_count) {
+    __shared__ int tabs[256 / AG][20];
+    double par[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) par[i] = x[i];
+    assoc_slots(cstack, sstack, nc, s0, s1, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, nullptr, cand_count, 0, tabs);
+}
+
+void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
+                      aloam_factor* out, unsigned long long* cand) {
+    if (s1 <= s0) return;
+    const int waves = (s1 - s0 + WAVE / AG - 1) / (WAVE / AG);
+    const int blocks = std::max(1, std::min(4096, (waves + 3) / 4));
+    k_s2m_assoc<<<blocks, 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, gc.desc, gc.cell_start, gc.pts, gc.idx, gs.desc,
+                                                gs.cell_start, gs.pts, gs.idx, out, cand);
+    HIPCHK(hipGetLastError());
 }
 
 __global__ void k_map_invalidate(aloam_factor* out, int n) {

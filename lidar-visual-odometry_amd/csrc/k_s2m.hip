@@ -1,0 +1,342 @@
+// k_s2m.hip — scan-to-map registration with the query stacks sharded over ranks (host side).
+//
+// The registration half of laserMapping::process (src/laserMapping.cpp:556-727) against a map the
+// caller supplies: per round, k_s2m_assoc (k_map.hip: pointAssociateToMap + 5-NN within 1 m + line /
+// plane fit, 8 lanes per query) over this rank's slots, then one Ceres-equivalent Solve as
+// max_iter + 1 passes of {k_s2m_partials -> exchange -> k_s2m_tail} (k_lm.hip). The exchange is the
+// only collective of the path: one 32-double record per fixed slot block,
+//   * world 1:   none (the tail reads the local records),
+//   * RCCL:      ncclAllGather on the context's stream (one process per GPU, xGMI),
+//   * group:     peer copies between the streams of contexts driven by one thread
+//                (aloam_s2m_register_group: several ranks on one GPU, or one process over several).
+// Because the block decomposition and the reduction order are global, every rank, in every mode and
+// world size, runs the bitwise-identical LM tail.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "aloam_internal.hpp"
+
+namespace aloam {
+
+void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
+                      aloam_factor* out, unsigned long long* cand);
+void s2m_partials_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const LMState* st,
+                         const double* x, int pass, double* send);
+void s2m_tail_launch(Ctx& C, const double* recs, int nrec, LMState* st, double* x, int pass, aloam_lm_summary* out, int* round_cnt);
+
+constexpr int S2M_REC = 32;                     // doubles per record (k_lm.hip)
+constexpr int NREC = ALOAM_S2M_RECORDS;
+constexpr int RECV_CAP = 2 * NREC;              // world * ceil(NREC / world) <= 2 NREC
+
+struct S2MOut {
+    aloam_lm_summary lm[ALOAM_MAX_ROUNDS];
+    int cnt[ALOAM_MAX_ROUNDS][2];
+};
+
+struct S2M {
+    int nc = 0, ns = 0, nqc = 0, nqs = 0;
+    int cap_mc = 0, cap_ms = 0, cap_qc = 0, cap_qs = 0, cap_f = 0;
+    float4 *d_mc = nullptr, *d_ms = nullptr, *d_qc = nullptr, *d_qs = nullptr;
+    int* d_n = nullptr;                         // [2] map sizes (grid builds read them on the device)
+    Grid gc, gs;
+    aloam_factor* d_f = nullptr;
+    LMState* d_st = nullptr;
+    double* d_x = nullptr;                      // [8] parameters (laserMapping.cpp:129)
+    double* d_send = nullptr;                   // 2 x NREC records (pass parity: group-mode reuse guard)
+    double* d_recv = nullptr;                   // RECV_CAP records
+    S2MOut* d_out = nullptr;
+    S2MOut* h_out = nullptr;                    // pinned
+    hipEvent_t ev[2] = {nullptr, nullptr};      // group mode: records of this rank ready (per parity)
+    bool have_map = false, have_q = false;
+};
+
+// ---- RCCL, loaded on first use (in a torch process this resolves to the librccl.so.1 torch loaded) ----
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string err;
+};
+static Rccl* rccl() {
+    static Rccl r;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) { r.err = std::string("cannot load librccl.so.1: ") + dlerror(); return nullptr; }
+        r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy || !r.error_string) {
+            r.err = "librccl.so.1 lacks the nccl* entry points";
+            r.get_unique_id = nullptr;
+        }
+    }
+    return r.get_unique_id ? &r : nullptr;
+}
+static void rcclchk(ncclResult_t e, const char* what) {
+    if (e != ncclSuccess) throw ApiError{ALOAM_E_HIP, std::string(what) + ": " + rccl()->error_string(e)};
+}
+
+// ---- slot decomposition ----
+struct Slice { int per, rp, rec0, rec1, s0, s1; };
+static Slice slice_of(int n_slots, int rank, int world) {
+    Slice s;
+    s.per = std::max(1, (n_slots + NREC - 1) / NREC);       // slots per record block
+    s.rp = (NREC + world - 1) / world;                       // record blocks per rank (the last rank may get fewer)
+    s.rec0 = std::min(NREC, rank * s.rp);
+    s.rec1 = std::min(NREC, s.rec0 + s.rp);
+    s.s0 = std::min(n_slots, s.rec0 * s.per);
+    s.s1 = std::min(n_slots, s.rec1 * s.per);
+    return s;
+}
+
+static S2M& s2m_of(Ctx& C) {
+    if (!C.s2m) {
+        S2M* S = new S2M();
+        C.s2m = S;
+        S->d_n = (int*)dalloc(C, sizeof(int) * 2);
+        S->d_st = (LMState*)dalloc(C, sizeof(LMState));
+        S->d_x = (double*)dalloc(C, sizeof(double) * 8);
+        S->d_send = (double*)dalloc(C, sizeof(double) * 2 * NREC * S2M_REC);
+        S->d_recv = (double*)dalloc(C, sizeof(double) * RECV_CAP * S2M_REC);
+        S->d_out = (S2MOut*)dalloc(C, sizeof(S2MOut));
+        HIPCHK(hipHostMalloc((void**)&S->h_out, sizeof(S2MOut), hipHostMallocDefault));
+        for (auto& e : S->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipMemsetAsync(S->d_recv, 0, sizeof(double) * RECV_CAP * S2M_REC, C.stream));
+    }
+    return *C.s2m;
+}
+
+void s2m_release(Ctx& C) {   // device buffers belong to C.bufs; the rest is released here
+    if (C.shard_comm && rccl()) (void)rccl()->comm_destroy((ncclComm_t)C.shard_comm);
+    C.shard_comm = nullptr;
+    if (!C.s2m) return;
+    for (auto& e : C.s2m->ev) if (e) (void)hipEventDestroy(e);
+    if (C.s2m->h_out) (void)hipHostFree(C.s2m->h_out);
+    delete C.s2m;
+    C.s2m = nullptr;
+}
+
+static void copy_in(Ctx& C, float4* dst, const float* src, int n, int flags) {
+    if (n > 0)
+        HIPCHK(hipMemcpyAsync(dst, src, sizeof(float4) * (size_t)n,
+                              (flags & ALOAM_INPUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, C.stream));
+}
+static float4* grow(Ctx& C, float4* p, int& cap, int n) {   // old buffers stay with the context until destroy
+    if (n <= cap) return p;
+    cap = std::max(n, 2 * cap);
+    return (float4*)dalloc(C, sizeof(float4) * (size_t)cap);
+}
+
+void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns, int flags) {
+    S2M& S = s2m_of(C);
+    S.d_mc = grow(C, S.d_mc, S.cap_mc, std::max(nc, 1));
+    S.d_ms = grow(C, S.d_ms, S.cap_ms, std::max(ns, 1));
+    copy_in(C, S.d_mc, corner, nc, flags);
+    copy_in(C, S.d_ms, surf, ns, flags);
+    // FromMap indices: 1.025 m cells (5-NN within 1 m: the 27-cell block holds the ball), sorted copies
+    if (S.gc.cap < std::max(nc, 1)) { Grid g{}; grid_alloc(C, g, std::max(std::max(nc, 1), 2 * S.gc.cap), 1.0f * 1.025f, 1, true); S.gc = g; }
+    if (S.gs.cap < std::max(ns, 1)) { Grid g{}; grid_alloc(C, g, std::max(std::max(ns, 1), 2 * S.gs.cap), 1.0f * 1.025f, 1, true); S.gs = g; }
+    set_counts2(C, S.d_n, nc, ns);
+    const GridBuild gb[2] = {{&S.gc, S.d_mc, S.d_n + 0, std::max(nc, 1), nullptr, nullptr},
+                             {&S.gs, S.d_ms, S.d_n + 1, std::max(ns, 1), nullptr, nullptr}};
+    grid_build_multi(C, gb, 2);
+    S.nc = nc;
+    S.ns = ns;
+    S.have_map = true;
+    HIPCHK(hipStreamSynchronize(C.stream));
+}
+
+void s2m_set_queries(Ctx& C, const float* corner, int ncq, const float* surf, int nsq, int flags) {
+    S2M& S = s2m_of(C);
+    S.d_qc = grow(C, S.d_qc, S.cap_qc, std::max(ncq, 1));
+    S.d_qs = grow(C, S.d_qs, S.cap_qs, std::max(nsq, 1));
+    copy_in(C, S.d_qc, corner, ncq, flags);
+    copy_in(C, S.d_qs, surf, nsq, flags);
+    const int q = std::max(ncq + nsq, 1);
+    if (S.cap_f < q) {
+        S.cap_f = std::max(q, 2 * S.cap_f);
+        S.d_f = (aloam_factor*)dalloc(C, sizeof(aloam_factor) * (size_t)S.cap_f);
+    }
+    S.nqc = ncq;
+    S.nqs = nsq;
+    S.have_q = true;
+    HIPCHK(hipStreamSynchronize(C.stream));
+}
+
+static void check_ready(Ctx& C) {
+    if (!C.s2m || !C.s2m->have_map || !C.s2m->have_q) throw ApiError{ALOAM_E_STATE, "aloam_s2m_register before set_map / set_queries"};
+}
+
+// the map gate of laserMapping.cpp:554
+static bool s2m_gate(const S2M& S) { return S.nc > 10 && S.ns > 50; }
+
+static void begin(Ctx& C, const double* x) {
+    S2M& S = *C.s2m;
+    HIPCHK(hipMemsetAsync(S.d_out, 0, sizeof(S2MOut), C.stream));
+    HIPCHK(hipMemcpyAsync(S.d_x, x, sizeof(double) * 7, hipMemcpyHostToDevice, C.stream));
+}
+
+static void finish(Ctx& C, int rank, int world, double* x, aloam_s2m_result* out, bool copy_x) {
+    S2M& S = *C.s2m;
+    double xo[7];
+    HIPCHK(hipMemcpyAsync(xo, S.d_x, sizeof(double) * 7, hipMemcpyDeviceToHost, C.stream));
+    HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, sizeof(S2MOut), hipMemcpyDeviceToHost, C.stream));
+    HIPCHK(hipStreamSynchronize(C.stream));
+    if (copy_x) std::memcpy(x, xo, sizeof(xo));
+    if (!out) return;
+    aloam_s2m_result r{};
+    r.optimized = s2m_gate(S) ? 1 : 0;
+    r.rounds = r.optimized ? std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS) : 0;
+    for (int i = 0; i < r.rounds; i++) {
+        r.corner_num[i] = S.h_out->cnt[i][0];
+        r.surf_num[i] = S.h_out->cnt[i][1];
+        r.lm[i] = S.h_out->lm[i];
+    }
+    for (int k = 0; k < 4; k++) r.q_w_curr[k] = xo[k];
+    for (int k = 0; k < 3; k++) r.t_w_curr[k] = xo[4 + k];
+    const Slice sl = slice_of(S.nqc + S.nqs, rank, world);
+    r.slot_begin = sl.s0;
+    r.slot_end = sl.s1;
+    r.world = world;
+    *out = r;
+}
+
+void s2m_register(Ctx& C, double* x, aloam_s2m_result* out) {
+    check_ready(C);
+    S2M& S = *C.s2m;
+    const int world = C.shard_world, rank = C.shard_rank;
+    if (world > 1 && !C.shard_comm) throw ApiError{ALOAM_E_STATE, "shard communicator not initialised"};
+    const bool rccl_exchange = C.shard_comm != nullptr;   // world 1 with a communicator: exercises the RCCL path
+    const int Q = S.nqc + S.nqs;
+    const Slice sl = slice_of(Q, rank, world);
+    begin(C, x);
+    if (s2m_gate(S)) {
+        const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
+        const int max_iter = std::min(C.P.max_solver_iterations, 200);
+        for (int it = 0; it < rounds; it++) {
+            s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.gs, S.d_f, nullptr);
+            for (int pass = 0; pass <= max_iter; pass++) {
+                s2m_partials_launch(C, S.d_f, Q, sl.per, sl.rec0, sl.rp, NREC, S.d_st, S.d_x, pass, S.d_send);
+                const double* recs = S.d_send;
+                if (rccl_exchange) {
+                    rcclchk(rccl()->all_gather(S.d_send, S.d_recv, (size_t)sl.rp * S2M_REC, ncclFloat64, (ncclComm_t)C.shard_comm,
+                                               C.stream), "ncclAllGather");
+                    recs = S.d_recv;
+                }
+                s2m_tail_launch(C, recs, NREC, S.d_st, S.d_x, pass, &S.d_out->lm[it], pass == 0 ? S.d_out->cnt[it] : nullptr);
+            }
+        }
+    }
+    finish(C, rank, world, x, out, true);
+}
+
+void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
+    for (int r = 0; r < world; r++) {
+        HIPCHK(hipSetDevice(cs[r]->device));
+        check_ready(*cs[r]);
+    }
+    S2M& S0 = *cs[0]->s2m;
+    const int Q = S0.nqc + S0.nqs;
+    for (int r = 1; r < world; r++) {
+        const S2M& S = *cs[r]->s2m;
+        if (S.nqc != S0.nqc || S.nqs != S0.nqs || S.nc != S0.nc || S.ns != S0.ns)
+            throw ApiError{ALOAM_E_ARG, "group ranks hold different maps / query stacks"};
+    }
+    for (int r = 0; r < world; r++) { HIPCHK(hipSetDevice(cs[r]->device)); begin(*cs[r], x); }
+    const int rp = slice_of(Q, 0, world).rp;
+    if (s2m_gate(S0)) {
+        const int rounds = std::min(cs[0]->P.map_rounds, ALOAM_MAX_ROUNDS);
+        const int max_iter = std::min(cs[0]->P.max_solver_iterations, 200);
+        int parity = 0;
+        for (int it = 0; it < rounds; it++) {
+            for (int r = 0; r < world; r++) {
+                Ctx& C = *cs[r];
+                S2M& S = *C.s2m;
+                const Slice sl = slice_of(Q, r, world);
+                HIPCHK(hipSetDevice(C.device));
+                s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.gs, S.d_f, nullptr);
+            }
+            for (int pass = 0; pass <= max_iter; pass++, parity ^= 1) {
+                for (int r = 0; r < world; r++) {      // every rank's records of this pass
+                    Ctx& C = *cs[r];
+                    S2M& S = *C.s2m;
+                    const Slice sl = slice_of(Q, r, world);
+                    HIPCHK(hipSetDevice(C.device));
+                    s2m_partials_launch(C, S.d_f, Q, sl.per, sl.rec0, rp, NREC, S.d_st, S.d_x, pass, S.d_send + (size_t)parity * NREC * S2M_REC);
+                    HIPCHK(hipEventRecord(S.ev[parity], C.stream));
+                }
+                for (int r = 0; r < world; r++) {      // all-gather as peer copies into every rank's recv (rank order)
+                    Ctx& C = *cs[r];
+                    HIPCHK(hipSetDevice(C.device));
+                    for (int p = 0; p < world; p++) {
+                        S2M& P = *cs[p]->s2m;
+                        HIPCHK(hipStreamWaitEvent(C.stream, P.ev[parity], 0));
+                        HIPCHK(hipMemcpyAsync(C.s2m->d_recv + (size_t)p * rp * S2M_REC, P.d_send + (size_t)parity * NREC * S2M_REC,
+                                              sizeof(double) * rp * S2M_REC, hipMemcpyDefault, C.stream));
+                    }
+                }
+                // a rank's send[parity] is rewritten two passes later, after its stream waited for every
+                // peer's next-pass records, which those peers recorded after copying this pass's
+                for (int r = 0; r < world; r++) {
+                    Ctx& C = *cs[r];
+                    S2M& S = *C.s2m;
+                    HIPCHK(hipSetDevice(C.device));
+                    s2m_tail_launch(C, S.d_recv, NREC, S.d_st, S.d_x, pass, &S.d_out->lm[it], pass == 0 ? S.d_out->cnt[it] : nullptr);
+                }
+            }
+        }
+    }
+    for (int r = 0; r < world; r++) {
+        HIPCHK(hipSetDevice(cs[r]->device));
+        finish(*cs[r], r, world, x, out ? out + r : nullptr, r == 0);
+    }
+}
+
+void shard_unique_id(unsigned char* id) {
+    Rccl* R = rccl();
+    if (!R) throw ApiError{ALOAM_E_NODEVICE, "RCCL unavailable"};
+    ncclUniqueId u;
+    rcclchk(R->get_unique_id(&u), "ncclGetUniqueId");
+    static_assert(sizeof(u) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(id, &u, sizeof(u));
+}
+
+void shard_init(Ctx& C, int rank, int world, const unsigned char* id) {
+    if (world < 1 || rank < 0 || rank >= world || world > NREC) throw ApiError{ALOAM_E_ARG, "bad rank / world"};
+    if (C.shard_comm) { (void)rccl()->comm_destroy((ncclComm_t)C.shard_comm); C.shard_comm = nullptr; }
+    C.shard_rank = rank;
+    C.shard_world = world;
+    if (!id) {
+        if (world == 1) return;   // no exchange at all
+        throw ApiError{ALOAM_E_ARG, "null unique id"};
+    }
+    Rccl* R = rccl();
+    if (!R) throw ApiError{ALOAM_E_NODEVICE, "RCCL unavailable"};
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclComm_t comm = nullptr;
+    HIPCHK(hipSetDevice(C.device));
+    rcclchk(R->comm_init_rank(&comm, world, u, rank), "ncclCommInitRank");
+    C.shard_comm = comm;
+}
+
+int shard_slot_range(int n_slots, int rank, int world, int* begin, int* end) {
+    if (n_slots < 0 || world < 1 || world > NREC || rank < 0 || rank >= world || !begin || !end) return ALOAM_E_ARG;
+    const Slice s = slice_of(n_slots, rank, world);
+    *begin = s.s0;
+    *end = s.s1;
+    return ALOAM_OK;
+}
+
+}  // namespace aloam

@@ -7,6 +7,10 @@ One process per GPU (torchrun; backend "nccl" = RCCL on the GPU box, "gloo" in C
 * Within one search (C4: one sweep against a large local map) queries are independent given the map:
   shard_range splits them into contiguous (scan-ordered, hence spatially coherent) chunks, map
   replicated, again without a collective.
+* Scan-to-map registration (Context.s2m_register, laserMapping.cpp:556-727) shards its query stacks
+  the same way and has ONE exchange step per LM pass: an RCCL all-gather of fixed-size normal-equation
+  records issued by the library on its own stream (k_s2m.hip). init_shard() creates that communicator
+  from an initialised torch.distributed group (the 128-byte RCCL id travels over it).
 """
 import time
 
@@ -48,3 +52,19 @@ def timed_region(fn, dist=None, sync=None, device=None):
 def aggregate_rate(units_per_rank, world, elapsed):
     """Whole-job throughput: all ranks' units over the max-over-ranks time."""
     return units_per_rank * world / elapsed if elapsed > 0 else 0.0
+
+
+def init_shard(ctx, dist=None, uid_fn=None):
+    """Attach ctx (anything with shard_init(rank, world, uid)) to a communicator spanning the
+    torch.distributed world: rank 0 makes the RCCL unique id (uid_fn, default lvo.shard_unique_id),
+    broadcasts it over the existing process group, every rank then joins (collective)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        ctx.shard_init(0, 1, None)
+        return 0, 1
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if uid_fn is None:
+        from . import shard_unique_id as uid_fn
+    box = [uid_fn() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    ctx.shard_init(rank, world, box[0])
+    return rank, world

@@ -106,3 +106,47 @@ def write_kitti_bin(path, pts):
 
 def read_kitti_bin(path):
     return np.fromfile(path, dtype=np.float32).reshape(-1, 4)
+
+
+def quat_from_rot(R):
+    """Unit quaternion (x, y, z, w) of a rotation matrix (Eigen's Quaternion(Matrix3) branch rule)."""
+    R = np.asarray(R, np.float64)
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    if tr > 0:
+        s = np.sqrt(tr + 1.0)
+        w = 0.5 * s
+        s = 0.5 / s
+        q = [(R[2, 1] - R[1, 2]) * s, (R[0, 2] - R[2, 0]) * s, (R[1, 0] - R[0, 1]) * s, w]
+    else:
+        i = int(np.argmax([R[0, 0], R[1, 1], R[2, 2]]))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0)
+        q = [0.0, 0.0, 0.0, 0.0]
+        q[i] = 0.5 * s
+        s = 0.5 / s
+        q[3] = (R[k, j] - R[j, k]) * s
+        q[j] = (R[j, i] + R[i, j]) * s
+        q[k] = (R[k, i] + R[i, k]) * s
+    return np.array(q)
+
+
+def c4_registration(name="l128", frame=0, half=50.0, map_step=0.107, seed=4, surf_stride=1, corner_stride=8,
+                    dyaw_deg=1.0, dt=(0.3, -0.2, 0.05)):
+    """BASELINE configs[3] registration workload: one sweep (sensor frame) as the query stacks against a
+    dense local map of the scene around the sensor (map frame = scene frame), starting from the true
+    pose perturbed by dyaw_deg of yaw and dt metres. Corner stack = every corner_stride-th point, surf
+    stack = every surf_stride-th point (surf_stride 1: the whole sweep, the C4 stress set); both map
+    kinds are the dense map. Returns (corner_map, surf_map, corner_q, surf_q, x0, x_true)."""
+    R, o = pose(name, frame)
+    m = dense_map(seed, float(o[0]), float(o[1]), half=half, step=map_step)
+    s = scan(name, frame)
+    qt = quat_from_rot(R)
+    x_true = np.concatenate([qt, o])
+    a = np.deg2rad(dyaw_deg) / 2
+    dq = np.array([0.0, 0.0, np.sin(a), np.cos(a)])
+    x, y, z, w = dq
+    X, Y, Z, W = qt
+    q0 = np.array([w * X + x * W + y * Z - z * Y, w * Y - x * Z + y * W + z * X, w * Z + x * Y - y * X + z * W,
+                   w * W - x * X - y * Y - z * Z])
+    x0 = np.concatenate([q0 / np.linalg.norm(q0), o + np.asarray(dt, np.float64)])
+    return m, m, np.ascontiguousarray(s[::corner_stride]), np.ascontiguousarray(s[::surf_stride]), x0, x_true

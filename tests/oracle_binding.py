@@ -55,6 +55,8 @@ def lib():
         L.oracle_voxel_grid.argtypes = [C.POINTER(C.c_float), C.c_int, C.c_float, C.c_int, C.POINTER(abi.Cloud)]
         L.oracle_knn.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float), C.c_int, C.c_int, C.c_float,
                                  C.POINTER(C.c_int), C.POINTER(C.c_float)]
+        L.oracle_s2m_register.argtypes = [C.POINTER(abi.Params)] + [C.POINTER(C.c_float), C.c_int] * 4 + [
+            C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(abi.LMSummary)]
         L.oracle_eigen_sym3.argtypes = [C.POINTER(C.c_double)] * 3
         L.oracle_colpiv_qr_5x3.argtypes = [C.POINTER(C.c_double)] * 3
         L.oracle_introsort_keys.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]
@@ -219,3 +221,22 @@ def introsort_perm(keys, libstdcxx=False):
     fn = lib().oracle_libstdcxx_sort_keys if libstdcxx else lib().oracle_introsort_keys
     fn(abi.fptr(k), len(k), abi.iptr(p))
     return p
+
+
+def s2m_register(params, corner_map, surf_map, corner_q, surf_q, x):
+    """oracle_s2m_register: the laserMapping registration rounds against a given map (kd-tree 5-NN,
+    Eigen line / plane fits, Ceres-style LM). Returns a dict shaped like Context.s2m_register's."""
+    arrs = [np.ascontiguousarray(a, np.float32).reshape(-1, 4) for a in (corner_map, surf_map, corner_q, surf_q)]
+    x = np.array(x, np.float64)
+    res = np.zeros(2 + 2 * abi.ALOAM_MAX_ROUNDS, np.int32)
+    lm_ = (abi.LMSummary * abi.ALOAM_MAX_ROUNDS)()
+    args = []
+    for a in arrs:
+        args += [abi.fptr(a), len(a)]
+    lib().oracle_s2m_register(C.byref(params), *args, abi.dptr(x), abi.iptr(res), lm_)
+    n = int(res[1])
+    return {"x": x, "q_w_curr": x[:4].copy(), "t_w_curr": x[4:].copy(), "optimized": int(res[0]), "rounds": n,
+            "corner_num": [int(v) for v in res[2:2 + n]],
+            "surf_num": [int(v) for v in res[2 + abi.ALOAM_MAX_ROUNDS:2 + abi.ALOAM_MAX_ROUNDS + n]],
+            "lm": [(lm_[i].iterations, lm_[i].successful_steps, lm_[i].termination, lm_[i].num_residual_blocks,
+                    lm_[i].initial_cost, lm_[i].final_cost) for i in range(n)]}
