@@ -241,6 +241,33 @@ typedef struct aloam_timing {
 int aloam_set_profiling(aloam_ctx* ctx, int enable);
 int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);
 
+/* ---- native pipeline: the reference's node split on one GPU ---------------------------------
+ * scanRegistration, laserOdometry and laserMapping run as three ROS processes in the reference, one
+ * hot thread each (scanRegistration.cpp:461-503, laserOdometry.cpp:311, laserMapping.cpp:934). The
+ * pipeline owns one context per stage and one native worker thread per later stage; push() runs the
+ * first stage of scan k on the caller's thread while the workers run the later stages of earlier
+ * scans, and hands data over device to device. stages = 2: [scanRegistration + laserOdometry] ||
+ * [laserMapping]; stages = 3: one stage per node. Every scan passes every stage in order, so the
+ * results equal aloam_process_scan's. */
+typedef struct aloam_pipeline aloam_pipeline;
+aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int stages);
+void            aloam_pipeline_destroy(aloam_pipeline* pl);
+const char*     aloam_pipeline_last_error(const aloam_pipeline* pl);
+/* stage 0 = scanRegistration context, 1 = laserOdometry (== 0 when stages == 2), 2 = laserMapping */
+aloam_ctx*      aloam_pipeline_context(aloam_pipeline* pl, int stage);
+/* Feeds one sweep (flags as aloam_scan_registration). Outputs the odometry result completed in this
+ * step (*have_od: scan k for stages 2, k-1 for stages 3) and the mapping result completed in it
+ * (*have_mp: scan k-1 / k-2). od / mp may be NULL. */
+int aloam_pipeline_push(aloam_pipeline* pl, const float* xyzr, int n, int flags,
+                        aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp);
+/* Drains the pipeline: the odometry result still in flight (stages 3), the mapping job in flight
+ * (mp) and the mapping of that last odometry result (mp2). */
+int aloam_pipeline_flush(aloam_pipeline* pl, aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp,
+                         aloam_map_result* mp2, int* have_mp2);
+/* HIP-event timing of each stage's last completed job (profiling on). */
+int aloam_pipeline_set_profiling(aloam_pipeline* pl, int enable);
+int aloam_pipeline_timing(aloam_pipeline* pl, int stage, aloam_timing* t);
+
 /* ---- scan-to-map registration, sharded over ranks (BASELINE configs[3]) ----
  * The registration half of laserMapping::process (src/laserMapping.cpp:556-727: 10 rounds of
  * pointAssociateToMap + 5-NN within 1 m + line / plane fit + one ceres::Solve) against a local map

@@ -66,6 +66,21 @@ def _declare(L):
     L.aloam_shard_unique_id.argtypes = [C.c_char_p]
     L.aloam_shard_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
     L.aloam_shard_slot_range.argtypes = [C.c_int, C.c_int, C.c_int, I, I]
+    L.aloam_pipeline_create.restype = vp
+    L.aloam_pipeline_create.argtypes = [C.POINTER(abi.Params), C.c_int, C.c_int]
+    L.aloam_pipeline_destroy.argtypes = [vp]
+    L.aloam_pipeline_last_error.restype = C.c_char_p
+    L.aloam_pipeline_last_error.argtypes = [vp]
+    L.aloam_pipeline_context.restype = vp
+    L.aloam_pipeline_context.argtypes = [vp, C.c_int]
+    L.aloam_pipeline_push.argtypes = [vp, vp, C.c_int, C.c_int, C.POINTER(abi.OdomResult), I,
+                                      C.POINTER(abi.MapResult), I]
+    L.aloam_pipeline_flush.argtypes = [vp, C.POINTER(abi.OdomResult), I, C.POINTER(abi.MapResult), I,
+                                       C.POINTER(abi.MapResult), I]
+    L.aloam_pipeline_set_profiling.argtypes = [vp, C.c_int]
+    L.aloam_pipeline_timing.argtypes = [vp, C.c_int, C.POINTER(abi.Timing)]
+    for name in ("aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing"):
+        getattr(L, name).restype = C.c_int
     for name in ("aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
                  "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range"):
         getattr(L, name).restype = C.c_int
@@ -104,6 +119,8 @@ EXPORTED_SYMBOLS = [
     "aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features",
     "aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
     "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range",
+    "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
+    "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
 ]
 
 
@@ -355,104 +372,82 @@ def shard_slot_range(n_slots, rank, world):
 
 
 class Pipeline:
-    """The reference's node split on one GPU. stages=3: scanRegistration, laserOdometry and
-    laserMapping each own a context (own HIP stream), and scan k+2's feature extraction, scan k+1's
-    odometry and scan k's mapping run concurrently — the three ROS processes of the reference
-    (src/scanRegistration.cpp, src/laserOdometry.cpp, src/laserMapping.cpp:934 `process` thread),
-    handing over device to device (aloam_forward_features / aloam_forward_mapping_input).
-    stages=2 (default; measured faster on one MI355X — three concurrent contexts contend): scanRegistration
-    + laserOdometry share the front context.
+    """The reference's node split on one GPU, run by the library's native pipeline
+    (aloam_pipeline_*, csrc/aloam_pipeline.hip): one context (own HIP stream) and one native worker
+    thread per later stage — the three ROS processes of the reference (src/scanRegistration.cpp,
+    src/laserOdometry.cpp, src/laserMapping.cpp:934 `process` thread) — handing over device to device.
+    stages=2 (default; measured faster on one MI355X): [scanRegistration + laserOdometry] of scan k on
+    the caller's thread || laserMapping of scan k-1 on a worker. stages=3: one stage per node.
     Every scan still goes through all three stages, in order; results equal Context.process_scan's."""
 
     def __init__(self, params=None, device=0, stages=2):
-        from concurrent.futures import ThreadPoolExecutor
+        self.p = params if params is not None else abi.default_params(64)
         self.stages = stages
-        self.front = Context(params, device)                       # scanRegistration (+ odometry if 2 stages)
-        self.odom = Context(params, device) if stages == 3 else self.front
-        self.back = Context(params, device)                        # laserMapping
-        self._pool = ThreadPoolExecutor(max_workers=2)             # ctypes calls release the GIL
-        self._pending_map = None
-        self._pending_odom = None
+        L = lib()
+        self.h = L.aloam_pipeline_create(C.byref(self.p), int(device), int(stages))
+        if not self.h:
+            raise ALOAMError(f"aloam_pipeline_create failed: {L.aloam_last_error(None).decode()}")
         self._profiling = False
         self.last_back_timing = None
         self.last_odom_timing = None
         self.last_front_timing = None
 
-    def _contexts(self):
-        return list({id(x): x for x in (self.front, self.odom, self.back)}.values())
+    def _check(self, rc):
+        if rc != 0:
+            raise ALOAMError(f"rc={rc}: {lib().aloam_pipeline_last_error(self.h).decode()}")
+
+    def context_handle(self, stage):
+        return lib().aloam_pipeline_context(self.h, int(stage))
+
+    def _timing(self, stage):
+        t = abi.Timing()
+        self._check(lib().aloam_pipeline_timing(self.h, stage, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
 
     def set_profiling(self, on):
-        for c in self._contexts():
-            c.set_profiling(on)
+        self._check(lib().aloam_pipeline_set_profiling(self.h, int(on)))
         self._profiling = bool(on)
-
-    def _map_job(self):
-        mp = self.back.mapping()
-        return mp, (self.back.timing() if self._profiling else None)
-
-    def _odom_job(self):
-        od = self.odom.odometry()
-        return od, (self.odom.timing() if self._profiling else None)
 
     def push(self, pts=None, device_ptr=None, n=None):
         """Feed one scan. Returns (odometry result, mapping result) of the scans that completed those
         stages during this step (None while the pipeline fills)."""
-        if self.stages == 2:
-            od, _ = self.front.process_scan(pts, device_ptr, n, mapping=False)
-            self.last_front_timing = self.front.timing() if self._profiling else None
-            self.last_odom_timing = self.last_front_timing
-            mp = self._join_map()
-            if od["publish_to_mapping"]:
-                self.front.forward_mapping_input(self.back)
-                self._pending_map = self._pool.submit(self._map_job)
-            return od, mp
-        # three stages: scanRegistration here, odometry and mapping of earlier scans in the workers
         if device_ptr is not None:
-            self.front.scan_registration(int(n), device_ptr=device_ptr)
+            ptr, cnt, flags = C.c_void_p(device_ptr), int(n), abi.ALOAM_INPUT_DEVICE
         else:
-            self.front.scan_registration(pts)
-        self.last_front_timing = self.front.timing() if self._profiling else None
-        od = self._join_odom()
-        mp = self._join_map()
-        if od is not None and od["publish_to_mapping"]:
-            self.odom.forward_mapping_input(self.back)
-            self._pending_map = self._pool.submit(self._map_job)
-        self.front.forward_features(self.odom)
-        self._pending_odom = self._pool.submit(self._odom_job)
-        return od, mp
-
-    def _join_odom(self):
-        if self._pending_odom is None:
-            return None
-        od, self.last_odom_timing = self._pending_odom.result()
-        self._pending_odom = None
-        return od
-
-    def _join_map(self):
-        if self._pending_map is None:
-            return None
-        mp, self.last_back_timing = self._pending_map.result()
-        self._pending_map = None
-        return mp
+            pts = np.ascontiguousarray(pts, np.float32)
+            ptr, cnt, flags = pts.ctypes.data_as(C.c_void_p), len(pts), 0
+        od, mp = abi.OdomResult(), abi.MapResult()
+        ho, hm = C.c_int(), C.c_int()
+        self._check(lib().aloam_pipeline_push(self.h, ptr, cnt, flags, C.byref(od), C.byref(ho), C.byref(mp), C.byref(hm)))
+        if self._profiling:
+            self.last_front_timing = self._timing(0)
+            self.last_odom_timing = self._timing(1)
+            self.last_back_timing = self._timing(2)
+        return (abi.odom_to_dict(od) if ho.value else None), (abi.map_to_dict(mp) if hm.value else None)
 
     def flush(self):
         """Drain the pipeline: the (odometry, mapping) results that complete while draining."""
+        od, mp, mp2 = abi.OdomResult(), abi.MapResult(), abi.MapResult()
+        ho, hm, hm2 = C.c_int(), C.c_int(), C.c_int()
+        self._check(lib().aloam_pipeline_flush(self.h, C.byref(od), C.byref(ho), C.byref(mp), C.byref(hm),
+                                               C.byref(mp2), C.byref(hm2)))
+        if self._profiling:
+            self.last_back_timing = self._timing(2)
         out = []
-        od = self._join_odom() if self.stages == 3 else None
-        mp = self._join_map()
-        if mp is not None:
-            out.append((None, mp))
-        if od is not None:
-            if od["publish_to_mapping"]:
-                self.odom.forward_mapping_input(self.back)
-                out.append((od, self.back.mapping()))
-                self.last_back_timing = self.back.timing() if self._profiling else None
-            else:
-                out.append((od, None))
+        if hm.value:
+            out.append((None, abi.map_to_dict(mp)))
+        if ho.value:
+            out.append((abi.odom_to_dict(od), abi.map_to_dict(mp2) if hm2.value else None))
         return out
 
     def close(self):
-        self.flush()
-        self._pool.shutdown()
-        for c in self._contexts():
-            c.close()
+        if getattr(self, "h", None):
+            self.flush()
+            lib().aloam_pipeline_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

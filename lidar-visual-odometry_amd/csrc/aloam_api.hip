@@ -36,6 +36,14 @@ void prof_mark(Ctx& C, int idx) {
 
 __global__ void k_set2(int* dst, int a, int b) { dst[0] = a; dst[1] = b; }
 void set_counts2(Ctx& C, int* dst, int a, int b) { k_set2<<<1, 1, 0, C.stream>>>(dst, a, b); }
+struct Vec7 { double v[7]; };
+__global__ void k_set7(double* dst, Vec7 x) { if (threadIdx.x < 7) dst[threadIdx.x] = x.v[threadIdx.x]; }
+// the destination's copies are queued on its stream; the source's stream waits for them before it may
+// overwrite its buffers (no host round trip on the hand-off)
+static void handoff_done(Ctx& S, Ctx& C) {
+    HIPCHK(hipEventRecord(C.ev_handoff, C.stream));
+    HIPCHK(hipStreamWaitEvent(S.stream, C.ev_handoff, 0));
+}
 
 static thread_local std::string g_create_err;
 
@@ -172,6 +180,7 @@ static void allocate(Ctx& C) {
     HIPCHK(hipStreamCreateWithFlags(&C.stream2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
     C.ev_ready = true;
     HIPCHK(hipStreamSynchronize(C.stream));   // all zero-fills and init kernels done
@@ -342,9 +351,11 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     if (r.publish_to_mapping) {
         for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = r.q_w_curr[k];
         for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = r.t_w_curr[k];
-        // the odometry pose is handed to the mapping state on device
-        HIPCHK(hipMemcpyAsync((char*)C.d_map + offsetof(MapState, q_wodom), C.h_map.q_wodom, sizeof(double) * 7,
-                              hipMemcpyHostToDevice, st));
+        // the odometry pose is handed to the mapping state on device (kernel argument, no pageable copy)
+        Vec7 pose;
+        std::memcpy(pose.v, C.h_map.q_wodom, sizeof(pose.v));
+        k_set7<<<1, 64, 0, st>>>((double*)((char*)C.d_map + offsetof(MapState, q_wodom)), pose);
+        HIPCHK(hipGetLastError());
     }
     if (C.profiling) {
         C.timing.odometry_ms = ev_ms(C, 2, 3);
@@ -486,6 +497,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     for (auto& g : C->graphs) if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
+    if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
     s2m_release(*C);
     for (auto& b : C->bufs) (void)hipFree(b.p);
     if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
@@ -579,7 +591,7 @@ int aloam_forward_features(aloam_ctx* src, aloam_ctx* dst) {
     C.have_features = true;
     C.features_from_host = false;
     C.features_swapped = false;
-    sync(C);
+    handoff_done(S, C);
     S.have_features = false;
     API_END
 }
@@ -697,8 +709,11 @@ int aloam_forward_mapping_input(aloam_ctx* src, aloam_ctx* dst) {
     set_counts2(C, C.d_map_in_n, C.n_map_corner_in, C.n_map_surf_in);
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = S.h_map.q_wodom[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = S.h_map.t_wodom[k];
-    HIPCHK(hipMemcpyAsync((char*)C.d_map + offsetof(MapState, q_wodom), C.h_map.q_wodom, sizeof(double) * 7, hipMemcpyHostToDevice, st));
-    sync(C);
+    Vec7 pose;
+    std::memcpy(pose.v, C.h_map.q_wodom, sizeof(pose.v));   // q_wodom[4] and t_wodom[3] are adjacent (MapState)
+    k_set7<<<1, 64, 0, st>>>((double*)((char*)C.d_map + offsetof(MapState, q_wodom)), pose);
+    HIPCHK(hipGetLastError());
+    handoff_done(S, C);
     C.have_map_input = true;
     S.have_map_input = false;
     API_END

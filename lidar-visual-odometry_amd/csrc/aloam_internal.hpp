@@ -111,6 +111,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;   // mapping: the surf half of the per-kind work runs here (fork/join)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_handoff = nullptr; // device-to-device hand-offs: the source stream waits on it
     bool profiling = false;
     aloam_timing timing{};
     std::vector<DevBuf> bufs;

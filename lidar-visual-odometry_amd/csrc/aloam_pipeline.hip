@@ -1,0 +1,242 @@
+// aloam_pipeline.hip — the reference's node split as a native pipeline on one GPU (host side only).
+//
+// The reference runs scanRegistration, laserOdometry and laserMapping as three ROS processes, each
+// with one thread doing its hot block (src/scanRegistration.cpp:461-503, src/laserOdometry.cpp:311,
+// src/laserMapping.cpp:934 `process` thread), connected by topics. Here each stage owns an aloam_ctx
+// (own HIP stream) and a native worker thread; the hand-offs are device-to-device copies
+// (aloam_forward_features / aloam_forward_mapping_input). push() runs the first stage on the caller's
+// thread while the workers run the later stages of earlier scans:
+//   stages 2: caller: scanRegistration + laserOdometry (scan k)   || worker M: laserMapping (scan k-1)
+//   stages 3: caller: scanRegistration (k) || worker O: laserOdometry (k-1) || worker M: laserMapping (k-2)
+// Every scan goes through all stages in order, so results equal aloam_process_scan's.
+// The workers spin briefly on an atomic job word before sleeping, so a hand-off costs a cache-line
+// transfer instead of a thread wake-up on the critical path.
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+
+#include "../../include/aloam_hip.h"
+
+namespace {
+
+struct Worker {
+    std::thread th;
+    std::atomic<int> state{0};            // 0 idle, 1 job posted, 2 job done, 3 quit
+    std::mutex m;
+    std::condition_variable cv;
+    int (*fn)(void*) = nullptr;
+    void* arg = nullptr;
+    int rc = 0;
+
+    void start() {
+        th = std::thread([this] {
+            for (;;) {
+                int s;
+                int spins = 0;
+                while ((s = state.load(std::memory_order_acquire)) == 0 || s == 2) {
+                    if (++spins < 20000) { std::this_thread::yield(); continue; }
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [this] { const int v = state.load(std::memory_order_acquire); return v == 1 || v == 3; });
+                    spins = 0;
+                }
+                if (s == 3) return;
+                rc = fn(arg);
+                state.store(2, std::memory_order_release);
+            }
+        });
+    }
+    void post(int (*f)(void*), void* a) {
+        fn = f;
+        arg = a;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            state.store(1, std::memory_order_release);
+        }
+        cv.notify_one();
+    }
+    bool busy() const { return state.load(std::memory_order_acquire) == 1; }
+    // waits for the posted job; returns its rc, or 1 when nothing was posted
+    int join() {
+        int s;
+        while ((s = state.load(std::memory_order_acquire)) == 1) std::this_thread::yield();
+        if (s != 2) return 1;
+        state.store(0, std::memory_order_release);
+        return rc;
+    }
+    void stop() {
+        join();
+        {
+            std::lock_guard<std::mutex> lk(m);
+            state.store(3, std::memory_order_release);
+        }
+        cv.notify_one();
+        if (th.joinable()) th.join();
+    }
+};
+
+}  // namespace
+
+struct aloam_pipeline {
+    int stages = 2;
+    aloam_ctx* front = nullptr;     // scanRegistration (+ laserOdometry when stages == 2)
+    aloam_ctx* odom = nullptr;      // laserOdometry (== front when stages == 2)
+    aloam_ctx* back = nullptr;      // laserMapping
+    Worker wo, wm;
+    aloam_odom_result od_job{};     // worker O output
+    aloam_map_result mp_job{};      // worker M output
+    aloam_timing t_stage[3]{};      // timing snapshots of the last completed job per stage
+    int profiling = 0;
+    std::string err;
+};
+
+namespace {
+
+int odom_job(void* a) {
+    aloam_pipeline* P = (aloam_pipeline*)a;
+    const int rc = aloam_odometry(P->odom, &P->od_job);
+    if (rc == 0 && P->profiling) aloam_get_timing(P->odom, &P->t_stage[1]);
+    return rc;
+}
+int map_job(void* a) {
+    aloam_pipeline* P = (aloam_pipeline*)a;
+    const int rc = aloam_mapping(P->back, &P->mp_job);
+    if (rc == 0 && P->profiling) aloam_get_timing(P->back, &P->t_stage[2]);
+    return rc;
+}
+int fail(aloam_pipeline* P, aloam_ctx* c, int rc) {
+    P->err = aloam_last_error(c);
+    return rc;
+}
+// joins worker M; *have = 1 and *mp filled when a mapping job completed
+int join_map(aloam_pipeline* P, aloam_map_result* mp, int* have) {
+    const int rc = P->wm.join();
+    if (rc == 1) return 0;                      // nothing pending
+    if (rc != 0) return fail(P, P->back, rc);
+    *have = 1;
+    if (mp) *mp = P->mp_job;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int stages) {
+    if (!p || (stages != 2 && stages != 3)) return nullptr;
+    aloam_pipeline* P = new (std::nothrow) aloam_pipeline();
+    if (!P) return nullptr;
+    P->stages = stages;
+    P->front = aloam_create(p, device);
+    P->odom = stages == 3 ? aloam_create(p, device) : P->front;
+    P->back = aloam_create(p, device);
+    if (!P->front || !P->odom || !P->back) {
+        if (P->back) aloam_destroy(P->back);
+        if (stages == 3 && P->odom) aloam_destroy(P->odom);
+        if (P->front) aloam_destroy(P->front);
+        delete P;
+        return nullptr;
+    }
+    P->wm.start();
+    if (stages == 3) P->wo.start();
+    return P;
+}
+
+void aloam_pipeline_destroy(aloam_pipeline* P) {
+    if (!P) return;
+    P->wm.stop();
+    if (P->stages == 3) P->wo.stop();
+    aloam_destroy(P->back);
+    if (P->stages == 3) aloam_destroy(P->odom);
+    aloam_destroy(P->front);
+    delete P;
+}
+
+const char* aloam_pipeline_last_error(const aloam_pipeline* P) { return P ? P->err.c_str() : "null pipeline"; }
+
+aloam_ctx* aloam_pipeline_context(aloam_pipeline* P, int stage) {
+    if (!P || stage < 0 || stage > 2) return nullptr;
+    return stage == 0 ? P->front : stage == 1 ? P->odom : P->back;
+}
+
+int aloam_pipeline_set_profiling(aloam_pipeline* P, int enable) {
+    if (!P || P->wm.busy() || (P->stages == 3 && P->wo.busy())) return ALOAM_E_STATE;
+    P->profiling = enable != 0;
+    int rc = aloam_set_profiling(P->front, enable);
+    if (!rc && P->stages == 3) rc = aloam_set_profiling(P->odom, enable);
+    if (!rc) rc = aloam_set_profiling(P->back, enable);
+    std::memset(P->t_stage, 0, sizeof(P->t_stage));
+    return rc;
+}
+
+int aloam_pipeline_timing(aloam_pipeline* P, int stage, aloam_timing* t) {
+    if (!P || !t || stage < 0 || stage > 2) return ALOAM_E_ARG;
+    *t = P->t_stage[stage];
+    return ALOAM_OK;
+}
+
+int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, aloam_odom_result* od, int* have_od,
+                        aloam_map_result* mp, int* have_mp) {
+    if (!P || !have_od || !have_mp) return ALOAM_E_ARG;
+    *have_od = 0;
+    *have_mp = 0;
+    int rc;
+    if (P->stages == 2) {
+        aloam_odom_result o{};
+        rc = aloam_process_scan(P->front, xyzr, n, flags | ALOAM_NO_MAPPING, &o, nullptr);
+        if (rc) return fail(P, P->front, rc);
+        if (P->profiling) aloam_get_timing(P->front, &P->t_stage[0]), P->t_stage[1] = P->t_stage[0];
+        *have_od = 1;
+        if (od) *od = o;
+        if ((rc = join_map(P, mp, have_mp))) return rc;
+        if (o.publish_to_mapping) {
+            if ((rc = aloam_forward_mapping_input(P->front, P->back))) return fail(P, P->back, rc);
+            P->wm.post(map_job, P);
+        }
+        return ALOAM_OK;
+    }
+    // three stages: scanRegistration here, odometry and mapping of earlier scans in the workers
+    rc = aloam_scan_registration(P->front, xyzr, n, flags);
+    if (rc) return fail(P, P->front, rc);
+    if (P->profiling) aloam_get_timing(P->front, &P->t_stage[0]);
+    const int orc = P->wo.join();
+    if (orc != 1 && orc != 0) return fail(P, P->odom, orc);
+    if ((rc = join_map(P, mp, have_mp))) return rc;
+    if (orc == 0) {
+        *have_od = 1;
+        if (od) *od = P->od_job;
+        if (P->od_job.publish_to_mapping) {
+            if ((rc = aloam_forward_mapping_input(P->odom, P->back))) return fail(P, P->back, rc);
+            P->wm.post(map_job, P);
+        }
+    }
+    if ((rc = aloam_forward_features(P->front, P->odom))) return fail(P, P->odom, rc);
+    P->wo.post(odom_job, P);
+    return ALOAM_OK;
+}
+
+int aloam_pipeline_flush(aloam_pipeline* P, aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp,
+                         aloam_map_result* mp2, int* have_mp2) {
+    if (!P || !have_od || !have_mp || !have_mp2) return ALOAM_E_ARG;
+    *have_od = *have_mp = *have_mp2 = 0;
+    int rc;
+    const int orc = P->stages == 3 ? P->wo.join() : 1;
+    if (orc != 1 && orc != 0) return fail(P, P->odom, orc);
+    if ((rc = join_map(P, mp, have_mp))) return rc;
+    if (orc == 0) {
+        *have_od = 1;
+        if (od) *od = P->od_job;
+        if (P->od_job.publish_to_mapping) {
+            if ((rc = aloam_forward_mapping_input(P->odom, P->back))) return fail(P, P->back, rc);
+            if ((rc = aloam_mapping(P->back, mp2))) return fail(P, P->back, rc);
+            if (P->profiling) aloam_get_timing(P->back, &P->t_stage[2]);
+            *have_mp2 = 1;
+        }
+    }
+    return ALOAM_OK;
+}
+
+}  // extern "C"

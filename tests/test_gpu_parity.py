@@ -307,3 +307,20 @@ def test_pipeline_matches_single_context(lvo, stages):
         np.testing.assert_allclose(o["t_w_curr"], o_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(m["t_w_curr"], m_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(m["q_w_curr"], m_ref["q_w_curr"], rtol=1e-9, atol=1e-12)
+
+
+def test_pipeline_errors_and_timing(lvo):
+    """The native pipeline reports stage errors through aloam_pipeline_last_error and stays usable;
+    with profiling on, every stage's HIP-event timing of its last job is available."""
+    p = abi.default_params(16)
+    pipe = lvo.Pipeline(p, stages=2)
+    with pytest.raises(lvo.ALOAMError):
+        pipe.push(np.zeros((p.max_scan_points + 1, 4), np.float32))
+    pipe.set_profiling(True)
+    for k in range(3):
+        pipe.push(synth.scan("vlp16", k))
+    out = pipe.flush()
+    assert len(out) == 1 and out[0][1] is not None
+    assert pipe.last_front_timing["scan_registration_ms"] > 0 and pipe.last_front_timing["odometry_ms"] > 0
+    assert pipe.last_back_timing["mapping_ms"] > 0
+    pipe.close()
