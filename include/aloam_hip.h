@@ -151,6 +151,12 @@ int         aloam_abi_version(void);
  * The features stay resident in the context for aloam_odometry(); fetch them with
  * aloam_get_features(). */
 int aloam_scan_registration(aloam_ctx* ctx, const float* xyzr, int n, int flags);
+/* The same from a sensor_msgs/PointCloud2 data blob as the /velodyne_points callback receives it
+ * (scanRegistration.cpp:114,131-133): n records of point_step bytes (multiple of 4, >= 12) with
+ * float32 x, y, z at byte offsets 0, 4, 8 (pcl::PointXYZ / PointXYZI / velodyne XYZIR layouts;
+ * 16 = KITTI .bin, 32 = pcl::PointXYZI). Other fields are ignored, as by pcl::fromROSMsg into the
+ * reference's PointXYZ cloud. Host blob, or device blob with ALOAM_INPUT_DEVICE. */
+int aloam_scan_registration_pc2(aloam_ctx* ctx, const void* data, int n, int point_step, int flags);
 int aloam_feature_counts(aloam_ctx* ctx, int counts[5]); /* full, sharp, less_sharp, flat, less_flat */
 int aloam_get_features(aloam_ctx* ctx, aloam_features* out);
 

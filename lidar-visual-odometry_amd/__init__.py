@@ -66,6 +66,8 @@ def _declare(L):
     L.aloam_shard_unique_id.argtypes = [C.c_char_p]
     L.aloam_shard_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
     L.aloam_shard_slot_range.argtypes = [C.c_int, C.c_int, C.c_int, I, I]
+    L.aloam_scan_registration_pc2.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int]
+    L.aloam_scan_registration_pc2.restype = C.c_int
     L.aloam_pipeline_create.restype = vp
     L.aloam_pipeline_create.argtypes = [C.POINTER(abi.Params), C.c_int, C.c_int]
     L.aloam_pipeline_destroy.argtypes = [vp]
@@ -119,6 +121,7 @@ EXPORTED_SYMBOLS = [
     "aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features",
     "aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
     "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range",
+    "aloam_scan_registration_pc2",
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
 ]
@@ -164,6 +167,17 @@ class Context:
             return
         pts = np.ascontiguousarray(pts, np.float32)
         self._check(lib().aloam_scan_registration(self.h, pts.ctypes.data_as(C.c_void_p), len(pts), 0))
+
+    def scan_registration_pc2(self, blob, n=None, point_step=32, device_ptr=None):
+        """aloam_scan_registration_pc2: a PointCloud2 data blob (bytes / uint8 array of n records of
+        point_step bytes, x y z float32 at offsets 0 4 8), or a device pointer with n given."""
+        if device_ptr is not None:
+            self._check(lib().aloam_scan_registration_pc2(self.h, C.c_void_p(device_ptr), int(n), int(point_step),
+                                                          abi.ALOAM_INPUT_DEVICE))
+            return
+        b = np.ascontiguousarray(np.frombuffer(blob, np.uint8) if isinstance(blob, (bytes, bytearray)) else blob).view(np.uint8)
+        n = len(b) // point_step if n is None else int(n)
+        self._check(lib().aloam_scan_registration_pc2(self.h, b.ctypes.data_as(C.c_void_p), n, int(point_step), 0))
 
     def feature_counts(self):
         cnt = (C.c_int * 5)()

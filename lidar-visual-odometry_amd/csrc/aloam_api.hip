@@ -244,6 +244,16 @@ static void read_meta(Ctx& C) {
     C.n_lflat = C.h_meta.counts[4];
 }
 
+// sensor_msgs/PointCloud2 blob -> float4 (x, y, z, 0): x, y, z float32 at byte offsets 0, 4, 8 of each
+// point_step-byte record (the fields pcl::fromROSMsg reads into the PointXYZ laserCloudIn,
+// scanRegistration.cpp:131-133; any further fields — intensity, ring, time — are not used by the path)
+__global__ void k_pc2_gather(const unsigned char* __restrict__ blob, int n, int step, float4* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* r = (const float*)(blob + (size_t)i * step);
+    out[i] = make_float4(r[0], r[1], r[2], 0.f);
+}
+
 static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     if (n < 0 || (n > 0 && !xyzr)) throw ApiError{ALOAM_E_ARG, "bad input"};
     if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "scan larger than max_scan_points"};
@@ -515,6 +525,28 @@ const char* aloam_last_error(const aloam_ctx* ctx) {
 int aloam_scan_registration(aloam_ctx* ctx, const float* xyzr, int n, int flags) {
     API_BEGIN(ctx)
     do_scan_registration(C, xyzr, n, flags);
+    API_END
+}
+
+int aloam_scan_registration_pc2(aloam_ctx* ctx, const void* data, int n, int point_step, int flags) {
+    API_BEGIN(ctx)
+    if (n < 0 || (n > 0 && !data) || point_step < 12 || point_step % 4) throw ApiError{ALOAM_E_ARG, "bad PointCloud2 blob"};
+    if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "scan larger than max_scan_points"};
+    const unsigned char* blob = (const unsigned char*)data;
+    const size_t bytes = (size_t)n * point_step;
+    if (!(flags & ALOAM_INPUT_DEVICE) && n > 0) {
+        if (bytes > C.cap_pc2) {
+            C.cap_pc2 = std::max(bytes, 2 * C.cap_pc2);
+            C.d_pc2 = (unsigned char*)dalloc(C, C.cap_pc2);
+        }
+        HIPCHK(hipMemcpyAsync(C.d_pc2, data, bytes, hipMemcpyHostToDevice, C.stream));
+        blob = C.d_pc2;
+    }
+    if (n > 0) {
+        k_pc2_gather<<<(n + 255) / 256, 256, 0, C.stream>>>(blob, n, point_step, C.d_in);
+        HIPCHK(hipGetLastError());
+    }
+    do_scan_registration(C, (const float*)C.d_in, n, ALOAM_INPUT_DEVICE);
     API_END
 }
 

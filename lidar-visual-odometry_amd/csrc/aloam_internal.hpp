@@ -119,6 +119,8 @@ struct Ctx {
     // ---- scanRegistration ----
     int cap_in = 0;
     float4* d_in = nullptr;        // raw points staging
+    unsigned char* d_pc2 = nullptr; // PointCloud2 blob staging (grown on demand)
+    size_t cap_pc2 = 0;
     float4* d_cl = nullptr;        // after NaN / range filter
     int* d_sid = nullptr;          // scanID per filtered point (-1 = dropped)
     float* d_ori = nullptr;        // raw -atan2f per filtered point

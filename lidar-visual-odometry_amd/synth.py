@@ -150,3 +150,17 @@ def c4_registration(name="l128", frame=0, half=50.0, map_step=0.107, seed=4, sur
                    w * W - x * X - y * Y - z * Z])
     x0 = np.concatenate([q0 / np.linalg.norm(q0), o + np.asarray(dt, np.float64)])
     return m, m, np.ascontiguousarray(s[::corner_stride]), np.ascontiguousarray(s[::surf_stride]), x0, x_true
+
+
+def to_pointcloud2(pts, point_step=32, seed=0):
+    """A sensor_msgs/PointCloud2 data blob of a sweep: x, y, z float32 at byte offsets 0, 4, 8 and,
+    when the record has room, intensity at 16 (pcl::PointXYZI, point_step 32) or 12; every other byte
+    is filled with seeded noise so a reader that touches them is caught."""
+    pts = np.asarray(pts, np.float32).reshape(-1, 4)
+    n = len(pts)
+    rec = np.random.default_rng(seed).integers(0, 256, size=(n, point_step), dtype=np.uint8)
+    rec[:, 0:12] = pts[:, :3].view(np.uint8).reshape(n, 12)
+    off = 16 if point_step >= 20 else (12 if point_step >= 16 else None)
+    if off is not None:
+        rec[:, off:off + 4] = pts[:, 3:4].view(np.uint8).reshape(n, 4)
+    return rec.tobytes()

@@ -92,3 +92,13 @@ def test_null_context_is_an_argument_error():
     L = lvo.lib()
     assert L.aloam_odometry(None, None) == abi.ALOAM_E_ARG
     assert L.aloam_scan_registration(None, None, 0, 0) == abi.ALOAM_E_ARG
+
+
+def test_cpp_host_tool_links_against_the_abi():
+    """tools/aloam_kitti (C++ host over include/aloam_hip.h only) is built and resolves the library;
+    without arguments it prints its usage before touching any device."""
+    exe = os.path.join(REPO, "lidar-visual-odometry_amd", "tools", "aloam_kitti")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 2 and "usage" in r.stderr
+    assert "libaloam_hip.so" in subprocess.check_output(["ldd", exe], text=True)

@@ -324,3 +324,46 @@ def test_pipeline_errors_and_timing(lvo):
     assert pipe.last_front_timing["scan_registration_ms"] > 0 and pipe.last_front_timing["odometry_ms"] > 0
     assert pipe.last_back_timing["mapping_ms"] > 0
     pipe.close()
+
+
+@pytest.mark.parametrize("step", [16, 20, 32, 48])
+def test_pointcloud2_ingestion_bit_exact(gpu_ctx_factory, step):
+    """aloam_scan_registration_pc2 (sensor_msgs/PointCloud2 blob, x y z at offsets 0 4 8, noise in every
+    other byte) gives the oracle's features bit for bit, from host and from device memory."""
+    import torch
+    ctx = gpu_ctx_factory(64)
+    orc = ob.Oracle(abi.default_params(64))
+    pts = synth.scan("hdl64", 2)
+    blob = synth.to_pointcloud2(pts, step, seed=step)
+    orc.scan_registration(pts)
+    fo = orc.features()
+    ctx.scan_registration_pc2(blob, point_step=step)
+    assert_features_equal(ctx.features(), fo)
+    d = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to("cuda:0")
+    ctx.scan_registration_pc2(None, n=len(pts), point_step=step, device_ptr=d.data_ptr())
+    assert_features_equal(ctx.features(), fo)
+    with pytest.raises(lvo.ALOAMError):
+        ctx.scan_registration_pc2(blob[:100], n=5, point_step=10)
+
+
+def test_cpp_host_tool_matches_python_host(lvo, tmp_path):
+    """The C++ headless host (tools/aloam_kitti: KITTI .bin files -> native pipeline -> KITTI poses)
+    reproduces the single-context trajectory."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(lvo.LIB_PATH), "..", "tools", "aloam_kitti")
+    frames = [synth.scan("hdl64", k) for k in range(6)]
+    paths = []
+    for k, f in enumerate(frames):
+        pth = str(tmp_path / f"{k:06d}.bin")
+        synth.write_kitti_bin(pth, f)
+        paths.append(pth)
+    out = str(tmp_path / "poses.txt")
+    subprocess.check_call([exe, "-l", "64", "-o", out] + paths, timeout=120)
+    poses = np.loadtxt(out).reshape(-1, 3, 4)
+    ctx = lvo.Context(abi.default_params(64))
+    ref = [ctx.process_scan(f)[1] for f in frames]
+    ctx.close()
+    assert len(poses) == len(frames)
+    for P, m in zip(poses, ref):
+        np.testing.assert_allclose(P[:, 3], m["t_w_curr"], rtol=1e-9, atol=1e-9)
