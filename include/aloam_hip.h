@@ -246,6 +246,9 @@ typedef struct aloam_timing {
 } aloam_timing;
 int aloam_set_profiling(aloam_ctx* ctx, int enable);
 int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);
+/* Restricts the context's streams to a set of CUs (bit i of mask[i / 32] = CU i; nwords = 0 lifts the
+ * restriction). Used to give concurrent pipeline stages disjoint CUs. The context must be idle. */
+int aloam_set_cu_mask(aloam_ctx* ctx, const unsigned* mask, int nwords);
 
 /* ---- native pipeline: the reference's node split on one GPU ---------------------------------
  * scanRegistration, laserOdometry and laserMapping run as three ROS processes in the reference, one

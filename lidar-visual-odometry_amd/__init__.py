@@ -66,6 +66,8 @@ def _declare(L):
     L.aloam_shard_unique_id.argtypes = [C.c_char_p]
     L.aloam_shard_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
     L.aloam_shard_slot_range.argtypes = [C.c_int, C.c_int, C.c_int, I, I]
+    L.aloam_set_cu_mask.argtypes = [vp, C.POINTER(C.c_uint), C.c_int]
+    L.aloam_set_cu_mask.restype = C.c_int
     L.aloam_scan_registration_pc2.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int]
     L.aloam_scan_registration_pc2.restype = C.c_int
     L.aloam_pipeline_create.restype = vp
@@ -121,7 +123,7 @@ EXPORTED_SYMBOLS = [
     "aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features",
     "aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
     "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range",
-    "aloam_scan_registration_pc2",
+    "aloam_scan_registration_pc2", "aloam_set_cu_mask",
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
 ]

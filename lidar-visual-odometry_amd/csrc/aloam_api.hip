@@ -482,6 +482,9 @@ aloam_ctx* aloam_create(const aloam_params* p, int device) {
     try {
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, device));
+        C->n_cus = prop.multiProcessorCount;
         allocate(*C);
     } catch (const HipError& e) {
         g_create_err = e.msg;
@@ -860,6 +863,34 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
         // B = sum_q [16 + 16 |C27(q)|] + 8 k Q
         C.timing.knn_bytes = 16.0 * nq + 16.0 * (double)cand + 8.0 * k * (double)nq;
     }
+    API_END
+}
+
+int aloam_set_cu_mask(aloam_ctx* ctx, const unsigned* mask, int nwords) {
+    API_BEGIN(ctx)
+    if (nwords < 0 || (nwords > 0 && !mask)) throw ApiError{ALOAM_E_ARG, "bad CU mask"};
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, C.device));
+    int n = 0;
+    for (int w = 0; w < nwords; w++)
+        for (int b = 0; b < 32; b++)
+            if (w * 32 + b < prop.multiProcessorCount && ((mask[w] >> b) & 1u)) n++;
+    if (nwords > 0 && n == 0) throw ApiError{ALOAM_E_ARG, "CU mask selects no CU"};
+    HIPCHK(hipStreamSynchronize(C.stream));
+    HIPCHK(hipStreamSynchronize(C.stream2));
+    hipStream_t s1 = nullptr, s2 = nullptr;
+    if (nwords > 0) {
+        HIPCHK(hipExtStreamCreateWithCUMask(&s1, (uint32_t)nwords, mask));
+        HIPCHK(hipExtStreamCreateWithCUMask(&s2, (uint32_t)nwords, mask));
+    } else {
+        HIPCHK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    }
+    (void)hipStreamDestroy(C.stream);
+    (void)hipStreamDestroy(C.stream2);
+    C.stream = s1;
+    C.stream2 = s2;
+    C.n_cus = nwords > 0 ? n : prop.multiProcessorCount;
     API_END
 }
 

@@ -221,6 +221,7 @@ struct Ctx {
     // ---- scan-to-map registration (k_s2m.hip) and its shard communicator ----
     struct S2M* s2m = nullptr;       // allocated by the first aloam_s2m_* call
     int shard_rank = 0, shard_world = 1;
+    int n_cus = 256;                 // CUs this context's streams may use (CU mask popcount; caps co-resident grids)
     void* shard_comm = nullptr;      // ncclComm_t (world > 1)
 };
 

@@ -563,7 +563,7 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
     const int est = std::max(1, std::min(nslots, live_hint > 0 ? live_hint + live_hint / 4 : nslots));
     static const int spt = getenv("ALOAM_LM_SPT") ? std::max(1, atoi(getenv("ALOAM_LM_SPT"))) : 1;   // tuning knob
     int G = std::max((est + spt * CB - 1) / (spt * CB), (est + LM_CACHE - 1) / LM_CACHE);
-    G = std::max(1, std::min(LM_COOP_MAX, G));
+    G = std::max(1, std::min(std::min(LM_COOP_MAX, C.n_cus), G));   // every workgroup must be co-resident (<= 1 per CU)
     const int cap = std::min(LM_CACHE, (nslots + G - 1) / G);          // LDS slots per workgroup
     const size_t lds = sizeof(aloam_factor) * (size_t)cap;
     k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_lm_recs, C.d_lm_seq, C.d_bar_err, out,

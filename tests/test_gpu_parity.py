@@ -367,3 +367,23 @@ def test_cpp_host_tool_matches_python_host(lvo, tmp_path):
     assert len(poses) == len(frames)
     for P, m in zip(poses, ref):
         np.testing.assert_allclose(P[:, 3], m["t_w_curr"], rtol=1e-9, atol=1e-9)
+
+
+def test_cu_mask_contexts_match(gpu_ctx_factory):
+    """A context restricted to a CU subset (aloam_set_cu_mask; the pipeline's per-stage partitions)
+    computes the same results — the persistent LM solver's grid is capped by the mask, so its fixed
+    reduction order (and the last bits of the pose) may differ: poses to 1e-9."""
+    import ctypes as C
+    frames = [synth.scan("vlp16", k) for k in range(4)]
+    a = gpu_ctx_factory(16)
+    b = gpu_ctx_factory(16)
+    mask = (C.c_uint * 8)(*([0xF] + [0] * 7))          # 4 CUs
+    assert lvo.lib().aloam_set_cu_mask(b.h, mask, 8) == 0
+    for f in frames:
+        oa, ma = a.process_scan(f)
+        ob_, mb = b.process_scan(f)
+        assert oa["corner_correspondence"] == ob_["corner_correspondence"]
+        np.testing.assert_allclose(ma["t_w_curr"], mb["t_w_curr"], rtol=1e-9, atol=1e-12)
+    assert lvo.lib().aloam_set_cu_mask(b.h, mask, 0) == 0
+    zero = (C.c_uint * 8)()
+    assert lvo.lib().aloam_set_cu_mask(b.h, zero, 8) != 0
