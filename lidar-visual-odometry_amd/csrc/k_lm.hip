@@ -572,33 +572,83 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
 }
 
 // ---- scan-to-map registration across ranks (aloam_s2m_*) ----------------------------
-// A Solve is max_iter + 1 passes of {k_s2m_partials -> record exchange -> k_s2m_tail}. The slots are
-// cut into nrec fixed blocks of `per` slots; a rank's partials launch covers its run of blocks, one
-// workgroup per block, and writes one S2M_REC-double record per block (the block's 29 normal-equation
-// sums in the fixed block_reduce_acc order + its corner / surf correspondence counts). After the
-// exchange every rank holds all nrec records in block order; k_s2m_tail reduces them with the same
-// fixed-order reduce_rows and runs the LM tail on the LMState in HBM, so every rank computes the
-// bitwise-identical step whatever the world size. A pass after termination is a no-op on every rank.
+// A Solve is max_iter + 1 pass launches, each followed by the record exchange, then one final launch.
+// The slots are cut into nrec fixed blocks of `per` slots; a rank's pass launch covers its run of
+// blocks, one workgroup per block, and writes one S2M_REC-double record per block (the block's 29
+// normal-equation sums in the fixed block_reduce_acc order + its corner / surf correspondence
+// counts). Pass p > 0 first finishes pass p-1 in EVERY workgroup: it reduces the nrec exchanged
+// records in block order (fixed-order reduce_rows) and runs the LM tail on its LDS copy of the state
+// (bitwise-identical in every workgroup and on every rank, whatever the world size), workgroup 0
+// publishing the new state into the other half of a double-buffered LMState; then it evaluates its
+// block at the new candidate. k_s2m_final runs the last tail and writes the parameters.
+// A pass after termination is a no-op on every rank.
 constexpr int S2M_REC = 32;
-static_assert(ALOAM_S2M_RECORDS * NACC * 8 <= 64 * 1024, "tail records must fit in LDS");
+static_assert(ALOAM_S2M_RECORDS <= CB, "one record per thread in the record reduction");
 
-__global__ void __launch_bounds__(CB) k_s2m_partials(const aloam_factor* __restrict__ f, int nslots, int per, int rec0, int nrec,
-                                                     const LMState* __restrict__ st, const double* __restrict__ x, int pass,
-                                                     double* __restrict__ send) {
+// records of the previous pass -> tot (every workgroup, fixed order): thread t loads record t (all 29
+// sums in flight at once), then the same fixed-order block reduction as a pass's own partials
+__device__ __forceinline__ void s2m_reduce_records(const double* __restrict__ recs, int nrec, double* rows, double* part8, double* tot) {
+    double acc[NACC];
+    const int t = threadIdx.x;
+    if (t < nrec) {
+        const double2* r2 = (const double2*)(recs + (size_t)t * S2M_REC);   // records are 256-B aligned
+        double2 v[(NACC + 1) / 2];
+#pragma unroll
+        for (int i = 0; i < (NACC + 1) / 2; i++) v[i] = r2[i];
+#pragma unroll
+        for (int i = 0; i < NACC; i++) acc[i] = (i & 1) ? v[i / 2].y : v[i / 2].x;
+    } else {
+#pragma unroll
+        for (int i = 0; i < NACC; i++) acc[i] = 0.0;
+    }
+    block_reduce_acc<CB>(acc, rows, part8, tot);
+}
+
+__global__ void __launch_bounds__(CB) k_s2m_pass(const aloam_factor* __restrict__ f, int nslots, int per, int rec0, int nrec,
+                                                 const double* __restrict__ prev, const LMState* __restrict__ st_in,
+                                                 LMState* __restrict__ st_out, const double* __restrict__ x0, int pass,
+                                                 aloam_lm_summary* sum, int max_iter, int* round_cnt, double* __restrict__ send) {
     __shared__ double rows[CB / 4 * NACC];
     __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
+    __shared__ LMState ls;
+    __shared__ double xl[7];
     __shared__ int cnt[2];
+    if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+    if (pass > 0) {
+        if (threadIdx.x == 0) ls = *st_in;
+        s2m_reduce_records(prev, nrec, rows, part8, tot);
+        if (pass == 1 && blockIdx.x == 0 && round_cnt) {          // correspondences of this round (pass-0 records)
+            int a = 0, b = 0;
+            for (int r = threadIdx.x; r < nrec; r += CB) { a += (int)prev[(size_t)r * S2M_REC + NACC]; b += (int)prev[(size_t)r * S2M_REC + NACC + 1]; }
+            a = wave_sum_i(a);
+            b = wave_sum_i(b);
+            if ((threadIdx.x & 63) == 0) { atomicAdd(&cnt[0], a); atomicAdd(&cnt[1], b); }
+        }
+        if (threadIdx.x == 0) {
+            if (pass == 1 || !ls.done) {
+                const double* xs = pass == 1 ? x0 : ls.x;
+                for (int i = 0; i < 7; i++) xl[i] = xs[i];
+                lm_tail_reg(&ls, tot, pass - 1, xl, blockIdx.x == 0 ? sum : nullptr, max_iter);
+            }
+        }
+        __syncthreads();
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) *st_out = ls;
+            if (pass == 1 && round_cnt && threadIdx.x < 2) round_cnt[threadIdx.x] = cnt[threadIdx.x];
+        }
+        __syncthreads();
+        if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+    }
     double* rec = send + (size_t)blockIdx.x * S2M_REC;
     const int g = rec0 + blockIdx.x;
-    if ((pass > 0 && st->done) || g >= nrec) {          // uniform: the same state on every rank
+    if ((pass > 0 && ls.done) || g >= nrec) {                    // uniform: the same state everywhere
         if (threadIdx.x < S2M_REC) rec[threadIdx.x] = 0.0;
         return;
     }
-    const double* xs = pass == 0 ? x : st->cand;
+    const double* xs = pass == 0 ? x0 : ls.cand;
     const dquat q{xs[0], xs[1], xs[2], xs[3]};
     const double t[3] = {xs[4], xs[5], xs[6]};
-    if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
     double acc[NACC];
 #pragma unroll
     for (int i = 0; i < NACC; i++) acc[i] = 0;
@@ -611,44 +661,44 @@ __global__ void __launch_bounds__(CB) k_s2m_partials(const aloam_factor* __restr
         accumulate(fi, q, t, acc);
     }
     __syncthreads();
-    const int se = wave_sum_i(ne), sp = wave_sum_i(np);
-    if ((threadIdx.x & 63) == 0 && (se | sp)) { atomicAdd(&cnt[0], se); atomicAdd(&cnt[1], sp); }
+    if (pass == 0) {
+        const int se = wave_sum_i(ne), sp = wave_sum_i(np);
+        if ((threadIdx.x & 63) == 0 && (se | sp)) { atomicAdd(&cnt[0], se); atomicAdd(&cnt[1], sp); }
+    }
     block_reduce_acc<CB>(acc, rows, part8, tot);
     if (threadIdx.x < NACC) rec[threadIdx.x] = tot[threadIdx.x];
     if (threadIdx.x == 0) { rec[NACC] = cnt[0]; rec[NACC + 1] = cnt[1]; rec[NACC + 2] = 0.0; }
 }
 
-__global__ void __launch_bounds__(CB) k_s2m_tail(const double* __restrict__ recs, int nrec, LMState* st, double* x, int pass,
-                                                 aloam_lm_summary* out, int max_iter, int* round_cnt) {
-    __shared__ double rows[ALOAM_S2M_RECORDS * NACC];
+// the tail of the last pass (one workgroup): parameters -> x
+__global__ void __launch_bounds__(CB) k_s2m_final(const double* __restrict__ prev, int nrec, const LMState* __restrict__ st_in,
+                                                  double* x, int last_pass, aloam_lm_summary* sum, int max_iter) {
+    __shared__ double rows[CB / 4 * NACC];
     __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
-    if (pass > 0 && st->done) return;
-    for (int i = threadIdx.x; i < nrec * NACC; i += CB) {
-        const int b = i / NACC, c = i - b * NACC;
-        rows[i] = recs[(size_t)b * S2M_REC + c];
-    }
-    if (pass == 0 && round_cnt && threadIdx.x < 2) {
-        int s = 0;
-        for (int b = 0; b < nrec; b++) s += (int)recs[(size_t)b * S2M_REC + NACC + threadIdx.x];
-        round_cnt[threadIdx.x] = s;
-    }
-    __syncthreads();
-    reduce_rows(rows, nrec, part8, tot);
+    __shared__ LMState ls;
+    __shared__ double xl[7];
+    if (threadIdx.x == 0) ls = *st_in;
+    s2m_reduce_records(prev, nrec, rows, part8, tot);
     if (threadIdx.x == 0) {
-        LMState L = *st;
-        lm_tail(&L, tot, pass, x, out, max_iter);
-        *st = L;
+        if (last_pass == 0 || !ls.done) {
+            const double* xs = last_pass == 0 ? x : ls.x;
+            for (int i = 0; i < 7; i++) xl[i] = xs[i];
+            lm_tail_reg(&ls, tot, last_pass, xl, sum, max_iter);
+        }
+        for (int i = 0; i < 7; i++) x[i] = ls.x[i];
     }
 }
 
-void s2m_partials_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const LMState* st,
-                         const double* x, int pass, double* send) {
-    k_s2m_partials<<<nrec_local, CB, 0, C.stream>>>(f, nslots, per, rec0, nrec, st, x, pass, send);
+void s2m_pass_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const double* prev,
+                     const LMState* st_in, LMState* st_out, const double* x0, int pass, aloam_lm_summary* sum, int* round_cnt,
+                     double* send) {
+    k_s2m_pass<<<nrec_local, CB, 0, C.stream>>>(f, nslots, per, rec0, nrec, prev, st_in, st_out, x0, pass, sum,
+                                                std::min(C.P.max_solver_iterations, 200), round_cnt, send);
     HIPCHK(hipGetLastError());
 }
-void s2m_tail_launch(Ctx& C, const double* recs, int nrec, LMState* st, double* x, int pass, aloam_lm_summary* out, int* round_cnt) {
-    k_s2m_tail<<<1, CB, 0, C.stream>>>(recs, nrec, st, x, pass, out, std::min(C.P.max_solver_iterations, 200), round_cnt);
+void s2m_final_launch(Ctx& C, const double* prev, int nrec, const LMState* st_in, double* x, int last_pass, aloam_lm_summary* sum) {
+    k_s2m_final<<<1, CB, 0, C.stream>>>(prev, nrec, st_in, x, last_pass, sum, std::min(C.P.max_solver_iterations, 200));
     HIPCHK(hipGetLastError());
 }
 

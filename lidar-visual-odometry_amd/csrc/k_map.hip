@@ -231,26 +231,131 @@ __global__ void __launch_bounds__(256) k_map_assoc(
                 exp, tabs);
 }
 
-// Scan-to-map registration (aloam_s2m_*): one rank's slots [s0, s1) of the stacks at pose x.
-__global__ void __launch_bounds__(256) k_s2m_assoc(
-    const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc, int s0, int s1, const double* __restrict__ x,
-    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
-    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    aloam_factor* __restrict__ out, unsigned long long* cand_count) {
+// Scan-to-map registration association (aloam_s2m_*). Each wave takes 8 NB stack points per pass:
+// NB batches of 8 lane groups run the 5-NN and park the neighbour positions in LDS, then 8 NB lanes
+// fit one point each (the fp64 line / plane fits on many lanes instead of one per group).
+// The 5-NN first searches the 3x3x3 block of a fine grid of the map (edge ~0.3 m): when its 5th
+// neighbour is closer than 0.99 fine cells, no point outside the block can be closer, so the result is
+// the exact 5-NN (same order, same ties by index). Groups it does not settle search the 1.025 m grid's
+// block, which holds the whole 1 m ball (laserMapping.cpp:583-584,649-650). On a dense map (C4: ~1000
+// points in the coarse block, the 5 neighbours within ~0.2 m) the fine block streams ~20x fewer points.
+struct KindGrids { const GridDesc* gd; const int* cs; const float4* sp; const int* si; };
+
+__device__ __forceinline__ int knn5_fine_coarse(const KindGrids& fc, const KindGrids& fs, const KindGrids& cc, const KindGrids& cs,
+                                                bool use_fine, bool corner, const float4 sel, bool live, int* pos,
+                                                const float4** sp, int* tab) {
+    int idx[5], found = 0;
+    float d2[5];
+    bool need = live;
+    *sp = corner ? cc.sp : cs.sp;
+    if (use_fine) {                                    // kernel-uniform
+        const KindGrids& f = corner ? fc : fs;
+        const GridDesc gd = *f.gd;
+        found = group_knn27<5, AG, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, f.cs, f.sp, f.si, sel.x, sel.y,
+                                         sel.z, 1.0f, live, pos, d2, idx, nullptr, tab, gd.n);
+        const float lim = 0.99f * gd.cell;
+        need = live && !(found == 5 && d2[4] < lim * lim);
+        *sp = f.sp;
+    }
+    if (__any(need)) {                                 // wave-uniform: every lane takes part in the group search
+        const KindGrids& c = corner ? cc : cs;
+        const GridDesc gd = *c.gd;
+        int p2[5], i2[5];
+        float e2[5];
+        const int f2 = group_knn27<5, AG, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, c.cs, c.sp, c.si, sel.x,
+                                                sel.y, sel.z, 1.0f, need, p2, e2, i2, nullptr, tab, gd.n);
+        if (need) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) pos[k] = p2[k];
+            found = f2;
+            *sp = c.sp;
+        }
+    }
+    return found;
+}
+
+template <int NB>
+__device__ __forceinline__ void assoc_slots_batched(const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int nc,
+                                                    const int s0, const int s1, const double* par, const KindGrids fc,
+                                                    const KindGrids fs, const KindGrids cc, const KindGrids cs, bool use_fine,
+                                                    aloam_factor* __restrict__ out, int (*tabs)[20], int (*park)[6]) {
+    const bool lead = (lane_id() & (AG - 1)) == 0;
+    const int per_wave = WAVE / AG;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
+    constexpr int PTS = NB * (WAVE / AG);
+    int (*my)[6] = park + (threadIdx.x / WAVE) * PTS;    // this wave's parking slots
+    for (int base = s0 + wave * PTS; base < s1; base += nwaves * PTS) {   // wave-uniform trip count
+#pragma unroll 1
+        for (int b = 0; b < NB; b++) {
+            const int slot = b * per_wave + lane_id() / AG;
+            const int qi = base + slot;
+            const bool live = qi < s1;
+            const bool corner = qi < nc;
+            const int li = corner ? qi : qi - nc;
+            const float4 po = live ? (corner ? cstack[li] : sstack[li]) : make_float4(0, 0, 0, 0);
+            const float4 sel = associate_to_map(par, po);
+            int pos[5];
+            const float4* sp;
+            const int found = knn5_fine_coarse(fc, fs, cc, cs, use_fine, corner, sel, live, pos, &sp, tabs[threadIdx.x / AG]);
+            if (lead) {
+#pragma unroll
+                for (int k = 0; k < 5; k++) my[slot][k] = pos[k];
+                // found | which sorted copy the positions index (1: fine grid) << 8
+                my[slot][5] = found | ((use_fine && sp == (corner ? fc.sp : fs.sp)) ? 256 : 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const int qi = base + lane_id();
+        if (lane_id() < PTS && qi < s1) {
+            const bool corner = qi < nc;
+            const float4 po = corner ? cstack[qi] : sstack[qi - nc];
+            int pos[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) pos[k] = my[lane_id()][k];
+            const int fl = my[lane_id()][5];
+            const float4* sp = (fl & 256) ? (corner ? fc.sp : fs.sp) : (corner ? cc.sp : cs.sp);
+            aloam_factor f;
+            f.type = -1; f.pad = 0;
+            if ((fl & 255) == 5) fit_factor(corner, po, sp, pos, f);
+            out[qi] = f;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// one rank's slots [s0, s1) of the stacks at pose x; NB = 1: latency regime, NB > 1: throughput regime
+template <int NB>
+__global__ void __launch_bounds__(256) k_s2m_assoc(const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc,
+                                                   int s0, int s1, const double* __restrict__ x, KindGrids fc, KindGrids fs,
+                                                   KindGrids cc, KindGrids cs, int use_fine, aloam_factor* __restrict__ out) {
     __shared__ int tabs[256 / AG][20];
+    __shared__ int park[4 * NB * (WAVE / AG)][6];
     double par[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) par[i] = x[i];
-    assoc_slots(cstack, sstack, nc, s0, s1, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, nullptr, cand_count, 0, tabs);
+    assoc_slots_batched<NB>(cstack, sstack, nc, s0, s1, par, fc, fs, cc, cs, use_fine != 0, out, tabs, park);
 }
 
 void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
-                      aloam_factor* out, unsigned long long* cand) {
+                      const Grid* gcf, const Grid* gsf, aloam_factor* out) {
     if (s1 <= s0) return;
-    const int waves = (s1 - s0 + WAVE / AG - 1) / (WAVE / AG);
-    const int blocks = std::max(1, std::min(4096, (waves + 3) / 4));
-    k_s2m_assoc<<<blocks, 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, gc.desc, gc.cell_start, gc.pts, gc.idx, gs.desc,
-                                                gs.cell_start, gs.pts, gs.idx, out, cand);
+    const char* bm = getenv("ALOAM_S2M_BATCH_MIN");                 // regime threshold (tests force either path)
+    const int batch_min = bm ? atoi(bm) : 65536;
+    const bool fine = gcf && gsf;
+    const KindGrids cc{gc.desc, gc.cell_start, gc.pts, gc.idx}, cs{gs.desc, gs.cell_start, gs.pts, gs.idx};
+    const KindGrids fc = fine ? KindGrids{gcf->desc, gcf->cell_start, gcf->pts, gcf->idx} : cc;
+    const KindGrids fs = fine ? KindGrids{gsf->desc, gsf->cell_start, gsf->pts, gsf->idx} : cs;
+    if (s1 - s0 >= batch_min) {      // throughput regime: 16 points per wave pass, fits on 16 lanes
+        constexpr int NB = 2;
+        const int waves = (s1 - s0 + 8 * NB - 1) / (8 * NB);
+        const int blocks = std::max(1, std::min(16384, (waves + 3) / 4));
+        k_s2m_assoc<NB><<<blocks, 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, fc, fs, cc, cs, fine, out);
+    } else {                         // latency regime: 8 points per wave pass
+        const int waves = (s1 - s0 + 7) / 8;
+        const int blocks = std::max(1, std::min(4096, (waves + 3) / 4));
+        k_s2m_assoc<1><<<blocks, 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, fc, fs, cc, cs, fine, out);
+    }
     HIPCHK(hipGetLastError());
 }
 

@@ -3,7 +3,8 @@
 // The registration half of laserMapping::process (src/laserMapping.cpp:556-727) against a map the
 // caller supplies: per round, k_s2m_assoc (k_map.hip: pointAssociateToMap + 5-NN within 1 m + line /
 // plane fit, 8 lanes per query) over this rank's slots, then one Ceres-equivalent Solve as
-// max_iter + 1 passes of {k_s2m_partials -> exchange -> k_s2m_tail} (k_lm.hip). The exchange is the
+// max_iter + 1 passes of {k_s2m_pass -> exchange} + k_s2m_final (k_lm.hip; each pass launch first
+// finishes the previous pass's LM step in every workgroup). The exchange is the
 // only collective of the path: one 32-double record per fixed slot block,
 //   * world 1:   none (the tail reads the local records),
 //   * RCCL:      ncclAllGather on the context's stream (one process per GPU, xGMI),
@@ -23,10 +24,11 @@
 namespace aloam {
 
 void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
-                      aloam_factor* out, unsigned long long* cand);
-void s2m_partials_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const LMState* st,
-                         const double* x, int pass, double* send);
-void s2m_tail_launch(Ctx& C, const double* recs, int nrec, LMState* st, double* x, int pass, aloam_lm_summary* out, int* round_cnt);
+                      const Grid* gcf, const Grid* gsf, aloam_factor* out);
+void s2m_pass_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const double* prev,
+                     const LMState* st_in, LMState* st_out, const double* x0, int pass, aloam_lm_summary* sum, int* round_cnt,
+                     double* send);
+void s2m_final_launch(Ctx& C, const double* prev, int nrec, const LMState* st_in, double* x, int last_pass, aloam_lm_summary* sum);
 
 constexpr int S2M_REC = 32;                     // doubles per record (k_lm.hip)
 constexpr int NREC = ALOAM_S2M_RECORDS;
@@ -42,9 +44,11 @@ struct S2M {
     int cap_mc = 0, cap_ms = 0, cap_qc = 0, cap_qs = 0, cap_f = 0;
     float4 *d_mc = nullptr, *d_ms = nullptr, *d_qc = nullptr, *d_qs = nullptr;
     int* d_n = nullptr;                         // [2] map sizes (grid builds read them on the device)
-    Grid gc, gs;
+    Grid gc, gs;                                // 1.025 m cells: the 3x3x3 block holds the 1 m ball
+    Grid gcf, gsf;                              // fine cells (~0.3 m): first-phase 5-NN (k_map.hip)
+    bool fine = false, shared = false;          // fine grids built; corner map == surf map (one set of grids)
     aloam_factor* d_f = nullptr;
-    LMState* d_st = nullptr;
+    LMState* d_st = nullptr;                    // [2] LM state, double-buffered across pass launches
     double* d_x = nullptr;                      // [8] parameters (laserMapping.cpp:129)
     double* d_send = nullptr;                   // 2 x NREC records (pass parity: group-mode reuse guard)
     double* d_recv = nullptr;                   // RECV_CAP records
@@ -105,7 +109,7 @@ static S2M& s2m_of(Ctx& C) {
         S2M* S = new S2M();
         C.s2m = S;
         S->d_n = (int*)dalloc(C, sizeof(int) * 2);
-        S->d_st = (LMState*)dalloc(C, sizeof(LMState));
+        S->d_st = (LMState*)dalloc(C, 2 * sizeof(LMState));
         S->d_x = (double*)dalloc(C, sizeof(double) * 8);
         S->d_send = (double*)dalloc(C, sizeof(double) * 2 * NREC * S2M_REC);
         S->d_recv = (double*)dalloc(C, sizeof(double) * RECV_CAP * S2M_REC);
@@ -144,13 +148,32 @@ void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns,
     S.d_ms = grow(C, S.d_ms, S.cap_ms, std::max(ns, 1));
     copy_in(C, S.d_mc, corner, nc, flags);
     copy_in(C, S.d_ms, surf, ns, flags);
-    // FromMap indices: 1.025 m cells (5-NN within 1 m: the 27-cell block holds the ball), sorted copies
-    if (S.gc.cap < std::max(nc, 1)) { Grid g{}; grid_alloc(C, g, std::max(std::max(nc, 1), 2 * S.gc.cap), 1.0f * 1.025f, 1, true); S.gc = g; }
-    if (S.gs.cap < std::max(ns, 1)) { Grid g{}; grid_alloc(C, g, std::max(std::max(ns, 1), 2 * S.gs.cap), 1.0f * 1.025f, 1, true); S.gs = g; }
+    // FromMap indices: 1.025 m cells (5-NN within 1 m: the 27-cell block holds the ball), sorted copies;
+    // plus fine grids for the first search phase. One set when the corner and surf maps are one array.
+    S.shared = corner == surf && nc == ns;
+    const char* fe = getenv("ALOAM_S2M_FINE_CELL");
+    const float fine_cell = fe ? (float)atof(fe) : 0.3f;
+    S.fine = fine_cell > 0.f;
+    auto need = [&](Grid& g, int n, float cell) {
+        if (g.cap < std::max(n, 1)) { Grid ng{}; grid_alloc(C, ng, std::max(std::max(n, 1), 2 * g.cap), cell, 1, true); g = ng; }
+        g.min_cell = cell;
+    };
+    need(S.gc, nc, 1.0f * 1.025f);
+    if (!S.shared) need(S.gs, ns, 1.0f * 1.025f);
+    if (S.fine) {
+        need(S.gcf, nc, fine_cell);
+        if (!S.shared) need(S.gsf, ns, fine_cell);
+    }
     set_counts2(C, S.d_n, nc, ns);
-    const GridBuild gb[2] = {{&S.gc, S.d_mc, S.d_n + 0, std::max(nc, 1), nullptr, nullptr},
-                             {&S.gs, S.d_ms, S.d_n + 1, std::max(ns, 1), nullptr, nullptr}};
-    grid_build_multi(C, gb, 2);
+    GridBuild gb[4];
+    int nb = 0;
+    gb[nb++] = {&S.gc, S.d_mc, S.d_n + 0, std::max(nc, 1), nullptr, nullptr};
+    if (!S.shared) gb[nb++] = {&S.gs, S.d_ms, S.d_n + 1, std::max(ns, 1), nullptr, nullptr};
+    if (S.fine) {
+        gb[nb++] = {&S.gcf, S.d_mc, S.d_n + 0, std::max(nc, 1), nullptr, nullptr};
+        if (!S.shared) gb[nb++] = {&S.gsf, S.d_ms, S.d_n + 1, std::max(ns, 1), nullptr, nullptr};
+    }
+    grid_build_multi(C, gb, nb);
     S.nc = nc;
     S.ns = ns;
     S.have_map = true;
@@ -225,17 +248,22 @@ void s2m_register(Ctx& C, double* x, aloam_s2m_result* out) {
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
         const int max_iter = std::min(C.P.max_solver_iterations, 200);
         for (int it = 0; it < rounds; it++) {
-            s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.gs, S.d_f, nullptr);
+            s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
+                             S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
+            const double* prev = nullptr;   // the exchanged records of the previous pass
             for (int pass = 0; pass <= max_iter; pass++) {
-                s2m_partials_launch(C, S.d_f, Q, sl.per, sl.rec0, sl.rp, NREC, S.d_st, S.d_x, pass, S.d_send);
-                const double* recs = S.d_send;
+                double* send = S.d_send + (size_t)(pass & 1) * NREC * S2M_REC;
+                s2m_pass_launch(C, S.d_f, Q, sl.per, sl.rec0, sl.rp, NREC, prev, S.d_st + ((pass + 1) & 1), S.d_st + (pass & 1), S.d_x,
+                                pass, &S.d_out->lm[it], S.d_out->cnt[it], send);
                 if (rccl_exchange) {
-                    rcclchk(rccl()->all_gather(S.d_send, S.d_recv, (size_t)sl.rp * S2M_REC, ncclFloat64, (ncclComm_t)C.shard_comm,
+                    rcclchk(rccl()->all_gather(send, S.d_recv, (size_t)sl.rp * S2M_REC, ncclFloat64, (ncclComm_t)C.shard_comm,
                                                C.stream), "ncclAllGather");
-                    recs = S.d_recv;
+                    prev = S.d_recv;
+                } else {
+                    prev = send;
                 }
-                s2m_tail_launch(C, recs, NREC, S.d_st, S.d_x, pass, &S.d_out->lm[it], pass == 0 ? S.d_out->cnt[it] : nullptr);
             }
+            s2m_final_launch(C, prev, NREC, S.d_st + (max_iter & 1), S.d_x, max_iter, &S.d_out->lm[it]);
         }
     }
     finish(C, rank, world, x, out, true);
@@ -258,22 +286,25 @@ void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
     if (s2m_gate(S0)) {
         const int rounds = std::min(cs[0]->P.map_rounds, ALOAM_MAX_ROUNDS);
         const int max_iter = std::min(cs[0]->P.max_solver_iterations, 200);
-        int parity = 0;
         for (int it = 0; it < rounds; it++) {
             for (int r = 0; r < world; r++) {
                 Ctx& C = *cs[r];
                 S2M& S = *C.s2m;
                 const Slice sl = slice_of(Q, r, world);
                 HIPCHK(hipSetDevice(C.device));
-                s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.gs, S.d_f, nullptr);
+                s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
+                             S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
             }
-            for (int pass = 0; pass <= max_iter; pass++, parity ^= 1) {
+            for (int pass = 0; pass <= max_iter; pass++) {
+                const int parity = pass & 1;
                 for (int r = 0; r < world; r++) {      // every rank's records of this pass
                     Ctx& C = *cs[r];
                     S2M& S = *C.s2m;
                     const Slice sl = slice_of(Q, r, world);
                     HIPCHK(hipSetDevice(C.device));
-                    s2m_partials_launch(C, S.d_f, Q, sl.per, sl.rec0, rp, NREC, S.d_st, S.d_x, pass, S.d_send + (size_t)parity * NREC * S2M_REC);
+                    s2m_pass_launch(C, S.d_f, Q, sl.per, sl.rec0, rp, NREC, pass ? S.d_recv : nullptr, S.d_st + ((pass + 1) & 1),
+                                    S.d_st + parity, S.d_x, pass, &S.d_out->lm[it], S.d_out->cnt[it],
+                                    S.d_send + (size_t)parity * NREC * S2M_REC);
                     HIPCHK(hipEventRecord(S.ev[parity], C.stream));
                 }
                 for (int r = 0; r < world; r++) {      // all-gather as peer copies into every rank's recv (rank order)
@@ -288,12 +319,12 @@ void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
                 }
                 // a rank's send[parity] is rewritten two passes later, after its stream waited for every
                 // peer's next-pass records, which those peers recorded after copying this pass's
-                for (int r = 0; r < world; r++) {
-                    Ctx& C = *cs[r];
-                    S2M& S = *C.s2m;
-                    HIPCHK(hipSetDevice(C.device));
-                    s2m_tail_launch(C, S.d_recv, NREC, S.d_st, S.d_x, pass, &S.d_out->lm[it], pass == 0 ? S.d_out->cnt[it] : nullptr);
-                }
+            }
+            for (int r = 0; r < world; r++) {
+                Ctx& C = *cs[r];
+                S2M& S = *C.s2m;
+                HIPCHK(hipSetDevice(C.device));
+                s2m_final_launch(C, S.d_recv, NREC, S.d_st + (max_iter & 1), S.d_x, max_iter, &S.d_out->lm[it]);
             }
         }
     }

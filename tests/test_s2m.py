@@ -154,3 +154,25 @@ def test_s2m_c4_scale_device_resident(gpu_ctx_factory):
     res = lvo.s2m_register_group(ctxs[1:], x0)
     for r in res:
         assert np.array_equal(r["x"].view(np.uint64), g["x"].view(np.uint64))
+
+
+@pytest.mark.parametrize("batch_min,fine_cell", [("1", "0.3"), ("1", "0"), ("100000000", "0.3"), ("100000000", "0.15")])
+def test_s2m_assoc_paths_bit_identical(gpu_ctx_factory, monkeypatch, batch_min, fine_cell):
+    """Every association path — latency (8 points per wave pass) or throughput regime (16), with or
+    without the fine-grid first phase (any fine cell) — emits the same factors: the registrations are
+    bit-identical to the plain path (latency regime, coarse grid only) and match the oracle. The map is
+    dense (0.1 m lattice) so the fine phase settles most queries."""
+    wl = small_workload(half=10.0, map_step=0.1, surf_stride=6, corner_stride=24)
+    cm, sm, cq, sq, x0, _ = wl
+    monkeypatch.setenv("ALOAM_S2M_BATCH_MIN", "100000000")
+    monkeypatch.setenv("ALOAM_S2M_FINE_CELL", "0")
+    ref = loaded_ctx(gpu_ctx_factory, wl).s2m_register(x0)
+    monkeypatch.setenv("ALOAM_S2M_BATCH_MIN", batch_min)
+    monkeypatch.setenv("ALOAM_S2M_FINE_CELL", fine_cell)
+    g = loaded_ctx(gpu_ctx_factory, wl).s2m_register(x0)
+    assert np.array_equal(g["x"].view(np.uint64), ref["x"].view(np.uint64))
+    assert g["lm"] == ref["lm"] and g["surf_num"] == ref["surf_num"] and g["corner_num"] == ref["corner_num"]
+    if batch_min == "1" and fine_cell == "0.3":
+        o = ob.s2m_register(abi.default_params(128), cm, sm, cq, sq, x0)
+        assert rel(g["x"], o["x"]) <= POSE_RTOL
+        assert g["surf_num"] == o["surf_num"] and g["corner_num"] == o["corner_num"]
