@@ -144,20 +144,27 @@ aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int sta
         delete P;
         return nullptr;
     }
-    // Disjoint CUs per stage: the front stage(s) get CUs [0, F), laserMapping [F, ncu). Concurrent
-    // latency-bound stages then stop queueing behind each other's workgroups (measured on one MI355X:
-    // 822-840 scans/s shared, 968-971 with contiguous halves; alternating runs of 1-32 CUs were in
-    // between). ALOAM_PIPE_CU_SPLIT = F overrides the default ncu / 2; 0 shares all CUs.
+    // Disjoint CUs per stage: the front stage(s) get CUs [0, F), laserMapping [F, ncu); with 3 stages
+    // scanRegistration gets [0, F3) and laserOdometry [F3, F). Concurrent latency-bound stages then stop
+    // queueing behind each other's workgroups (measured on one MI355X, 2 stages: 822-840 scans/s shared,
+    // 968-971 with contiguous halves; alternating runs of 1-32 CUs were in between).
+    // ALOAM_PIPE_CU_SPLIT = F (default ncu / 2; 0 shares all CUs), ALOAM_PIPE_CU_SPLIT3 = F3 (default F / 3).
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
         const int ncu = prop.multiProcessorCount, nw = (ncu + 31) / 32;
         const char* env = std::getenv("ALOAM_PIPE_CU_SPLIT");
         const int F = env ? std::atoi(env) : ncu / 2;
-        if (F > 0 && F < ncu) {
-            std::vector<unsigned> m0(nw, 0u), m1(nw, 0u);
-            for (int c = 0; c < ncu; c++) (c < F ? m0 : m1)[c / 32] |= 1u << (c % 32);
-            if (aloam_set_cu_mask(P->front, m0.data(), nw) || (stages == 3 && aloam_set_cu_mask(P->odom, m0.data(), nw)) ||
-                aloam_set_cu_mask(P->back, m1.data(), nw)) {
+        const char* env3 = std::getenv("ALOAM_PIPE_CU_SPLIT3");
+        const int F3 = env3 ? std::atoi(env3) : F / 3;
+        if (F > 0 && F < ncu && (stages == 2 || (F3 > 0 && F3 < F))) {
+            auto range = [&](int a, int b) {
+                std::vector<unsigned> m(nw, 0u);
+                for (int c = a; c < b; c++) m[c / 32] |= 1u << (c % 32);
+                return m;
+            };
+            const std::vector<unsigned> mf = range(0, stages == 3 ? F3 : F), mo = range(F3, F), mm = range(F, ncu);
+            if (aloam_set_cu_mask(P->front, mf.data(), nw) || (stages == 3 && aloam_set_cu_mask(P->odom, mo.data(), nw)) ||
+                aloam_set_cu_mask(P->back, mm.data(), nw)) {
                 aloam_destroy(P->back);
                 if (stages == 3) aloam_destroy(P->odom);
                 aloam_destroy(P->front);
