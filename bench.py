@@ -364,6 +364,10 @@ def main():
                     "traffic = rocprofv3 FETCH_SIZE per launch (KiB x1024 x2 for gfx950; Infinity-Cache hits included)",
             "queries_per_s": round(c4["queries"] / (c4["ms"] * 1e-3), 0),
             "found5_frac": round(c4["found5"], 4),
+            # where the candidate stream is actually served from (MI355X_MICROARCH.md: L2 4 MiB per XCD,
+            # 34.5 TB/s aggregate; random rows of a 38 MB table from the Infinity Cache: 8.6 TB/s chip-wide)
+            "cache_roofline": {"level": "L2 + Infinity Cache (33 MB map)", "achieved_TBps": round(ach / 1000.0, 2),
+                               "infinity_cache_gather_TBps": 8.6, "l2_aggregate_TBps": 34.5},
         }
 
     if args.c4_reg_steps > 0:
