@@ -73,7 +73,18 @@ def c4_traffic(timeout_s=240):
     if not shutil.which("rocprofv3"):
         return None
     out = tempfile.mkdtemp(prefix="c4pmc_", dir="/tmp")
-    env = dict(os.environ, TMPDIR="/tmp")
+    # the child is a single-process run on this rank's GPU: drop the torchrun rendezvous variables, or
+    # under --gpus N it would try to join the job's process group as a second rank 0
+    dist_vars = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+                 "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+                 "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE", "ROLE_NAME")
+    env = {k: v for k, v in os.environ.items() if k not in dist_vars}
+    env["TMPDIR"] = "/tmp"
+    local = os.environ.get("LOCAL_RANK")
+    if local is not None:   # keep the child on this rank's GPU
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+        ids = vis.split(",") if vis else None
+        env["HIP_VISIBLE_DEVICES"] = ids[int(local)] if ids and int(local) < len(ids) else local
     cmd = ["rocprofv3", "--pmc", "FETCH_SIZE", "-d", out, "-o", "run", "--output-format", "csv", "--",
            sys.executable, os.path.abspath(__file__), "--c4-only", "--c4-launches", "3"]
     try:
@@ -180,11 +191,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 flow on a one-GPU box (never set by the driver): every rank on GPU 0 with the
+    # gloo backend; RCCL refuses two ranks on one GPU, so the sharded registration reports its error
+    rehearsal = os.environ.get("ALOAM_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local_rank = 0
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group("gloo" if rehearsal else "nccl", rank=rank, world_size=world)
     torch.cuda.set_device(local_rank)
 
     from lvo_amd_loader import lvo
