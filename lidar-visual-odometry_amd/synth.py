@@ -9,6 +9,7 @@ Configs (BASELINE.json ``configs``):
   * ``hdl64``  — C2/C3: HDL-64E elevation table of scanRegistration.cpp:189-192, 2,083 azimuths
                  (~100-125k points after the 5 m minimum range)
   * ``l128``   — C4: 128 lines uniform -25..+15 deg, 1,875 azimuths (~240k points)
+  * ``c5``     — C5 stand-in: HDL-64E, 271 frames of a straight road (seed 5; KITTI-04 is not on the box)
 """
 import ctypes as C
 import os
@@ -29,8 +30,11 @@ PRESETS = {
     "vlp16": dict(model=16, n_azimuth=1800, range_sigma=0.02, max_range=100.0, seed=1, speed=1.0, yaw_amp_deg=2.0),
     "hdl64": dict(model=64, n_azimuth=2083, range_sigma=0.02, max_range=120.0, seed=2, speed=1.0, yaw_amp_deg=2.0),
     "l128": dict(model=128, n_azimuth=1875, range_sigma=0.02, max_range=120.0, seed=4, speed=1.0, yaw_amp_deg=2.0),
+    # C5 stand-in (KITTI-04 is 271 frames of a straight road; no KITTI data on the box)
+    "c5": dict(model=64, n_azimuth=2083, range_sigma=0.02, max_range=120.0, seed=5, speed=1.0, yaw_amp_deg=0.0),
 }
-SCAN_LINES = {"vlp16": 16, "hdl64": 64, "l128": 128}
+SCAN_LINES = {"vlp16": 16, "hdl64": 64, "l128": 128, "c5": 64}
+C5_FRAMES = 271
 
 _lib = None
 
