@@ -242,7 +242,7 @@ def test_pipeline_sequence_ate(gpu_ctx_factory):
         tg.append(mg["t_w_curr"])
         to.append(mo["t_w_curr"])
     ate = np.sqrt(np.mean(np.sum((np.array(tg) - np.array(to)) ** 2, axis=1)))
-    print(f"C5 ATE delta vs oracle {ate:.3e} m")
+    print(f"ATE delta vs oracle {ate:.3e} m")
     assert ate <= 1e-4, ate
 
 
