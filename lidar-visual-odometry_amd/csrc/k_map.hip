@@ -705,10 +705,12 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
         else run_graph(C, 2, nullptr, nullptr, rounds, [&] { issue(false, hint); });
     }
     k_map_update<<<1, 1, 0, st>>>(C.d_map);
-    fork_lane1(C);
-    rebuild_map(C, 0, ub_c, C.d_cstack, C.d_stack_n + 0, C.P.mapping_line_resolution);
-    rebuild_map(C, 1, ub_s, C.d_sstack, C.d_stack_n + 1, C.P.mapping_plane_resolution);
-    join_lane1(C);
+    if (!(g_exp & 4)) {              // (profiling experiment 4: skip the map update — results invalid)
+        fork_lane1(C);
+        rebuild_map(C, 0, ub_c, C.d_cstack, C.d_stack_n + 0, C.P.mapping_line_resolution);
+        rebuild_map(C, 1, ub_s, C.d_sstack, C.d_stack_n + 1, C.P.mapping_plane_resolution);
+        join_lane1(C);
+    }
     if (C.n_map_full_in > 0)
         k_map_register<<<(C.n_map_full_in + MB - 1) / MB, MB, 0, st>>>(C.d_map_full_in, C.n_map_full_in, C.d_map, C.d_registered);
     HIPCHK(hipGetLastError());
