@@ -509,10 +509,20 @@ __global__ void k_cubevox_bbox(const float4* __restrict__ B, CubeArrays a, const
     if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     __syncthreads();
     unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-    for (int p = a.off[c] + threadIdx.x; p < a.off[c + 1]; p += blockDim.x) {
-        const float4 q = B[p];
-        const unsigned u[3] = {f2ord(q.x), f2ord(q.y), f2ord(q.z)};
-        for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], u[d]); mx[d] = max(mx[d], u[d]); }
+    const int p0 = a.off[c], p1 = a.off[c + 1];
+    constexpr int U = 4;                                   // 4 independent loads in flight per thread
+    for (int base = p0 + threadIdx.x; base < p1; base += U * blockDim.x) {
+        float4 q[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int p = base + u * blockDim.x;
+            q[u] = p < p1 ? B[p] : B[base];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const unsigned v[3] = {f2ord(q[u].x), f2ord(q[u].y), f2ord(q[u].z)};
+            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+        }
     }
     for (int d = 0; d < 3; d++) {
         const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
@@ -612,8 +622,9 @@ __global__ void k_scan_small_m(int* a, int nb, int* total) {
 // ------------------------------------------------------------------------------------------
 static int nblk(int n) { return std::max(1, std::min(2048, (n + MB - 1) / MB)); }
 
+static int g_map_exp();
 static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, const int* d_stack_n, float leaf) {
-    hipStream_t st = which ? C.stream2 : C.stream;          // the kinds rebuild concurrently
+    hipStream_t st = (which && !(g_map_exp() & 8)) ? C.stream2 : C.stream;   // the kinds rebuild concurrently
     KindScratch& K = C.ks[which];
     float4* A = which == 0 ? C.d_mc : C.d_ms;
     int* Acube = which == 0 ? C.d_mc_cube : C.d_ms_cube;
@@ -631,7 +642,10 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     unsigned* k1 = (unsigned*)K.vkeys;
     unsigned* k2 = (unsigned*)K.vkeys2;
     k_map_insert<<<nblk(ub_new), MB, 0, st>>>(stack, d_stack_n, ub_new, C.d_map, K.ins_pts, k1, K.ins_val);
-    if (ub_new > 0) stable_sort_pairs(C, k1, k2, K.ins_val, K.ins_val2, ub_new, 13, which);
+    if (ub_new > 0) {
+        size_t bytes = C.sort_tmp_bytes;
+        HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, k1, k2, K.ins_val, K.ins_val2, (unsigned)ub_new, 0, 13, st));
+    }
     k_cube_reset<<<(CUBE_N + 1 + 255) / 256, 256, 0, st>>>(a);
     k_cube_count_old<<<nblk(n_old_ub), MB, 0, st>>>(Acube, d_n_old, a);
     k_cube_count_new<<<nblk(ub_new), MB, 0, st>>>(k2, ub_new, a);
@@ -665,6 +679,7 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
 
 // The whole laserMapping frame; results are read back by the caller (aloam_api.hip).
 static const int g_exp = getenv("ALOAM_EXP") ? atoi(getenv("ALOAM_EXP")) : 0;   // profiling experiments only
+static int g_map_exp() { return g_exp; }
 void map_frame_launch(Ctx& C, aloam_map_result* R) {
     hipStream_t st = C.stream;
     (void)R;

@@ -338,7 +338,10 @@ static const int g_odom_exp = getenv("ALOAM_ODOM_EXP") ? atoi(getenv("ALOAM_ODOM
 // the device-side count exit at once
 void odom_round_search(Ctx& C, int round) {
     const int threads = 256;
-    const int nb = (MAXL * (LINE_SHARP_CAP + LINE_FLAT_CAP) * WAVE + threads - 1) / threads;
+    // upper bound of the live queries: this context's scan lines x the per-line selection caps (the
+    // counts themselves are on the device, so the launch stays graph-replayable)
+    const int lines = std::max(1, std::min(MAXL, C.P.scan_line));
+    const int nb = (lines * (LINE_SHARP_CAP + LINE_FLAT_CAP) * WAVE + threads - 1) / threads;
     k_odom_search<<<nb, threads, 0, C.stream>>>(
         C.d_sharp, C.d_flat, C.d_odom_nq, C.d_corner_last, C.d_surf_last, C.d_last_n,
         C.g_corner_last.desc, C.g_corner_last.cell_start, C.g_corner_last.pts, C.g_corner_last.idx,
