@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
@@ -383,12 +384,28 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
     hipStream_t st = C.stream;
     if (C.profiling) HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long) * 2, st));
     prof_mark(C, 4);
+    static const bool host_timing = getenv("ALOAM_HOST_TIMING") != nullptr;   // profiling aid
+    const auto th0 = std::chrono::steady_clock::now();
     map_frame_launch(C, &r);
+    const auto th1 = std::chrono::steady_clock::now();
     prof_mark(C, 5);
     // map state, counts, summaries, sizes: one copy of the results block into the pinned mirror
     HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, sizeof(DevOut), hipMemcpyDeviceToHost, st));
     sync(C);
     C.h_map = C.h_out->map;
+    if (host_timing) {
+        static double acc_issue = 0, acc_total = 0, acc_pre = 0;
+        static int nfr = 0, seen = 0;
+        const auto th2 = std::chrono::steady_clock::now();
+        if (++seen > 20) {               // past graph instantiation and allocation
+            acc_issue += std::chrono::duration<double, std::micro>(th1 - th0).count();
+            acc_total += std::chrono::duration<double, std::micro>(th2 - th0).count();
+            acc_pre += std::chrono::duration<double, std::micro>(C.t_rounds_issued - th0).count();
+            if (++nfr % 40 == 0)
+                std::fprintf(stderr, "[aloam host] mapping: issue until rounds %.1f us, whole issue %.1f us, issue+wait %.1f us (mean of %d)\n",
+                             acc_pre / nfr, acc_issue / nfr, acc_total / nfr, nfr);
+        }
+    }
     const int* cnt = C.h_out->round_cnt + 2 * ALOAM_MAX_ROUNDS;
     std::memcpy(r.lm, C.h_out->lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
     const int* mapn = C.h_out->map_n;

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <chrono>
 #include <functional>
 #include <string>
 #include <vector>
@@ -217,6 +218,7 @@ struct Ctx {
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling
     int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
+    std::chrono::steady_clock::time_point t_rounds_issued{};   // host-issue profiling (ALOAM_HOST_TIMING)
 
     // ---- scan-to-map registration (k_s2m.hip) and its shard communicator ----
     struct S2M* s2m = nullptr;       // allocated by the first aloam_s2m_* call
@@ -265,7 +267,9 @@ void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, i
 size_t voxel_sort_tmp_bytes(int cap);
 size_t cube_sort_tmp_bytes(int cap);
 // lane 0: C.stream + the primary scratch; lane 1: C.stream2 + the second scratch set
-void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane = 0);
+void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane = 0,
+                       bool hdr_armed = false);
+unsigned* voxel_hdr(Ctx& C, int lane);   // bb[6] + nrun of the lane's VoxelGrid header (device)
 void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit, int lane = 0);
 void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so far
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far

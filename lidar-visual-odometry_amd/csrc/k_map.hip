@@ -42,8 +42,15 @@ __device__ inline float4 associate_to_map(const double* par, float4 p) {   // :1
     return make_float4((float)(r.x + par[4]), (float)(r.y + par[5]), (float)(r.z + par[6]), p.w);
 }
 
-__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid) {
+// also zeroes this frame's mapping round counters and arms the stacks' VoxelGrid headers (saves three
+// launches on the host-issue-bound part of the frame)
+__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* round_cnt, unsigned* vox_bb0, unsigned* vox_bb1) {
     __shared__ int valid_num;
+    if (threadIdx.x < 2 * ALOAM_MAX_ROUNDS) round_cnt[threadIdx.x] = 0;
+    if (threadIdx.x < 8) {                      // VoxHdr {bb[6], nrun, pad} of both lanes
+        const unsigned v = threadIdx.x < 3 ? 0xffffffffu : 0u;
+        if (threadIdx.x < 7) { vox_bb0[threadIdx.x] = v; vox_bb1[threadIdx.x] = v; }
+    }
     if (threadIdx.x == 0) {
         // transformAssociateToMap (:142-146)
         const dquat qm{m->q_wmap_wodom[0], m->q_wmap_wodom[1], m->q_wmap_wodom[2], m->q_wmap_wodom[3]};
@@ -81,10 +88,11 @@ __global__ void k_map_prepare(MapState* m, unsigned char* cube_valid) {
 }
 
 // recentring: cube (i,j,k) -> (i+si, j+sj, k+sk); cubes pushed off the grid are cleared (:325-507)
-__global__ void k_map_shift(int* __restrict__ cube, const int* d_n, const MapState* m) {
+__global__ void k_map_shift(int* __restrict__ cube_c, int* __restrict__ cube_s, const int* d_n, const MapState* m) {
     const int si = m->shift[0], sj = m->shift[1], sk = m->shift[2];
     if (si == 0 && sj == 0 && sk == 0) return;
-    const int n = *d_n;
+    int* cube = blockIdx.y == 0 ? cube_c : cube_s;     // y = map kind
+    const int n = d_n[blockIdx.y];
     for (int p = blockIdx.x * MB + threadIdx.x; p < n; p += gridDim.x * MB) {
         int c = cube[p];
         if (c < 0) continue;
@@ -684,20 +692,19 @@ void map_frame_launch(Ctx& C, aloam_map_result* R) {
     hipStream_t st = C.stream;
     (void)R;
     const int ub_c = C.n_map_corner_in, ub_s = C.n_map_surf_in;
-    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid);
-    k_map_shift<<<nblk(C.n_mc), MB, 0, st>>>(C.d_mc_cube, C.d_map_n + 0, C.d_map);
-    k_map_shift<<<nblk(C.n_ms), MB, 0, st>>>(C.d_ms_cube, C.d_map_n + 1, C.d_map);
+    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, voxel_hdr(C, 0), voxel_hdr(C, 1));
+    k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
     const GridBuild gb[2] = {{&C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid},
                              {&C.g_map_surf, C.d_ms, C.d_map_n + 1, std::max(C.n_ms, 1), C.d_ms_cube, C.d_cube_valid}};
     grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
     // stacks (:542-550)
     fork_lane1(C);
-    voxel_grid_sorted(C, C.d_map_corner_in, C.d_map_in_n + 0, ub_c, C.P.mapping_line_resolution, C.d_cstack, C.d_stack_n + 0, 0);
-    voxel_grid_sorted(C, C.d_map_surf_in, C.d_map_in_n + 1, ub_s, C.P.mapping_plane_resolution, C.d_sstack, C.d_stack_n + 1, 1);
+    voxel_grid_sorted(C, C.d_map_corner_in, C.d_map_in_n + 0, ub_c, C.P.mapping_line_resolution, C.d_cstack, C.d_stack_n + 0, 0, true);
+    voxel_grid_sorted(C, C.d_map_surf_in, C.d_map_in_n + 1, ub_s, C.P.mapping_plane_resolution, C.d_sstack, C.d_stack_n + 1, 1, true);
     join_lane1(C);
     const int nq = ub_c + ub_s;
-    HIPCHK(hipMemsetAsync(C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, 0, sizeof(int) * 2 * ALOAM_MAX_ROUNDS, st));
+    C.t_rounds_issued = std::chrono::steady_clock::now();
     if (nq > 0) {
         if (nq > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity exceeded"};
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);

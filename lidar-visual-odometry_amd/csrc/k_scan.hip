@@ -441,16 +441,22 @@ __device__ void bitonic_sort_reg4(unsigned long long* k, int n2) {
 #ifdef ALOAM_LF_TIMING
 __device__ unsigned long long g_lf_ts[64][8];      // micro-benchmark only: per-line phase stamps
 #define LF_TS(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts[blockIdx.x][k] = wall_clock64(); } while (0)
+__device__ unsigned long long g_lf_ts2[64][16];     // greedy: per-segment stamps (corners, flats)
+#define LF_TS2(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts2[blockIdx.x][k] = wall_clock64(); } while (0)
+extern "C" int aloam_dbg_lf_ts2(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_ts2), sizeof(g_lf_ts2)); }
 extern "C" int aloam_dbg_lf_ts(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_ts), sizeof(g_lf_ts)); }
 #else
 #define LF_TS(k) do { } while (0)
+#define LF_TS2(k) do { } while (0)
 #endif
-__global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__ cloud, const float* __restrict__ gcurv,
+// The body, instantiated per storage class of the line's arrays: with LDS lines the pointers are
+// provably LDS, so the compiler emits ds_* instructions instead of generic flat accesses.
+template <bool BIG>
+__device__ __forceinline__ void line_features_body(const float4* __restrict__ cloud, const float* __restrict__ gcurv,
                                                       const ScanMeta* meta, int N_SCANS,
                                                       float4* g_xyz, unsigned long long* g_keys, int* g_i,
                                                       int* line_sharp, int* line_lsharp, int* line_flat, int* line_cnt,
-                                                      float4* line_lf) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+                                                      float4* line_lf, unsigned char* smem_raw) {
     // all LDS is dynamic (Guideline 17: no statics ahead of the dynamic base)
     struct LineShared { int flag, ncand, nrun, cnt[3]; unsigned bb[6]; int wsum[LT / WAVE]; int tie[6]; };
     LineShared& SH = *(LineShared*)smem_raw;
@@ -467,22 +473,22 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         if (threadIdx.x < 4) cnt_out[threadIdx.x] = 0;
         return;
     }
-    const bool big = nl > LINE_LDS_CAP;
+    constexpr bool big = BIG;              // lines above the LDS cap keep their arrays in global scratch
     // carve LDS (or global scratch at the line's offset for oversized lines)
     float *X, *Y, *Z, *Cv;
     int* S;                 // sorted global indices per segment position
-    volatile int8_t* picked;
+    int8_t* picked;                   // ordered by the fence at the end of every greedy chunk
     int8_t* label;
     unsigned* gapw;         // bit i of word i/32: pair (i, i+1) is a suppression stop
     unsigned long long* keys;
-    if (!big) {
+    if constexpr (!big) {
         X = (float*)smem;
         Y = X + LINE_LDS_CAP;
         Z = Y + LINE_LDS_CAP;
         Cv = Z + LINE_LDS_CAP;
         S = (int*)(Cv + LINE_LDS_CAP);
         keys = (unsigned long long*)(S + LINE_LDS_CAP);
-        picked = (volatile int8_t*)(keys + LINE_LDS_CAP);
+        picked = (int8_t*)(keys + LINE_LDS_CAP);
         label = (int8_t*)(picked + LINE_LDS_CAP);
         gapw = (unsigned*)(label + LINE_LDS_CAP);
     } else {
@@ -493,7 +499,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         Cv = gx + 3 * (size_t)meta->cloud_size + off0;
         S = g_i + off0;
         keys = g_keys + 2 * (size_t)off0;   // 2x room for the power-of-two padding
-        picked = (volatile int8_t*)(g_i + (size_t)meta->cloud_size + off0);
+        picked = (int8_t*)(g_i + (size_t)meta->cloud_size + off0);
         label = (int8_t*)(g_i + 2 * (size_t)meta->cloud_size + off0);
         gapw = (unsigned*)((int8_t*)(g_i + (size_t)meta->cloud_size + off0) + ((nl + 3) & ~3));   // rest of picked's int slab
     }
@@ -584,6 +590,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
     if (threadIdx.x < WAVE) {
         const int lane = threadIdx.x;
         int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+        int r_sharp = 0, r_ls0 = 0, r_ls1 = 0, r_flat = 0;     // list slots lane, lane + 64
         // suppression extents of line position p: marks p+1..p+nf and p-1..p-nb (:321-338)
         auto extents = [&](int p, int& nf, int& nbk) {
             const int q0 = p - 5;                                              // pairs p-5 .. p+4
@@ -612,9 +619,14 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                 if (!__ballot(cv_ok)) break;                                   // sorted: nothing > 0.1 remains
                 int nf = 0, nbk = 0;
                 if (cv_ok) extents(ind - off0, nf, nbk);
+                // the chunk's picked flags live in a register from here on: a pick at P with extents
+                // (pf, pb) marks exactly the line positions P-pb .. P+pf (itself included), so each lane
+                // updates its own flag without an LDS round trip; the LDS flags are still written for
+                // later chunks and the flat pass (read after the fence at the end of the chunk)
+                bool pk = valid && picked[ind - off0] != 0;
                 int last = -1;
                 while (true) {
-                    const unsigned long long mk = __ballot(cv_ok && lane > last && picked[ind - off0] == 0);
+                    const unsigned long long mk = __ballot(cv_ok && lane > last && !pk);
                     if (!mk) break;
                     const int f = __ffsll((long long)mk) - 1;
                     last = f;
@@ -623,22 +635,23 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                     if (largest > 20) { stop = true; break; }
                     const int pf = readlane_i(nf, f), pb = readlane_i(nbk, f);
                     if (lane == 0) {
-                        if (largest <= 2) {
-                            label[indf - off0] = 2;
-                            line_sharp[line * LINE_SHARP_CAP + n_sharp] = indf;
-                        } else {
-                            label[indf - off0] = 1;
-                        }
-                        line_lsharp[line * LINE_LSHARP_CAP + n_lsharp] = indf;
+                        label[indf - off0] = largest <= 2 ? 2 : 1;
                         picked[indf - off0] = 1;
                     }
+                    // the index lists are collected in registers (slot i in lane i % 64) and stored once
+                    // after the selection: a global store inside this serial loop made every pick wait
+                    // for its completion
+                    if (largest <= 2 && lane == n_sharp) r_sharp = indf;
+                    if (lane == (n_lsharp & (WAVE - 1))) { if (n_lsharp < WAVE) r_ls0 = indf; else r_ls1 = indf; }
                     mark(indf - off0, pf, pb);
+                    pk = pk || (ind >= indf - pb && ind <= indf + pf);
                     if (largest <= 2) n_sharp++;
                     n_lsharp++;
-                    __threadfence_block();
-                    __builtin_amdgcn_wave_barrier();
                 }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
             }
+            LF_TS2(2 * j);
             // flats: from the smallest curvature; the 4th pick is not marked (:366-388)
             int smallest = 0;
             stop = false;
@@ -650,28 +663,35 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                 if (!__ballot(cv_ok)) break;                                   // sorted: nothing < 0.1 remains
                 int nf = 0, nbk = 0;
                 if (cv_ok) extents(ind - off0, nf, nbk);
+                bool pk = valid && picked[ind - off0] != 0;     // register flags, as in the corner pass
                 int last = -1;
                 while (true) {
-                    const unsigned long long mk = __ballot(cv_ok && lane > last && picked[ind - off0] == 0);
+                    const unsigned long long mk = __ballot(cv_ok && lane > last && !pk);
                     if (!mk) break;
                     const int f = __ffsll((long long)mk) - 1;
                     last = f;
                     const int indf = readlane_i(ind, f);
-                    if (lane == 0) {
-                        label[indf - off0] = -1;
-                        line_flat[line * LINE_FLAT_CAP + n_flat] = indf;
-                    }
+                    if (lane == 0) label[indf - off0] = -1;
+                    if (lane == n_flat) r_flat = indf;
                     n_flat++;
                     smallest++;
                     if (smallest >= 4) { stop = true; break; }
                     const int pf = readlane_i(nf, f), pb = readlane_i(nbk, f);
                     if (lane == 0) picked[indf - off0] = 1;
                     mark(indf - off0, pf, pb);
-                    __threadfence_block();
-                    __builtin_amdgcn_wave_barrier();
+                    pk = pk || (ind >= indf - pb && ind <= indf + pf);
                 }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
             }
+            LF_TS2(2 * j + 1);
         }
+        LF_TS2(12);
+        static_assert(LINE_SHARP_CAP <= WAVE && LINE_FLAT_CAP <= WAVE && LINE_LSHARP_CAP <= 2 * WAVE, "list slots");
+        if (lane < n_sharp) line_sharp[line * LINE_SHARP_CAP + lane] = r_sharp;
+        if (lane < n_lsharp) line_lsharp[line * LINE_LSHARP_CAP + lane] = r_ls0;
+        if (lane + WAVE < n_lsharp) line_lsharp[line * LINE_LSHARP_CAP + WAVE + lane] = r_ls1;
+        if (lane < n_flat) line_flat[line * LINE_FLAT_CAP + lane] = r_flat;
         if (lane == 0) { s_cnt[0] = n_sharp; s_cnt[1] = n_lsharp; s_cnt[2] = n_flat; }
     }
     __syncthreads();
@@ -786,6 +806,17 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
         cnt_out[0] = s_cnt[0]; cnt_out[1] = s_cnt[1]; cnt_out[2] = s_cnt[2]; cnt_out[3] = nrun;
     }
     LF_TS(7);
+}
+
+__global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__ cloud, const float* __restrict__ gcurv,
+                                                      const ScanMeta* meta, int N_SCANS,
+                                                      float4* g_xyz, unsigned long long* g_keys, int* g_i,
+                                                      int* line_sharp, int* line_lsharp, int* line_flat, int* line_cnt,
+                                                      float4* line_lf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int nl_ = meta->line_off[blockIdx.x + 1] - meta->line_off[blockIdx.x];
+    if (nl_ > LINE_LDS_CAP) line_features_body<true>(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, smem_raw);
+    else line_features_body<false>(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, smem_raw);
 }
 
 // concatenate per-line outputs in line order (:304-310,356,407)

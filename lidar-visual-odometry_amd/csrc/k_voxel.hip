@@ -108,7 +108,12 @@ __global__ void k_scan_small_v(int* a, int nb, int* total) {
     block_scan_array(a, nb, total);
 }
 
-void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane) {
+unsigned* voxel_hdr(Ctx& C, int lane) {   // the lane's VoxHdr lives behind its value buffer
+    return ((VoxHdr*)(C.ks[lane].vvals2 + C.cap_voxel))->bb;
+}
+
+void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane,
+                       bool hdr_armed) {
     hipStream_t st = lane ? C.stream2 : C.stream;
     KindScratch& K = C.ks[lane];
     if (cap_n <= 0) { HIPCHK(hipMemsetAsync(d_nout, 0, sizeof(int), st)); return; }
@@ -120,7 +125,7 @@ void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, flo
     int* heads = (int*)(K.vkeys + C.cap_voxel);      // second half of the key scratch
     const int nb = (cap_n + VB - 1) / VB;
     const int nbr = std::min(nb, 1024);
-    k_vox_init<<<1, 64, 0, st>>>(h);
+    if (!hdr_armed) k_vox_init<<<1, 64, 0, st>>>(h);   // else armed by an earlier kernel of the stream (k_map_prepare)
     k_vox_bbox<<<nbr, VB, 0, st>>>(pts, d_n, h);
     k_vox_keys<<<nbr, VB, 0, st>>>(pts, d_n, cap_n, h, leaf, k1, K.vvals);
     size_t bytes = C.sort_tmp_bytes;

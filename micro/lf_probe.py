@@ -22,3 +22,9 @@ for i, n in enumerate(names):
 print("total per block: mean %.1f max %.1f us; block start spread %.1f us" % (
     (ts[:51, 7] - ts[:51, 0]).astype(float).mean() / 100, (ts[:51, 7] - ts[:51, 0]).astype(float).max() / 100,
     (ts[:51, 0].max() - ts[:51, 0].min()) / 100.0))
+
+ts2 = np.zeros((64, 16), np.uint64)
+lvo.lib().aloam_dbg_lf_ts2(ts2.ctypes.data_as(C.c_void_p))
+g0 = ts[:51, 1].astype(np.float64)
+seg = np.diff(np.concatenate([g0[:, None], ts2[:51, :13].astype(np.float64)], axis=1), axis=1) / 100.0
+print("greedy per segment (corner, flat) us:", " ".join(f"{seg[:, i].mean():.1f}" for i in range(12)), "| tail", f"{seg[:, 12].mean():.1f}")

@@ -415,3 +415,16 @@ def test_c5_sequence_ate_vs_oracle(lvo):
     drift = np.linalg.norm(np.array(traj) - gt, axis=1).max()
     print(f"C5 max drift vs ground truth {drift:.3f} m over {synth.C5_FRAMES} m")
     assert drift < 0.01 * synth.C5_FRAMES, drift          # < 1% of the 271 m travelled
+
+
+@pytest.mark.parametrize("n_azimuth", [4200, 9000])
+def test_scan_registration_oversized_lines_bit_exact(gpu_ctx_factory, n_azimuth):
+    """Lines longer than the kernel's LDS capacity (4096 points) take the global-scratch instantiation of
+    the line kernel (k_scan.hip line_features_body<true>); its features must match the oracle bit for
+    bit like the LDS instantiation's."""
+    pts = synth.scan("vlp16", 3, n_azimuth=n_azimuth)
+    ctx = gpu_ctx_factory(16, max_scan_points=max(len(pts), 1024) + 1024)
+    orc = ob.Oracle(abi.default_params(16))
+    ctx.scan_registration(pts)
+    orc.scan_registration(pts)
+    assert_features_equal(ctx.features(), orc.features())
