@@ -38,6 +38,19 @@ void prof_mark(Ctx& C, int idx) {
 __global__ void k_set2(int* dst, int a, int b) { dst[0] = a; dst[1] = b; }
 void set_counts2(Ctx& C, int* dst, int a, int b) { k_set2<<<1, 1, 0, C.stream>>>(dst, a, b); }
 struct Vec7 { double v[7]; };
+struct ForwardJob { const float4* src[3]; float4* dst[3]; int n[3]; int* counts; double* pose_dst; double pose[7];
+                   const double* pose_src = nullptr; };   // pose_src (device) overrides pose
+// y = cloud (corner, surf, full): grid-stride copy; block (0, 0) also writes the counts and the pose
+__global__ void k_forward_map_input(ForwardJob j) {
+    const int c = blockIdx.y;
+    const float4* __restrict__ src = j.src[c];
+    float4* __restrict__ dst = j.dst[c];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < j.n[c]; i += gridDim.x * blockDim.x) dst[i] = src[i];
+    if (blockIdx.x == 0 && c == 0) {
+        if (threadIdx.x < 2) j.counts[threadIdx.x] = j.n[threadIdx.x];
+        if (threadIdx.x < 7) j.pose_dst[threadIdx.x] = j.pose_src ? j.pose_src[threadIdx.x] : j.pose[threadIdx.x];
+    }
+}
 __global__ void k_set7(double* dst, Vec7 x) { if (threadIdx.x < 7) dst[threadIdx.x] = x.v[threadIdx.x]; }
 // the destination's copies are queued on its stream; the source's stream waits for them before it may
 // overwrite its buffers (no host round trip on the hand-off)
@@ -338,13 +351,20 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     if (r.publish_to_mapping) C.odom_frame_count = 0;
     C.odom_frame_count++;
     if (r.publish_to_mapping) {   // /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3, pose
-        if (C.n_corner_last) HIPCHK(hipMemcpyAsync(C.d_map_corner_in, C.d_corner_last, sizeof(float4) * C.n_corner_last, hipMemcpyDeviceToDevice, st));
-        if (C.n_surf_last) HIPCHK(hipMemcpyAsync(C.d_map_surf_in, C.d_surf_last, sizeof(float4) * C.n_surf_last, hipMemcpyDeviceToDevice, st));
-        if (C.n_full && !C.features_from_host) HIPCHK(hipMemcpyAsync(C.d_map_full_in, C.d_cloud, sizeof(float4) * C.n_full, hipMemcpyDeviceToDevice, st));
         C.n_map_corner_in = C.n_corner_last;
         C.n_map_surf_in = C.n_surf_last;
         C.n_map_full_in = C.features_from_host ? 0 : C.n_full;
-        set_counts2(C, C.d_map_in_n, C.n_map_corner_in, C.n_map_surf_in);
+        // clouds, counts and the composed pose (laserOdometry.cpp:588-598) into the mapping input: one launch
+        ForwardJob j;
+        j.src[0] = C.d_corner_last; j.src[1] = C.d_surf_last; j.src[2] = C.d_cloud;
+        j.dst[0] = C.d_map_corner_in; j.dst[1] = C.d_map_surf_in; j.dst[2] = C.d_map_full_in;
+        j.n[0] = C.n_map_corner_in; j.n[1] = C.n_map_surf_in; j.n[2] = C.n_map_full_in;
+        j.counts = C.d_map_in_n;
+        j.pose_dst = (double*)((char*)C.d_map + offsetof(MapState, q_wodom));
+        j.pose_src = C.d_odom->q_w;                    // q_w[4], t_w[3] adjacent (OdomState)
+        const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
+        k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
+        HIPCHK(hipGetLastError());
         C.have_map_input = true;
     }
     prof_mark(C, 3);
@@ -359,14 +379,9 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     for (int i = 0; i < r.rounds; i++) { r.corner_correspondence[i] = cnt[2 * i]; r.plane_correspondence[i] = cnt[2 * i + 1]; }
     for (int k = 0; k < 4; k++) { r.q_w_curr[k] = C.h_odom.q_w[k]; r.q_last_curr[k] = C.h_odom.para[k]; }
     for (int k = 0; k < 3; k++) { r.t_w_curr[k] = C.h_odom.t_w[k]; r.t_last_curr[k] = C.h_odom.para[4 + k]; }
-    if (r.publish_to_mapping) {
+    if (r.publish_to_mapping) {   // (the device copy of this pose was written by k_forward_map_input)
         for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = r.q_w_curr[k];
         for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = r.t_w_curr[k];
-        // the odometry pose is handed to the mapping state on device (kernel argument, no pageable copy)
-        Vec7 pose;
-        std::memcpy(pose.v, C.h_map.q_wodom, sizeof(pose.v));
-        k_set7<<<1, 64, 0, st>>>((double*)((char*)C.d_map + offsetof(MapState, q_wodom)), pose);
-        HIPCHK(hipGetLastError());
     }
     if (C.profiling) {
         C.timing.odometry_ms = ev_ms(C, 2, 3);
@@ -754,16 +769,20 @@ int aloam_forward_mapping_input(aloam_ctx* src, aloam_ctx* dst) {
     if (S.n_map_corner_in > MAXL * LINE_LSHARP_CAP || S.n_map_surf_in > C.cap_in || S.n_map_full_in > C.cap_in)
         throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
     hipStream_t st = C.stream;   // the source's stream is idle: its API calls return synchronised
-    if (S.n_map_corner_in) HIPCHK(hipMemcpyAsync(C.d_map_corner_in, S.d_map_corner_in, sizeof(float4) * S.n_map_corner_in, hipMemcpyDeviceToDevice, st));
-    if (S.n_map_surf_in) HIPCHK(hipMemcpyAsync(C.d_map_surf_in, S.d_map_surf_in, sizeof(float4) * S.n_map_surf_in, hipMemcpyDeviceToDevice, st));
-    if (S.n_map_full_in) HIPCHK(hipMemcpyAsync(C.d_map_full_in, S.d_map_full_in, sizeof(float4) * S.n_map_full_in, hipMemcpyDeviceToDevice, st));
     C.n_map_corner_in = S.n_map_corner_in; C.n_map_surf_in = S.n_map_surf_in; C.n_map_full_in = S.n_map_full_in;
-    set_counts2(C, C.d_map_in_n, C.n_map_corner_in, C.n_map_surf_in);
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = S.h_map.q_wodom[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = S.h_map.t_wodom[k];
-    Vec7 pose;
-    std::memcpy(pose.v, C.h_map.q_wodom, sizeof(pose.v));   // q_wodom[4] and t_wodom[3] are adjacent (MapState)
-    k_set7<<<1, 64, 0, st>>>((double*)((char*)C.d_map + offsetof(MapState, q_wodom)), pose);
+    // the three clouds, their counts and the odometry pose in ONE launch (this hand-off sits on the
+    // mapping stage's critical path: five separate copies / kernels cost ~15 us more)
+    ForwardJob j;
+    j.src[0] = S.d_map_corner_in; j.src[1] = S.d_map_surf_in; j.src[2] = S.d_map_full_in;
+    j.dst[0] = C.d_map_corner_in; j.dst[1] = C.d_map_surf_in; j.dst[2] = C.d_map_full_in;
+    j.n[0] = C.n_map_corner_in; j.n[1] = C.n_map_surf_in; j.n[2] = C.n_map_full_in;
+    j.counts = C.d_map_in_n;
+    j.pose_dst = (double*)((char*)C.d_map + offsetof(MapState, q_wodom));   // q_wodom[4], t_wodom[3] adjacent
+    std::memcpy(j.pose, C.h_map.q_wodom, sizeof(j.pose));
+    const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
+    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
     HIPCHK(hipGetLastError());
     handoff_done(S, C);
     C.have_map_input = true;
