@@ -484,8 +484,16 @@ constexpr int LM_CACHE = 1024;                      // factor slots per workgrou
 #ifdef ALOAM_LM_TIMING
 __device__ unsigned long long g_lm_ts[8][5];   // micro-benchmark only: block-0 phase stamps per pass
 #define LM_TS(p, k) do { if (blockIdx.x == 0 && threadIdx.x == 0 && (p) < 8) g_lm_ts[p][k] = wall_clock64(); } while (0)
+__device__ unsigned long long g_lm_ts_edge[2];   // kernel entry / exit of block 0
+#define LM_TS_EDGE(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_lm_ts_edge[k] = wall_clock64(); } while (0)
+extern "C" int aloam_dbg_lm_ts(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lm_ts), sizeof(g_lm_ts));
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 40, HIP_SYMBOL(g_lm_ts_edge), sizeof(g_lm_ts_edge));
+    return (int)e;
+}
 #else
 #define LM_TS(p, k) do { } while (0)
+#define LM_TS_EDGE(k) do { } while (0)
 #endif
 __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__ f, int nslots, double* xp, LMState* st,
                                                 unsigned long long* recs, unsigned long long* seq, int* err, aloam_lm_summary* out,
@@ -497,6 +505,7 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
     __shared__ int done;
     __shared__ LMState ls;
     extern __shared__ aloam_factor fcache[];        // this workgroup's contiguous slice of factor slots
+    LM_TS_EDGE(0);
     if (gate && *gate == 0) return;                 // mapping skipped (laserMapping.cpp:554)
     if (dn) nslots = min(nslots, dn[0] + dn[1]);    // live slot count known on the device only
     const unsigned G = gridDim.x;
@@ -543,6 +552,7 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
         if (threadIdx.x < 7) xp[threadIdx.x] = xl[threadIdx.x];
         const int nw = sizeof(LMState) / 8;
         for (int i = threadIdx.x; i < nw; i += CB) ((unsigned long long*)st)[i] = ((const unsigned long long*)&ls)[i];
+        LM_TS_EDGE(1);
     }
 }
 
