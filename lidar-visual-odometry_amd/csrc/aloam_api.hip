@@ -158,6 +158,9 @@ static void allocate(Ctx& C) {
     C.d_map_corner_in = (float4*)dalloc(C, sizeof(float4) * capLS);
     C.d_map_surf_in = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_map_full_in = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_map_corner_alt = (float4*)dalloc(C, sizeof(float4) * capLS);
+    C.d_map_surf_alt = (float4*)dalloc(C, sizeof(float4) * N);
+    C.d_map_full_alt = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_map_in_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_cstack = (float4*)dalloc(C, sizeof(float4) * capLS);
     C.d_sstack = (float4*)dalloc(C, sizeof(float4) * N);
@@ -354,6 +357,11 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         C.n_map_corner_in = C.n_corner_last;
         C.n_map_surf_in = C.n_surf_last;
         C.n_map_full_in = C.features_from_host ? 0 : C.n_full;
+        // publish into the other buffer set: a hand-off taken by value (MapSnapshot) stays valid until the
+        // publish after next
+        std::swap(C.d_map_corner_in, C.d_map_corner_alt);
+        std::swap(C.d_map_surf_in, C.d_map_surf_alt);
+        std::swap(C.d_map_full_in, C.d_map_full_alt);
         // clouds, counts and the composed pose (laserOdometry.cpp:588-598) into the mapping input: one launch
         ForwardJob j;
         j.src[0] = C.d_corner_last; j.src[1] = C.d_surf_last; j.src[2] = C.d_cloud;
@@ -453,6 +461,35 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
         C.timing.map_search_bytes = 16.0 * Q + 16.0 * (double)cand[0] + 8.0 * 5.0 * Q;
     }
     if (R) *R = r;
+}
+
+void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
+    if (!S.have_map_input) throw ApiError{ALOAM_E_STATE, "source has no published odometry output"};
+    o->src[0] = S.d_map_corner_in; o->src[1] = S.d_map_surf_in; o->src[2] = S.d_map_full_in;
+    o->n[0] = S.n_map_corner_in; o->n[1] = S.n_map_surf_in; o->n[2] = S.n_map_full_in;
+    for (int k = 0; k < 4; k++) o->pose[k] = S.h_map.q_wodom[k];
+    for (int k = 0; k < 3; k++) o->pose[4 + k] = S.h_map.t_wodom[k];
+    S.have_map_input = false;
+}
+
+void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
+    HIPCHK(hipSetDevice(C.device));
+    if (s.n[0] > MAXL * LINE_LSHARP_CAP || s.n[1] > C.cap_in || s.n[2] > C.cap_in)
+        throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
+    C.n_map_corner_in = s.n[0]; C.n_map_surf_in = s.n[1]; C.n_map_full_in = s.n[2];
+    for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = s.pose[k];
+    for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = s.pose[4 + k];
+    ForwardJob j;
+    for (int c = 0; c < 3; c++) j.src[c] = s.src[c], j.n[c] = s.n[c];
+    j.dst[0] = C.d_map_corner_in; j.dst[1] = C.d_map_surf_in; j.dst[2] = C.d_map_full_in;
+    j.counts = C.d_map_in_n;
+    j.pose_dst = (double*)((char*)C.d_map + offsetof(MapState, q_wodom));
+    std::memcpy(j.pose, s.pose, sizeof(j.pose));
+    const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
+    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, C.stream>>>(j);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(copied, C.stream));
+    C.have_map_input = true;
 }
 
 }  // namespace aloam

@@ -186,6 +186,7 @@ struct Ctx {
     unsigned char* d_cube_valid = nullptr;               // [CUBE_N]
     Grid g_map_corner, g_map_surf;
     float4 *d_map_corner_in = nullptr, *d_map_surf_in = nullptr, *d_map_full_in = nullptr;
+    float4 *d_map_corner_alt = nullptr, *d_map_surf_alt = nullptr, *d_map_full_alt = nullptr;   // publish ping-pong
     int n_map_corner_in = 0, n_map_surf_in = 0, n_map_full_in = 0;
     float4 *d_cstack = nullptr, *d_sstack = nullptr;
     int* d_stack_n = nullptr;                            // [2]
@@ -275,6 +276,11 @@ void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so f
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
 void map_frame_launch(Ctx& C, aloam_map_result* R);
 void* dalloc(Ctx& C, size_t bytes);
+// the odometry -> mapping hand-off as a value: published buffers (valid until the publish after next),
+// counts and pose; the native pipeline forwards it from its mapping thread (aloam_api.hip)
+struct MapSnapshot { const float4* src[3]; int n[3]; double pose[7]; };
+void snapshot_mapping_input(Ctx& S, MapSnapshot* out);
+void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied);
 // scan-to-map registration + shard communicator (k_s2m.hip)
 void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns, int flags);
 void s2m_set_queries(Ctx& C, const float* corner, int ncq, const float* surf, int nsq, int flags);

@@ -11,6 +11,10 @@
 // Every scan goes through all stages in order, so results equal aloam_process_scan's.
 // The workers spin briefly on an atomic job word before sleeping, so a hand-off costs a cache-line
 // transfer instead of a thread wake-up on the critical path.
+// With 2 stages the mapping thread is a server over a 2-deep queue of hand-offs taken by value
+// (MapSnapshot): it forwards scan k's odometry output and maps it as soon as scan k-1's mapping is done,
+// without waiting for the caller's thread; the front publishes into alternating buffer sets, and before a
+// publish overwrites a set the front's stream waits (GPU-side) for the copy that read it.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -23,7 +27,7 @@
 #include <string>
 #include <thread>
 
-#include "../../include/aloam_hip.h"
+#include "aloam_internal.hpp"
 
 namespace {
 
@@ -84,6 +88,23 @@ struct Worker {
 
 }  // namespace
 
+namespace {
+struct MapServer {
+    std::thread th;
+    std::atomic<long> posted{0}, issued{0}, done{0};
+    std::atomic<bool> quit{false};
+    std::mutex m;
+    std::condition_variable cv;
+    aloam::MapSnapshot snap[2];
+    aloam_map_result res[2];
+    aloam_timing tim[2];
+    int rc[2] = {0, 0};
+    std::string err[2];
+    hipEvent_t copied[2] = {nullptr, nullptr};   // after the copy of hand-off j (index j & 1)
+    long returned = 0;                           // results handed to the caller
+};
+}  // namespace
+
 struct aloam_pipeline {
     int stages = 2;
     aloam_ctx* front = nullptr;     // scanRegistration (+ laserOdometry when stages == 2)
@@ -95,6 +116,7 @@ struct aloam_pipeline {
     aloam_timing t_stage[3]{};      // timing snapshots of the last completed job per stage
     int profiling = 0;
     std::string err;
+    MapServer ms;                   // stages == 2
 };
 
 namespace {
@@ -111,6 +133,53 @@ int map_job(void* a) {
     if (rc == 0 && P->profiling) aloam_get_timing(P->back, &P->t_stage[2]);
     return rc;
 }
+void map_server(aloam_pipeline* P) {
+    MapServer& S = P->ms;
+    aloam::Ctx& B = *(aloam::Ctx*)P->back;
+    for (long j = 0;; j++) {
+        int spins = 0;
+        while (S.posted.load(std::memory_order_acquire) <= j) {
+            if (S.quit.load(std::memory_order_acquire)) return;
+            if (++spins < 20000) { std::this_thread::yield(); continue; }
+            std::unique_lock<std::mutex> lk(S.m);
+            S.cv.wait(lk, [&] { return S.posted.load(std::memory_order_acquire) > j || S.quit.load(std::memory_order_acquire); });
+            spins = 0;
+        }
+        const int i = (int)(j & 1);
+        int rc = 0;
+        try {
+            aloam::forward_snapshot(B, S.snap[i], S.copied[i]);
+        } catch (const aloam::ApiError& e) {
+            rc = e.code;
+            S.err[i] = e.msg;
+        } catch (const aloam::HipError& e) {
+            rc = ALOAM_E_HIP;
+            S.err[i] = e.msg;
+        }
+        S.issued.store(j + 1, std::memory_order_release);
+        if (!rc) {
+            rc = aloam_mapping(P->back, &S.res[i]);
+            if (rc) S.err[i] = aloam_last_error(P->back);
+            else if (P->profiling) aloam_get_timing(P->back, &S.tim[i]);
+        }
+        S.rc[i] = rc;
+        S.done.store(j + 1, std::memory_order_release);
+    }
+}
+// hands the caller the oldest unreturned mapping result once done (waits); rc of that job
+int take_result(aloam_pipeline* P, aloam_map_result* mp, int* have) {
+    MapServer& S = P->ms;
+    const long j = S.returned;
+    while (S.done.load(std::memory_order_acquire) <= j) std::this_thread::yield();
+    const int i = (int)(j & 1);
+    S.returned = j + 1;
+    if (S.rc[i]) { P->err = S.err[i]; return S.rc[i]; }
+    *have = 1;
+    if (mp) *mp = S.res[i];
+    if (P->profiling) P->t_stage[2] = S.tim[i];
+    return 0;
+}
+
 int fail(aloam_pipeline* P, aloam_ctx* c, int rc) {
     P->err = aloam_last_error(c);
     return rc;
@@ -173,15 +242,31 @@ aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int sta
             }
         }
     }
-    P->wm.start();
-    if (stages == 3) P->wo.start();
+    if (stages == 2) {
+        for (auto& e : P->ms.copied)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+        P->ms.th = std::thread(map_server, P);
+    } else {
+        P->wm.start();
+        P->wo.start();
+    }
     return P;
 }
 
 void aloam_pipeline_destroy(aloam_pipeline* P) {
     if (!P) return;
-    P->wm.stop();
-    if (P->stages == 3) P->wo.stop();
+    if (P->stages == 2) {
+        {
+            std::lock_guard<std::mutex> lk(P->ms.m);
+            P->ms.quit.store(true, std::memory_order_release);
+        }
+        P->ms.cv.notify_one();
+        if (P->ms.th.joinable()) P->ms.th.join();
+        for (auto& e : P->ms.copied) if (e) (void)hipEventDestroy(e);
+    } else {
+        P->wm.stop();
+        P->wo.stop();
+    }
     aloam_destroy(P->back);
     if (P->stages == 3) aloam_destroy(P->odom);
     aloam_destroy(P->front);
@@ -197,6 +282,7 @@ aloam_ctx* aloam_pipeline_context(aloam_pipeline* P, int stage) {
 
 int aloam_pipeline_set_profiling(aloam_pipeline* P, int enable) {
     if (!P || P->wm.busy() || (P->stages == 3 && P->wo.busy())) return ALOAM_E_STATE;
+    if (P->stages == 2 && P->ms.done.load() != P->ms.posted.load()) return ALOAM_E_STATE;
     P->profiling = enable != 0;
     int rc = aloam_set_profiling(P->front, enable);
     if (!rc && P->stages == 3) rc = aloam_set_profiling(P->odom, enable);
@@ -218,17 +304,41 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
     *have_mp = 0;
     int rc;
     if (P->stages == 2) {
+        MapServer& S = P->ms;
+        aloam::Ctx& F = *(aloam::Ctx*)P->front;
+        const long seq = S.posted.load(std::memory_order_relaxed);     // index of the next hand-off
+        if (seq >= 2) {
+            // this scan may publish into the buffer set hand-off seq-2 was taken from: its copy must be
+            // issued (host) and finished (GPU) first
+            while (S.issued.load(std::memory_order_acquire) < seq - 1) std::this_thread::yield();
+            if (hipSetDevice(F.device) != hipSuccess || hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0) != hipSuccess) {
+                P->err = "hipStreamWaitEvent failed";
+                return ALOAM_E_HIP;
+            }
+        }
         aloam_odom_result o{};
         rc = aloam_process_scan(P->front, xyzr, n, flags | ALOAM_NO_MAPPING, &o, nullptr);
         if (rc) return fail(P, P->front, rc);
         if (P->profiling) aloam_get_timing(P->front, &P->t_stage[0]), P->t_stage[1] = P->t_stage[0];
         *have_od = 1;
         if (od) *od = o;
-        if ((rc = join_map(P, mp, have_mp))) return rc;
+        bool posted = false;
         if (o.publish_to_mapping) {
-            if ((rc = aloam_forward_mapping_input(P->front, P->back))) return fail(P, P->back, rc);
-            P->wm.post(map_job, P);
+            try {
+                aloam::snapshot_mapping_input(F, &S.snap[seq & 1]);
+            } catch (const aloam::ApiError& e) {
+                P->err = e.msg;
+                return e.code;
+            }
+            {
+                std::lock_guard<std::mutex> lk(S.m);
+                S.posted.store(seq + 1, std::memory_order_release);
+            }
+            S.cv.notify_one();
+            posted = true;
         }
+        // the previous scan's mapping result (the job before the one just posted)
+        if (S.returned < S.posted.load(std::memory_order_relaxed) - (posted ? 1 : 0)) return take_result(P, mp, have_mp);
         return ALOAM_OK;
     }
     // three stages: scanRegistration here, odometry and mapping of earlier scans in the workers
@@ -256,7 +366,11 @@ int aloam_pipeline_flush(aloam_pipeline* P, aloam_odom_result* od, int* have_od,
     if (!P || !have_od || !have_mp || !have_mp2) return ALOAM_E_ARG;
     *have_od = *have_mp = *have_mp2 = 0;
     int rc;
-    const int orc = P->stages == 3 ? P->wo.join() : 1;
+    if (P->stages == 2) {
+        if (P->ms.returned < P->ms.posted.load(std::memory_order_relaxed)) return take_result(P, mp, have_mp);
+        return ALOAM_OK;
+    }
+    const int orc = P->wo.join();
     if (orc != 1 && orc != 0) return fail(P, P->odom, orc);
     if ((rc = join_map(P, mp, have_mp))) return rc;
     if (orc == 0) {

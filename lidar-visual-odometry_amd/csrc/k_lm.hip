@@ -268,6 +268,13 @@ __device__ __forceinline__ void lm_finish(LMState* st, aloam_lm_summary* out, in
     }
 }
 
+#ifdef ALOAM_LM_TIMING
+__device__ unsigned long long g_ns_ts[4];
+#define NS_TS(k) do { if (blockIdx.x == 0) g_ns_ts[k] = wall_clock64(); } while (0)
+extern "C" int aloam_dbg_ns_ts(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ns_ts), sizeof(g_ns_ts)); }
+#else
+#define NS_TS(k) do { } while (0)
+#endif
 // LevenbergMarquardtStrategy::ComputeStep + model cost change; loops over invalid steps.
 __device__ __forceinline__ void lm_next_step(LMState* st, aloam_lm_summary* out, int max_iter) {
     while (true) {
@@ -292,7 +299,9 @@ __device__ __forceinline__ void lm_next_step(LMState* st, aloam_lm_summary* out,
             M[a][a] += st->diag[a] * inv_radius;   // D^2 with D = sqrt(diag / radius)
         }
         double y[6];
+        NS_TS(0);
         const bool ok = chol_solve6(M, gs, y);
+        NS_TS(1);
         st->reuse_diag = 1;
         double step[6], mcc = -1.0;
         if (ok) {
@@ -318,11 +327,13 @@ __device__ __forceinline__ void lm_next_step(LMState* st, aloam_lm_summary* out,
         double delta[6];
         #pragma unroll
         for (int a = 0; a < 6; a++) delta[a] = step[a] * st->scale[a];
+        NS_TS(2);
         plus7(st->x, delta, st->cand);
         double dx[7];
         #pragma unroll
         for (int i = 0; i < 7; i++) dx[i] = st->x[i] - st->cand[i];
         st->step_norm = norm7(dx);
+        NS_TS(3);
         st->mcc = mcc;
         return;
     }

@@ -21,3 +21,8 @@ print("stamps (us from kernel entry): pass: accumulated, block-reduced, gathered
 for p in range(5):
     print(p, " ".join(f"{(t[p, k] - e0) / 100:7.2f}" for k in (4, 0, 1, 2, 3)))
 print("exit", (e1 - e0) / 100)
+
+ns = np.zeros(4, np.uint64)
+lvo.lib().aloam_dbg_ns_ts(ns.ctypes.data_as(C.c_void_p))
+n = ns.astype(np.float64)
+print("last next_step: chol %.2f us, step->plus7 %.2f us, plus7+norm %.2f us" % ((n[1] - n[0]) / 100, (n[2] - n[1]) / 100, (n[3] - n[2]) / 100))
