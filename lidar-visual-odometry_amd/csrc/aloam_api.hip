@@ -106,6 +106,9 @@ static void allocate(Ctx& C) {
     C.d_out = (DevOut*)dalloc(C, sizeof(DevOut));
     HIPCHK(hipHostMalloc((void**)&C.h_out, sizeof(DevOut), hipHostMallocDefault));
     std::memset(C.h_out, 0, sizeof(DevOut));
+    HIPCHK(hipHostMalloc((void**)&C.h_mout[0], 2 * sizeof(DevOut), hipHostMallocDefault));
+    std::memset(C.h_mout[0], 0, 2 * sizeof(DevOut));
+    C.h_mout[1] = C.h_mout[0] + 1;
     C.d_odom = &C.d_out->odom;
     std::memset(&C.h_odom, 0, sizeof(C.h_odom));
     C.h_odom.para[3] = 1.0;
@@ -198,6 +201,7 @@ static void allocate(Ctx& C) {
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
+    for (auto& e : C.ev_mdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
     C.ev_ready = true;
     HIPCHK(hipStreamSynchronize(C.stream));   // all zero-fills and init kernels done
@@ -401,42 +405,72 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     if (R) *R = r;
 }
 
-static void do_mapping(Ctx& C, aloam_map_result* R) {
+void mapping_issue(Ctx& C) {
     if (!C.have_map_input) throw ApiError{ALOAM_E_STATE, "mapping before odometry output"};
-    aloam_map_result r{};
+    if (C.m_issued - C.m_done >= 2) throw ApiError{ALOAM_E_STATE, "two mapping frames already in flight"};
+    if (C.profiling && C.m_issued != C.m_done) throw ApiError{ALOAM_E_STATE, "profiling needs one frame at a time"};
     hipStream_t st = C.stream;
+    const int slot = (int)(C.m_issued & 1);
     if (C.profiling) HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long) * 2, st));
     prof_mark(C, 4);
-    static const bool host_timing = getenv("ALOAM_HOST_TIMING") != nullptr;   // profiling aid
     const auto th0 = std::chrono::steady_clock::now();
-    map_frame_launch(C, &r);
-    const auto th1 = std::chrono::steady_clock::now();
+    map_frame_launch(C, nullptr);
+    C.t_issue_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th0).count();
+    C.t_pre_us = std::chrono::duration<double, std::micro>(C.t_rounds_issued - th0).count();
     prof_mark(C, 5);
-    // map state, counts, summaries, sizes: one copy of the results block into the pinned mirror
-    HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, sizeof(DevOut), hipMemcpyDeviceToHost, st));
-    sync(C);
-    C.h_map = C.h_out->map;
+    // map state, counts, summaries, sizes: one copy of the results block into this frame's pinned mirror
+    HIPCHK(hipMemcpyAsync(C.h_mout[slot], C.d_out, sizeof(DevOut), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(C.ev_mdone[slot], st));
+    C.m_pend[slot][0] = C.n_map_corner_in;
+    C.m_pend[slot][1] = C.n_map_surf_in;
+    C.m_nfull[slot] = C.n_map_full_in;
+    C.n_mc += C.n_map_corner_in;      // the map can grow by at most the frame's stacks until its sizes arrive
+    C.n_ms += C.n_map_surf_in;
+    C.have_map_input = false;
+    C.map_frame_count++;
+    C.m_issued++;
+}
+
+void mapping_complete(Ctx& C, aloam_map_result* R) {
+    if (C.m_done == C.m_issued) throw ApiError{ALOAM_E_STATE, "no mapping frame in flight"};
+    const int slot = (int)(C.m_done & 1);
+    static const bool host_timing = getenv("ALOAM_HOST_TIMING") != nullptr;   // profiling aid
+    const auto tw0 = std::chrono::steady_clock::now();
+    HIPCHK(hipEventSynchronize(C.ev_mdone[slot]));
+    if (*(volatile int*)C.h_bar_err) {   // a solver grid barrier timed out: every frame in flight is void
+        C.m_done = C.m_issued;
+        sync(C);
+    }
+    C.m_done++;
+    const DevOut* H = C.h_mout[slot];
+    aloam_map_result r{};
+    double wodom[7];                     // the host's odometry pose of the latest hand-off stays
+    std::memcpy(wodom, C.h_map.q_wodom, sizeof(double) * 4);
+    std::memcpy(wodom + 4, C.h_map.t_wodom, sizeof(double) * 3);
+    C.h_map = H->map;
+    std::memcpy(C.h_map.q_wodom, wodom, sizeof(double) * 4);
+    std::memcpy(C.h_map.t_wodom, wodom + 4, sizeof(double) * 3);
     if (host_timing) {
-        static double acc_issue = 0, acc_total = 0, acc_pre = 0;
+        static double acc_issue = 0, acc_wait = 0, acc_pre = 0;
         static int nfr = 0, seen = 0;
-        const auto th2 = std::chrono::steady_clock::now();
         if (++seen > 20) {               // past graph instantiation and allocation
-            acc_issue += std::chrono::duration<double, std::micro>(th1 - th0).count();
-            acc_total += std::chrono::duration<double, std::micro>(th2 - th0).count();
-            acc_pre += std::chrono::duration<double, std::micro>(C.t_rounds_issued - th0).count();
+            acc_issue += C.t_issue_us;
+            acc_pre += C.t_pre_us;
+            acc_wait += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
             if (++nfr % 40 == 0)
-                std::fprintf(stderr, "[aloam host] mapping: issue until rounds %.1f us, whole issue %.1f us, issue+wait %.1f us (mean of %d)\n",
-                             acc_pre / nfr, acc_issue / nfr, acc_total / nfr, nfr);
+                std::fprintf(stderr, "[aloam host] mapping: issue until rounds %.1f us, whole issue %.1f us, completion wait %.1f us (mean of %d)\n",
+                             acc_pre / nfr, acc_issue / nfr, acc_wait / nfr, nfr);
         }
     }
-    const int* cnt = C.h_out->round_cnt + 2 * ALOAM_MAX_ROUNDS;
-    std::memcpy(r.lm, C.h_out->lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
-    const int* mapn = C.h_out->map_n;
-    const int* stackn = C.h_out->stack_n;
-    const unsigned long long* cand = C.h_out->cand;
-    C.n_mc = mapn[0];
-    C.n_ms = mapn[1];
-    C.n_registered = C.n_map_full_in;
+    const int* cnt = H->round_cnt + 2 * ALOAM_MAX_ROUNDS;
+    std::memcpy(r.lm, H->lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
+    const int* mapn = H->map_n;
+    const int* stackn = H->stack_n;
+    const unsigned long long* cand = H->cand;
+    const bool later = C.m_issued > C.m_done;      // a later frame is still in flight
+    C.n_mc = mapn[0] + (later ? C.m_pend[slot ^ 1][0] : 0);
+    C.n_ms = mapn[1] + (later ? C.m_pend[slot ^ 1][1] : 0);
+    C.n_registered = C.m_nfull[slot];
     r.optimized = C.h_map.optimize;
     r.rounds = r.optimized ? std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS) : 0;
     if (!r.optimized) std::memset(r.lm, 0, sizeof(r.lm));
@@ -446,10 +480,8 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
     r.corner_stack_num = stackn[0];
     r.surf_stack_num = stackn[1];
     C.map_slots_hint = stackn[0] + stackn[1];
-    r.map_total_points = C.n_mc + C.n_ms;
+    r.map_total_points = mapn[0] + mapn[1];
     for (int k = 0; k < 7; k++) (k < 4 ? r.q_w_curr[k] : r.t_w_curr[k - 4]) = C.h_map.parameters[k];
-    C.have_map_input = false;
-    C.map_frame_count++;
     if (C.profiling) {
         C.timing.mapping_ms = ev_ms(C, 4, 5);
         float s = 0;
@@ -461,6 +493,12 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
         C.timing.map_search_bytes = 16.0 * Q + 16.0 * (double)cand[0] + 8.0 * 5.0 * Q;
     }
     if (R) *R = r;
+}
+
+static void do_mapping(Ctx& C, aloam_map_result* R) {
+    if (C.m_issued != C.m_done) throw ApiError{ALOAM_E_STATE, "a pipelined mapping frame is in flight"};
+    mapping_issue(C);
+    mapping_complete(C, R);
 }
 
 void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
@@ -560,6 +598,7 @@ aloam_ctx* aloam_create(const aloam_params* p, int device) {
         for (auto& b : C->bufs) (void)hipFree(b.p);
         if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
         if (C->h_out) (void)hipHostFree(C->h_out);
+        if (C->h_mout[0]) (void)hipHostFree(C->h_mout[0]);
         if (C->stream2) (void)hipStreamDestroy(C->stream2);
         if (C->stream) (void)hipStreamDestroy(C->stream);
         delete C;
@@ -580,10 +619,12 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
+    for (auto e : C->ev_mdone) if (e) (void)hipEventDestroy(e);
     s2m_release(*C);
     for (auto& b : C->bufs) (void)hipFree(b.p);
     if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
     if (C->h_out) (void)hipHostFree(C->h_out);
+    if (C->h_mout[0]) (void)hipHostFree(C->h_mout[0]);
     if (C->stream2) (void)hipStreamDestroy(C->stream2);
     if (C->stream) (void)hipStreamDestroy(C->stream);
     delete C;
@@ -749,6 +790,7 @@ int aloam_mapping(aloam_ctx* ctx, aloam_map_result* out) {
 int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out) {
     API_BEGIN(ctx)
     if (!out) throw ApiError{ALOAM_E_ARG, "null cloud"};
+    if (C.m_issued != C.m_done) throw ApiError{ALOAM_E_STATE, "a pipelined mapping frame is in flight"};
     // map arrays are sorted by cube id; the surround cloud is the surrounding cubes' points
     std::vector<int> cube_c(C.n_mc), cube_s(C.n_ms);
     std::vector<float4> pc(C.n_mc), ps(C.n_ms);
@@ -781,6 +823,7 @@ int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out) {
 
 int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out) {
     API_BEGIN(ctx)
+    if (C.m_issued != C.m_done) throw ApiError{ALOAM_E_STATE, "a pipelined mapping frame is in flight"};
     d2h_cloud(C, C.d_registered, C.n_registered, out);
     sync(C);
     API_END

@@ -179,7 +179,8 @@ struct Ctx {
     float4* d_ms = nullptr; int* d_ms_cube = nullptr;    // surf map
     float4* d_mc2 = nullptr; int* d_mc2_cube = nullptr;  // double buffers
     float4* d_ms2 = nullptr; int* d_ms2_cube = nullptr;
-    int n_mc = 0, n_ms = 0;                              // host-known sizes (synced per frame)
+    int n_mc = 0, n_ms = 0;                              // host-known sizes: exact when no mapping frame is in
+                                                         // flight, else upper bounds (+ in-flight stack sizes)
     int* d_map_n = nullptr;                              // device sizes [2]
     int* d_cube_cnt = nullptr;                           // [2][CUBE_N + 1]
     int* d_cube_off = nullptr;                           // [2][CUBE_N + 1]
@@ -214,12 +215,20 @@ struct Ctx {
     KindScratch ks[2];
     DevOut* d_out = nullptr;         // device results block (d_odom, d_round_cnt, ... point into it)
     DevOut* h_out = nullptr;         // pinned host mirror
+    // laserMapping frames in flight (mapping_issue / mapping_complete): per parity a pinned results
+    // mirror, the event after its copy, and what the host needs back from that frame
+    DevOut* h_mout[2] = {nullptr, nullptr};
+    hipEvent_t ev_mdone[2] = {nullptr, nullptr};
+    long m_issued = 0, m_done = 0;
+    int m_pend[2][2] = {{0, 0}, {0, 0}};  // corner / surf stack upper bounds of the frame (map growth)
+    int m_nfull[2] = {0, 0};
     struct GraphSlot { const void* key[2] = {nullptr, nullptr}; int n = -1; hipGraphExec_t exec = nullptr; };
     GraphSlot graphs[3];             // 0,1: odometry rounds (last-cloud buffer parity), 2: mapping rounds
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling
     int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
     std::chrono::steady_clock::time_point t_rounds_issued{};   // host-issue profiling (ALOAM_HOST_TIMING)
+    double t_issue_us = 0, t_pre_us = 0;
 
     // ---- scan-to-map registration (k_s2m.hip) and its shard communicator ----
     struct S2M* s2m = nullptr;       // allocated by the first aloam_s2m_* call
@@ -281,6 +290,10 @@ void* dalloc(Ctx& C, size_t bytes);
 struct MapSnapshot { const float4* src[3]; int n[3]; double pose[7]; };
 void snapshot_mapping_input(Ctx& S, MapSnapshot* out);
 void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied);
+// laserMapping split in two so the host can issue frame k while the GPU still runs frame k-1 (at most
+// two frames in flight; every launch size of frame k is an upper bound known before k-1 completes)
+void mapping_issue(Ctx& C);
+void mapping_complete(Ctx& C, aloam_map_result* R);
 // scan-to-map registration + shard communicator (k_s2m.hip)
 void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns, int flags);
 void s2m_set_queries(Ctx& C, const float* corner, int ncq, const float* surf, int nsq, int flags);

@@ -133,12 +133,41 @@ int map_job(void* a) {
     if (rc == 0 && P->profiling) aloam_get_timing(P->back, &P->t_stage[2]);
     return rc;
 }
+template <class Fn>
+int guarded(Fn&& fn, std::string& err) {
+    try {
+        fn();
+        return 0;
+    } catch (const aloam::ApiError& e) {
+        err = e.msg;
+        return e.code;
+    } catch (const aloam::HipError& e) {
+        err = e.msg;
+        return ALOAM_E_HIP;
+    } catch (const std::bad_alloc&) {
+        err = "host allocation failed";
+        return ALOAM_E_CAPACITY;
+    }
+}
+// Hand-off j: forward it, issue its mapping frame, and only then wait for frame j-1 (software pipelining
+// on the mapping stream: the host issues frame j while the GPU still runs frame j-1, so the ~0.2-0.4 ms
+// of launch issue per frame leaves the critical path). With no next hand-off posted, the frame in
+// flight is completed at once. Results are published in order (done = j + 1 after result j).
 void map_server(aloam_pipeline* P) {
     MapServer& S = P->ms;
     aloam::Ctx& B = *(aloam::Ctx*)P->back;
-    for (long j = 0;; j++) {
+    long inflight = -1;
+    auto complete = [&](long j) {
+        const int i = (int)(j & 1);
+        const int rc = guarded([&] { aloam::mapping_complete(B, &S.res[i]); }, S.err[i]);
+        if (!rc && P->profiling) aloam_get_timing(P->back, &S.tim[i]);
+        S.rc[i] = rc;
+        S.done.store(j + 1, std::memory_order_release);
+    };
+    for (long j = 0;;) {
         int spins = 0;
         while (S.posted.load(std::memory_order_acquire) <= j) {
+            if (inflight >= 0) { complete(inflight); inflight = -1; continue; }
             if (S.quit.load(std::memory_order_acquire)) return;
             if (++spins < 20000) { std::this_thread::yield(); continue; }
             std::unique_lock<std::mutex> lk(S.m);
@@ -146,24 +175,21 @@ void map_server(aloam_pipeline* P) {
             spins = 0;
         }
         const int i = (int)(j & 1);
-        int rc = 0;
-        try {
-            aloam::forward_snapshot(B, S.snap[i], S.copied[i]);
-        } catch (const aloam::ApiError& e) {
-            rc = e.code;
-            S.err[i] = e.msg;
-        } catch (const aloam::HipError& e) {
-            rc = ALOAM_E_HIP;
-            S.err[i] = e.msg;
-        }
+        std::string e;
+        int rc = guarded([&] { aloam::forward_snapshot(B, S.snap[i], S.copied[i]); }, e);
         S.issued.store(j + 1, std::memory_order_release);
-        if (!rc) {
-            rc = aloam_mapping(P->back, &S.res[i]);
-            if (rc) S.err[i] = aloam_last_error(P->back);
-            else if (P->profiling) aloam_get_timing(P->back, &S.tim[i]);
+        if (!rc) rc = guarded([&] { aloam::mapping_issue(B); }, e);
+        if (inflight >= 0) { complete(inflight); inflight = -1; }
+        if (rc) {
+            S.err[i] = e;
+            S.rc[i] = rc;
+            S.done.store(j + 1, std::memory_order_release);
+        } else if (P->profiling) {
+            complete(j);                  // profiling events are per context: one frame at a time
+        } else {
+            inflight = j;
         }
-        S.rc[i] = rc;
-        S.done.store(j + 1, std::memory_order_release);
+        j++;
     }
 }
 // hands the caller the oldest unreturned mapping result once done (waits); rc of that job
