@@ -444,10 +444,20 @@ __device__ unsigned long long g_lf_ts[64][8];      // micro-benchmark only: per-
 __device__ unsigned long long g_lf_ts2[64][16];     // greedy: per-segment stamps (corners, flats)
 #define LF_TS2(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts2[blockIdx.x][k] = wall_clock64(); } while (0)
 extern "C" int aloam_dbg_lf_ts2(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_ts2), sizeof(g_lf_ts2)); }
+__device__ unsigned long long g_lf_ts3[64][8];      // sort phase sub-steps
+#define LF_TS3(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts3[blockIdx.x][k] = wall_clock64(); } while (0)
+extern "C" int aloam_dbg_lf_ts3(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_ts3), sizeof(g_lf_ts3)); }
 extern "C" int aloam_dbg_lf_ts(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_ts), sizeof(g_lf_ts)); }
+__device__ int g_lf_cnt[64][12];                    // per segment: corner chunks, corner pick-loop trips
+#define LF_CNT(j, k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_cnt[blockIdx.x][2 * (j) + (k)]++; } while (0)
+#define LF_CNT0(j) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_cnt[blockIdx.x][2 * (j)] = g_lf_cnt[blockIdx.x][2 * (j) + 1] = 0; } while (0)
+extern "C" int aloam_dbg_lf_cnt(int* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lf_cnt), sizeof(g_lf_cnt)); }
 #else
+#define LF_CNT(j, k) do { } while (0)
+#define LF_CNT0(j) do { } while (0)
 #define LF_TS(k) do { } while (0)
 #define LF_TS2(k) do { } while (0)
+#define LF_TS3(k) do { } while (0)
 #endif
 // The body, instantiated per storage class of the line's arrays: with LDS lines the pointers are
 // provably LDS, so the compiler emits ds_* instructions instead of generic flat accesses.
@@ -515,16 +525,15 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     LF_TS(0);
     // ---- gap bits: pair (i, i+1) of the line is a suppression stop when its fp32 squared
     // distance > 0.05 (:321-338, :366-383 compute exactly this for every neighbour test) ----
-    for (int wd = threadIdx.x; wd < (nl + 31) / 32; wd += LT) {
-        unsigned bits = 0;
-        for (int bb = 0; bb < 32; bb++) {
-            const int i = wd * 32 + bb;
-            if (i + 1 < nl) {
-                const float dx = X[i + 1] - X[i], dy = Y[i + 1] - Y[i], dz = Z[i + 1] - Z[i];
-                if (dx * dx + dy * dy + dz * dz > 0.05) bits |= 1u << bb;
-            }
+    for (int base = threadIdx.x & ~(WAVE - 1); base < nl; base += LT) {
+        const int i = base + lane_id();
+        bool gap = false;
+        if (i + 1 < nl) {
+            const float dx = X[i + 1] - X[i], dy = Y[i + 1] - Y[i], dz = Z[i + 1] - Z[i];
+            gap = dx * dx + dy * dy + dz * dz > 0.05;
         }
-        gapw[wd] = bits;
+        const unsigned long long m = __ballot(gap);
+        if (lane_id() < 2) gapw[base / 32 + lane_id()] = (unsigned)(m >> (32 * lane_id()));
     }
     // ---- segment sorts (:282-289), all 6 segments at once. LDS lines: one bitonic sort of
     // (segment, curvature bits, position) keys — stable by position, like the rank order; big lines:
@@ -532,7 +541,12 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     // (thread 0), since std::sort's unstable order is what the reference produces. ----
     if (threadIdx.x < 6) s_tie[threadIdx.x] = 0;
     __syncthreads();
+    LF_TS3(0);
+#ifdef ALOAM_LF_RANKSORT
+    if (false) {
+#else
     if (!big) {
+#endif
         const int M = e - s;                                             // positions s .. e-1
         int n2 = 256;
         while (n2 < M) n2 <<= 1;
@@ -548,7 +562,9 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
             keys[i] = key;
         }
         __syncthreads();
+        LF_TS3(1);
         bitonic_sort_reg4(keys, n2);
+        LF_TS3(2);
         for (int i = threadIdx.x; i < M; i += LT) {
             const unsigned long long key = keys[i];
             S[s - off0 + i] = s + (int)(key & 0xfffu);
@@ -573,6 +589,8 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         }
     }
     __syncthreads();
+    LF_TS3(3);
+    int8_t* posmap = (int8_t*)keys;      // greedy scratch (chunk lane + 1 by line position); keys are rebuilt after
     if (threadIdx.x == 0) {
         for (int j = 0; j < 6; j++) {
             if (!s_tie[j]) continue;
@@ -581,16 +599,22 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
             for (int a = 0; a < m; a++) S[b0 + a] = sp + a;
             dev_std_sort(S + b0, S + b0 + m, CurvLess{Cv, off0});
         }
+        LF_TS3(4);
     }
+    for (int k = threadIdx.x; k < nl; k += LT) posmap[k] = 0;
     __syncthreads();
     LF_TS(1);
-    // ---- greedy selection, one wave, segments in order (:291-390). Suppression of the <= 5
-    // neighbours each side is a prefix of non-gap pairs, read from the gap bits and marked by
-    // lanes in parallel. ----
+    // ---- greedy selection, one wave, segments in order (:291-390). The sorted candidates go in
+    // chunks of 64 (one per lane). Within a chunk the sequential greedy is resolved in parallel:
+    // suppression is symmetric (a pick at P marks P+d, |d| <= 5, iff no gap pair lies between them,
+    // which is also the test seen from P+d), so lane i can only lose to an earlier-ranked candidate
+    // inside its own extents; those are found through a position -> lane map, and the picks follow
+    // in rank order by fixed-point rounds over the conflict masks (usually 1-3). Only the first
+    // `quota` picks of a chunk count, exactly as the sequential loop stops at its quota. ----
     if (threadIdx.x < WAVE) {
         const int lane = threadIdx.x;
+        const unsigned long long lt = lanemask_lt64();
         int n_sharp = 0, n_lsharp = 0, n_flat = 0;
-        int r_sharp = 0, r_ls0 = 0, r_ls1 = 0, r_flat = 0;     // list slots lane, lane + 64
         // suppression extents of line position p: marks p+1..p+nf and p-1..p-nb (:321-338)
         auto extents = [&](int p, int& nf, int& nbk) {
             const int q0 = p - 5;                                              // pairs p-5 .. p+4
@@ -601,97 +625,104 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
             nf = fwd ? __builtin_ctz(fwd) : 5;
             nbk = bwd ? __builtin_clz(bwd << 27) : 5;
         };
+        // picks among this chunk's candidates (lane order = rank order), resolved in parallel
+        auto resolve = [&](bool cand, int p, int nf, int nbk) -> unsigned long long {
+            if (cand) posmap[p] = (int8_t)(lane + 1);
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long conf = 0;
+            if (cand) {
+#pragma unroll
+                for (int d = 1; d <= 5; d++) {
+                    const int qf = d <= nf ? posmap[p + d] : 0, qb = d <= nbk ? posmap[p - d] : 0;
+                    if (qf) conf |= 1ull << (qf - 1);
+                    if (qb) conf |= 1ull << (qb - 1);
+                }
+            }
+            const unsigned long long cm = __ballot(cand);
+            conf &= cm & lt;                                   // only earlier-ranked candidates suppress
+            unsigned long long decided = ~cm, pickm = 0;
+            while (~decided) {
+                const bool ready = !((decided >> lane) & 1) && (conf & ~decided) == 0;
+                pickm |= __ballot(ready && (conf & pickm) == 0);
+                decided |= __ballot(ready);
+            }
+            if (cand) posmap[p] = 0;
+            return pickm;
+        };
         auto mark = [&](int p, int nf, int nbk) {
-            if (lane >= 1 && lane <= nf) picked[p + lane] = 1;
-            if (lane >= 33 && lane <= 32 + nbk) picked[p - (lane - 32)] = 1;
+            picked[p] = 1;
+#pragma unroll
+            for (int d = 1; d <= 5; d++) {
+                if (d <= nf) picked[p + d] = 1;
+                if (d <= nbk) picked[p - d] = 1;
+            }
         };
         for (int j = 0; j < 6; j++) {
             const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
-            // corners: chunks of 64 sorted positions from the largest curvature; per pick only the
-            // picked flags are re-read, everything else of the chunk stays in registers
+            // corners: from the largest curvature, at most 20 picks, the first 2 sharp
             int largest = 0;
             bool stop = false;
+            LF_CNT0(j);
             for (int top = ep; top >= sp && !stop; top -= WAVE) {
+                LF_CNT(j, 0);
                 const int k = top - lane;
                 const bool valid = k >= sp;
-                const int ind = valid ? S[k - off0] : sp;
-                const bool cv_ok = valid && (double)Cv[ind - off0] > 0.1;
+                const int p = (valid ? S[k - off0] : sp) - off0;
+                const bool cv_ok = valid && (double)Cv[p] > 0.1;
                 if (!__ballot(cv_ok)) break;                                   // sorted: nothing > 0.1 remains
                 int nf = 0, nbk = 0;
-                if (cv_ok) extents(ind - off0, nf, nbk);
-                // the chunk's picked flags live in a register from here on: a pick at P with extents
-                // (pf, pb) marks exactly the line positions P-pb .. P+pf (itself included), so each lane
-                // updates its own flag without an LDS round trip; the LDS flags are still written for
-                // later chunks and the flat pass (read after the fence at the end of the chunk)
-                bool pk = valid && picked[ind - off0] != 0;
-                int last = -1;
-                while (true) {
-                    const unsigned long long mk = __ballot(cv_ok && lane > last && !pk);
-                    if (!mk) break;
-                    const int f = __ffsll((long long)mk) - 1;
-                    last = f;
-                    const int indf = readlane_i(ind, f);
-                    largest++;
-                    if (largest > 20) { stop = true; break; }
-                    const int pf = readlane_i(nf, f), pb = readlane_i(nbk, f);
-                    if (lane == 0) {
-                        label[indf - off0] = largest <= 2 ? 2 : 1;
-                        picked[indf - off0] = 1;
-                    }
-                    // the index lists are collected in registers (slot i in lane i % 64) and stored once
-                    // after the selection: a global store inside this serial loop made every pick wait
-                    // for its completion
-                    if (largest <= 2 && lane == n_sharp) r_sharp = indf;
-                    if (lane == (n_lsharp & (WAVE - 1))) { if (n_lsharp < WAVE) r_ls0 = indf; else r_ls1 = indf; }
-                    mark(indf - off0, pf, pb);
-                    pk = pk || (ind >= indf - pb && ind <= indf + pf);
-                    if (largest <= 2) n_sharp++;
-                    n_lsharp++;
+                if (cv_ok) extents(p, nf, nbk);
+                const bool cand = cv_ok && picked[p] == 0;
+                const unsigned long long pickm = resolve(cand, p, nf, nbk);
+                const int npk = __popcll(pickm), quota = 20 - largest;
+                const int rank = __popcll(pickm & lt);
+                if ((pickm >> lane) & 1 && rank < quota) {
+                    const int g = largest + rank;                              // 0-based pick number
+                    label[p] = g < 2 ? 2 : 1;
+                    mark(p, nf, nbk);
+                    if (g < 2) line_sharp[line * LINE_SHARP_CAP + n_sharp + g] = p + off0;
+                    line_lsharp[line * LINE_LSHARP_CAP + n_lsharp + g] = p + off0;
                 }
+                if (npk > quota) stop = true;
+                largest += min(npk, quota);
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
             }
+            n_sharp += min(largest, 2);
+            n_lsharp += largest;
             LF_TS2(2 * j);
-            // flats: from the smallest curvature; the 4th pick is not marked (:366-388)
+            // flats: from the smallest curvature; the 4th pick is labelled but not marked (:366-388)
             int smallest = 0;
             stop = false;
             for (int bot = sp; bot <= ep && !stop; bot += WAVE) {
                 const int k = bot + lane;
                 const bool valid = k <= ep;
-                const int ind = valid ? S[k - off0] : sp;
-                const bool cv_ok = valid && (double)Cv[ind - off0] < 0.1;
+                const int p = (valid ? S[k - off0] : sp) - off0;
+                const bool cv_ok = valid && (double)Cv[p] < 0.1;
                 if (!__ballot(cv_ok)) break;                                   // sorted: nothing < 0.1 remains
                 int nf = 0, nbk = 0;
-                if (cv_ok) extents(ind - off0, nf, nbk);
-                bool pk = valid && picked[ind - off0] != 0;     // register flags, as in the corner pass
-                int last = -1;
-                while (true) {
-                    const unsigned long long mk = __ballot(cv_ok && lane > last && !pk);
-                    if (!mk) break;
-                    const int f = __ffsll((long long)mk) - 1;
-                    last = f;
-                    const int indf = readlane_i(ind, f);
-                    if (lane == 0) label[indf - off0] = -1;
-                    if (lane == n_flat) r_flat = indf;
-                    n_flat++;
-                    smallest++;
-                    if (smallest >= 4) { stop = true; break; }
-                    const int pf = readlane_i(nf, f), pb = readlane_i(nbk, f);
-                    if (lane == 0) picked[indf - off0] = 1;
-                    mark(indf - off0, pf, pb);
-                    pk = pk || (ind >= indf - pb && ind <= indf + pf);
+                if (cv_ok) extents(p, nf, nbk);
+                const bool cand = cv_ok && picked[p] == 0;
+                const unsigned long long pickm = resolve(cand, p, nf, nbk);
+                const int npk = __popcll(pickm), quota = 4 - smallest;
+                const int rank = __popcll(pickm & lt);
+                if ((pickm >> lane) & 1 && rank < quota) {
+                    const int g = smallest + rank;
+                    label[p] = -1;
+                    line_flat[line * LINE_FLAT_CAP + n_flat + g] = p + off0;
+                    if (g < 3) mark(p, nf, nbk);
                 }
+                smallest += min(npk, quota);
+                if (smallest >= 4) stop = true;
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
             }
+            n_flat += smallest;
             LF_TS2(2 * j + 1);
         }
         LF_TS2(12);
-        static_assert(LINE_SHARP_CAP <= WAVE && LINE_FLAT_CAP <= WAVE && LINE_LSHARP_CAP <= 2 * WAVE, "list slots");
-        if (lane < n_sharp) line_sharp[line * LINE_SHARP_CAP + lane] = r_sharp;
-        if (lane < n_lsharp) line_lsharp[line * LINE_LSHARP_CAP + lane] = r_ls0;
-        if (lane + WAVE < n_lsharp) line_lsharp[line * LINE_LSHARP_CAP + WAVE + lane] = r_ls1;
-        if (lane < n_flat) line_flat[line * LINE_FLAT_CAP + lane] = r_flat;
+        static_assert(LINE_SHARP_CAP >= 12 && LINE_FLAT_CAP >= 24 && LINE_LSHARP_CAP >= 120, "list slots");
         if (lane == 0) { s_cnt[0] = n_sharp; s_cnt[1] = n_lsharp; s_cnt[2] = n_flat; }
     }
     __syncthreads();
