@@ -468,12 +468,12 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
                                                       int* line_sharp, int* line_lsharp, int* line_flat, int* line_cnt,
                                                       float4* line_lf, unsigned char* smem_raw) {
     // all LDS is dynamic (Guideline 17: no statics ahead of the dynamic base)
-    struct LineShared { int flag, ncand, nrun, cnt[3]; unsigned bb[6]; int wsum[LT / WAVE]; int tie[6]; };
+    struct LineShared { int flag, ncand, nrun, cnt[3]; unsigned bb[6]; int wsum[LT / WAVE]; int tlo[6], thi[6]; };
     LineShared& SH = *(LineShared*)smem_raw;
     unsigned char* smem = smem_raw + LINE_HDR;
     static_assert(sizeof(LineShared) <= LINE_HDR, "LineShared");
     int& s_flag = SH.flag; int& s_ncand = SH.ncand; int& s_nrun = SH.nrun;
-    int* s_cnt = SH.cnt; unsigned* s_bb = SH.bb; int* s_wsum = SH.wsum; int* s_tie = SH.tie;
+    int* s_cnt = SH.cnt; unsigned* s_bb = SH.bb; int* s_wsum = SH.wsum; int* s_tlo = SH.tlo; int* s_thi = SH.thi;
     const int line = blockIdx.x;
     const int off0 = meta->line_off[line], off1 = meta->line_off[line + 1];
     const int nl = off1 - off0;
@@ -539,7 +539,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     // (segment, curvature bits, position) keys — stable by position, like the rank order; big lines:
     // rank sort. A segment with exact curvature ties is redone by the libstdc++ introsort replica
     // (thread 0), since std::sort's unstable order is what the reference produces. ----
-    if (threadIdx.x < 6) s_tie[threadIdx.x] = 0;
+    if (threadIdx.x < 6) { s_tlo[threadIdx.x] = 0x7fffffff; s_thi[threadIdx.x] = -1; }
     __syncthreads();
     LF_TS3(0);
 #ifdef ALOAM_LF_RANKSORT
@@ -568,7 +568,10 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         for (int i = threadIdx.x; i < M; i += LT) {
             const unsigned long long key = keys[i];
             S[s - off0 + i] = s + (int)(key & 0xfffu);
-            if (i > 0 && (keys[i - 1] >> 12) == (key >> 12)) s_tie[(int)(key >> 44)] = 1;
+            if (i > 0 && (keys[i - 1] >> 12) == (key >> 12)) {          // exact tie: sorted slots s+i-1, s+i
+                atomicMin(&s_tlo[(int)(key >> 44)], s + i - 1);
+                atomicMax(&s_thi[(int)(key >> 44)], s + i);
+            }
         }
     } else {
         for (int a = s + threadIdx.x; a <= e - 1; a += LT) {
@@ -585,22 +588,15 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
                 ties += (cb == ca);
             }
             S[b0 + rank] = a;
-            if (ties > 1) s_tie[j] = 1;
+            if (ties > 1) { atomicMin(&s_tlo[j], sp + rank); atomicMax(&s_thi[j], sp + rank); }
         }
     }
     __syncthreads();
     LF_TS3(3);
+    // exact curvature ties: std::sort's unstable order decides how a tie group is arranged, which
+    // matters only if the greedy below reads one of the group's sorted slots; such a segment is redone
+    // by the libstdc++ introsort replica and the selection rerun (rare: ties fall mid-order)
     int8_t* posmap = (int8_t*)keys;      // greedy scratch (chunk lane + 1 by line position); keys are rebuilt after
-    if (threadIdx.x == 0) {
-        for (int j = 0; j < 6; j++) {
-            if (!s_tie[j]) continue;
-            const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
-            const int b0 = sp - off0, m = ep - sp + 1;
-            for (int a = 0; a < m; a++) S[b0 + a] = sp + a;
-            dev_std_sort(S + b0, S + b0 + m, CurvLess{Cv, off0});
-        }
-        LF_TS3(4);
-    }
     for (int k = threadIdx.x; k < nl; k += LT) posmap[k] = 0;
     __syncthreads();
     LF_TS(1);
@@ -615,6 +611,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         const int lane = threadIdx.x;
         const unsigned long long lt = lanemask_lt64();
         int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+        unsigned redone = 0;                                    // segments in libstdc++ tie order
         // suppression extents of line position p: marks p+1..p+nf and p-1..p-nb (:321-338)
         auto extents = [&](int p, int& nf, int& nbk) {
             const int q0 = p - 5;                                              // pairs p-5 .. p+4
@@ -658,10 +655,15 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
                 if (d <= nbk) picked[p - d] = 1;
             }
         };
-        for (int j = 0; j < 6; j++) {
+        for (;;) {
+        unsigned need = 0;
+        n_sharp = n_lsharp = n_flat = 0;
+        for (int j = 0; j < 6 && !need; j++) {
+            int lo_read, hi_read;                               // sorted slots read: corners [lo, ep], flats [sp, hi]
             const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
             // corners: from the largest curvature, at most 20 picks, the first 2 sharp
             int largest = 0;
+            lo_read = ep + 1;
             bool stop = false;
             LF_CNT0(j);
             for (int top = ep; top >= sp && !stop; top -= WAVE) {
@@ -671,6 +673,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
                 const int p = (valid ? S[k - off0] : sp) - off0;
                 const bool cv_ok = valid && (double)Cv[p] > 0.1;
                 if (!__ballot(cv_ok)) break;                                   // sorted: nothing > 0.1 remains
+                lo_read = max(top - (WAVE - 1), sp);
                 int nf = 0, nbk = 0;
                 if (cv_ok) extents(p, nf, nbk);
                 const bool cand = cv_ok && picked[p] == 0;
@@ -694,6 +697,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
             LF_TS2(2 * j);
             // flats: from the smallest curvature; the 4th pick is labelled but not marked (:366-388)
             int smallest = 0;
+            hi_read = sp - 1;
             stop = false;
             for (int bot = sp; bot <= ep && !stop; bot += WAVE) {
                 const int k = bot + lane;
@@ -701,6 +705,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
                 const int p = (valid ? S[k - off0] : sp) - off0;
                 const bool cv_ok = valid && (double)Cv[p] < 0.1;
                 if (!__ballot(cv_ok)) break;                                   // sorted: nothing < 0.1 remains
+                hi_read = min(bot + (WAVE - 1), ep);
                 int nf = 0, nbk = 0;
                 if (cv_ok) extents(p, nf, nbk);
                 const bool cand = cv_ok && picked[p] == 0;
@@ -720,6 +725,25 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
             }
             n_flat += smallest;
             LF_TS2(2 * j + 1);
+            // a segment whose tie group overlaps the slots read is redone in libstdc++ order and the
+            // selection reruns from the start (later segments see its marks); redone segments are exact
+            if (!((redone >> j) & 1) && s_tlo[j] <= s_thi[j] && (s_thi[j] >= lo_read || s_tlo[j] <= hi_read)) need = 1u << j;
+        }
+        if (!need) break;
+        if (lane == 0) {
+            for (int j = 0; j < 6; j++) {
+                if (!((need >> j) & 1)) continue;
+                const int sp = s + (e - s) * j / 6, ep = s + (e - s) * (j + 1) / 6 - 1;
+                const int b0 = sp - off0, m = ep - sp + 1;
+                for (int a = 0; a < m; a++) S[b0 + a] = sp + a;
+                dev_std_sort(S + b0, S + b0 + m, CurvLess{Cv, off0});
+            }
+            LF_TS3(4);
+        }
+        for (int k = lane; k < nl; k += WAVE) { picked[k] = 0; label[k] = 0; }
+        redone |= need;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
         }
         LF_TS2(12);
         static_assert(LINE_SHARP_CAP >= 12 && LINE_FLAT_CAP >= 24 && LINE_LSHARP_CAP >= 120, "list slots");

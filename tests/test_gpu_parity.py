@@ -71,16 +71,19 @@ def test_unsupported_scan_lines_is_an_error(gpu_ctx_factory):
         ctx.scan_registration(synth.scan("vlp16", 0))
 
 
-def test_tied_curvatures_follow_std_sort(gpu_ctx_factory):
-    """Quantised coordinates create exact curvature ties: the order must be libstdc++'s."""
-    ctx = gpu_ctx_factory(16)
-    orc = ob.Oracle(abi.default_params(16))
-    pts = synth.scan("vlp16", 2)
-    q = pts.copy()
-    q[:, :3] = np.round(q[:, :3] * 20) / 20   # 5 cm lattice
-    ctx.scan_registration(q)
-    orc.scan_registration(q)
-    assert_features_equal(ctx.features(), orc.features())
+@pytest.mark.parametrize("lines,preset,lattice", [(16, "vlp16", 20), (64, "hdl64", 20), (64, "hdl64", 100), (64, "hdl64", 1000)])
+def test_tied_curvatures_follow_std_sort(gpu_ctx_factory, lines, preset, lattice):
+    """Quantised coordinates create exact curvature ties: where the selection reads a tie group's sorted
+    slots the order must be libstdc++'s (k_scan.hip redoes such segments and reruns the selection);
+    coarse lattices put ties everywhere, fine ones only here and there."""
+    ctx = gpu_ctx_factory(lines)
+    orc = ob.Oracle(abi.default_params(lines))
+    for k in range(2):
+        q = synth.scan(preset, 2 + k).copy()
+        q[:, :3] = np.round(q[:, :3] * lattice) / lattice
+        ctx.scan_registration(q)
+        orc.scan_registration(q)
+        assert_features_equal(ctx.features(), orc.features())
 
 
 def random_factors(rng, n):
@@ -417,12 +420,14 @@ def test_c5_sequence_ate_vs_oracle(lvo):
     assert drift < 0.01 * synth.C5_FRAMES, drift          # < 1% of the 271 m travelled
 
 
-@pytest.mark.parametrize("n_azimuth", [4200, 9000])
-def test_scan_registration_oversized_lines_bit_exact(gpu_ctx_factory, n_azimuth):
+@pytest.mark.parametrize("n_azimuth,lattice", [(4200, 0), (9000, 0), (4200, 20)])
+def test_scan_registration_oversized_lines_bit_exact(gpu_ctx_factory, n_azimuth, lattice):
     """Lines longer than the kernel's LDS capacity (4096 points) take the global-scratch instantiation of
     the line kernel (k_scan.hip line_features_body<true>); its features must match the oracle bit for
-    bit like the LDS instantiation's."""
+    bit like the LDS instantiation's (also with lattice-quantised points: many exact curvature ties)."""
     pts = synth.scan("vlp16", 3, n_azimuth=n_azimuth)
+    if lattice:
+        pts[:, :3] = np.round(pts[:, :3] * lattice) / lattice
     ctx = gpu_ctx_factory(16, max_scan_points=max(len(pts), 1024) + 1024)
     orc = ob.Oracle(abi.default_params(16))
     ctx.scan_registration(pts)
