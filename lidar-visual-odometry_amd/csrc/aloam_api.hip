@@ -158,16 +158,17 @@ static void allocate(Ctx& C) {
     C.d_cube_valid = (unsigned char*)dalloc(C, CUBE_N);
     grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f, 1, true);     // 5-NN within 1 m, 3x3x3 cells
     grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f, 1, true);
-    C.d_map_corner_in = (float4*)dalloc(C, sizeof(float4) * capLS);
-    C.d_map_surf_in = (float4*)dalloc(C, sizeof(float4) * N);
-    C.d_map_full_in = (float4*)dalloc(C, sizeof(float4) * N);
-    C.d_map_corner_alt = (float4*)dalloc(C, sizeof(float4) * capLS);
-    C.d_map_surf_alt = (float4*)dalloc(C, sizeof(float4) * N);
-    C.d_map_full_alt = (float4*)dalloc(C, sizeof(float4) * N);
-    C.d_map_in_n = (int*)dalloc(C, sizeof(int) * 2);
-    C.d_cstack = (float4*)dalloc(C, sizeof(float4) * capLS);
-    C.d_sstack = (float4*)dalloc(C, sizeof(float4) * N);
-    C.d_stack_n = C.d_out->stack_n;
+    for (auto& m : C.mset) {
+        m.corner = (float4*)dalloc(C, sizeof(float4) * capLS);
+        m.surf = (float4*)dalloc(C, sizeof(float4) * N);
+        m.full = (float4*)dalloc(C, sizeof(float4) * N);
+        m.n = (int*)dalloc(C, sizeof(int) * 2);
+        m.pose = (double*)dalloc(C, sizeof(double) * 8);
+        m.cstack = (float4*)dalloc(C, sizeof(float4) * capLS);
+        m.sstack = (float4*)dalloc(C, sizeof(float4) * N);
+    }
+    use_input_set(C, 0);
+    C.d_tmp_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_registered = (float4*)dalloc(C, sizeof(float4) * N);
     // voxel / sort scratch
     C.cap_voxel = std::max(N, capLS) + 64;
@@ -197,7 +198,18 @@ static void allocate(Ctx& C) {
     k1.seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (4 * (size_t)M + 32768));
     k1.blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, M / 256 + 1) + 4096));
     k1.map_tmp = (float4*)dalloc(C, sizeof(float4) * M);
+    KindScratch& kv = C.ksv;            // stream3: the stacks' VoxelGrid (vkeys, vvals, sort, blk only)
+    kv.vkeys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)C.cap_voxel);
+    kv.vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
+    kv.vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
+    kv.vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
+    kv.sort_tmp = dalloc(C, C.sort_tmp_bytes);
+    kv.blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, M / 256 + 1) + 4096));
     HIPCHK(hipStreamCreateWithFlags(&C.stream2, hipStreamNonBlocking));
+    for (auto& m : C.mset) {
+        HIPCHK(hipEventCreateWithFlags(&m.ready, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&m.released, hipEventDisableTiming));
+    }
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
@@ -358,25 +370,26 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     if (r.publish_to_mapping) C.odom_frame_count = 0;
     C.odom_frame_count++;
     if (r.publish_to_mapping) {   // /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3, pose
-        C.n_map_corner_in = C.n_corner_last;
-        C.n_map_surf_in = C.n_surf_last;
-        C.n_map_full_in = C.features_from_host ? 0 : C.n_full;
-        // publish into the other buffer set: a hand-off taken by value (MapSnapshot) stays valid until the
-        // publish after next
-        std::swap(C.d_map_corner_in, C.d_map_corner_alt);
-        std::swap(C.d_map_surf_in, C.d_map_surf_alt);
-        std::swap(C.d_map_full_in, C.d_map_full_alt);
+        // publish into the other input set: a hand-off taken by value (MapSnapshot) stays valid until the
+        // publish after next, and a mapping frame of this context keeps reading its own set
+        const int t = C.in_cur ^ 1;
+        Ctx::MapInSet& m = C.mset[t];
+        m.nc = C.n_corner_last;
+        m.ns = C.n_surf_last;
+        m.nf = C.features_from_host ? 0 : C.n_full;
+        m.stacks = false;
         // clouds, counts and the composed pose (laserOdometry.cpp:588-598) into the mapping input: one launch
         ForwardJob j;
         j.src[0] = C.d_corner_last; j.src[1] = C.d_surf_last; j.src[2] = C.d_cloud;
-        j.dst[0] = C.d_map_corner_in; j.dst[1] = C.d_map_surf_in; j.dst[2] = C.d_map_full_in;
-        j.n[0] = C.n_map_corner_in; j.n[1] = C.n_map_surf_in; j.n[2] = C.n_map_full_in;
-        j.counts = C.d_map_in_n;
-        j.pose_dst = (double*)((char*)C.d_map + offsetof(MapState, q_wodom));
+        j.dst[0] = m.corner; j.dst[1] = m.surf; j.dst[2] = m.full;
+        j.n[0] = m.nc; j.n[1] = m.ns; j.n[2] = m.nf;
+        j.counts = m.n;
+        j.pose_dst = m.pose;
         j.pose_src = C.d_odom->q_w;                    // q_w[4], t_w[3] adjacent (OdomState)
         const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
         k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
         HIPCHK(hipGetLastError());
+        use_input_set(C, t);
         C.have_map_input = true;
     }
     prof_mark(C, 3);
@@ -411,21 +424,25 @@ void mapping_issue(Ctx& C) {
     if (C.profiling && C.m_issued != C.m_done) throw ApiError{ALOAM_E_STATE, "profiling needs one frame at a time"};
     hipStream_t st = C.stream;
     const int slot = (int)(C.m_issued & 1);
+    const int X = C.in_cur;
+    Ctx::MapInSet& in = C.mset[X];
     if (C.profiling) HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long) * 2, st));
     prof_mark(C, 4);
     const auto th0 = std::chrono::steady_clock::now();
-    map_frame_launch(C, nullptr);
+    map_frame_launch(C, X);
     C.t_issue_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th0).count();
     C.t_pre_us = std::chrono::duration<double, std::micro>(C.t_rounds_issued - th0).count();
     prof_mark(C, 5);
     // map state, counts, summaries, sizes: one copy of the results block into this frame's pinned mirror
     HIPCHK(hipMemcpyAsync(C.h_mout[slot], C.d_out, sizeof(DevOut), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(C.ev_mdone[slot], st));
-    C.m_pend[slot][0] = C.n_map_corner_in;
-    C.m_pend[slot][1] = C.n_map_surf_in;
-    C.m_nfull[slot] = C.n_map_full_in;
-    C.n_mc += C.n_map_corner_in;      // the map can grow by at most the frame's stacks until its sizes arrive
-    C.n_ms += C.n_map_surf_in;
+    HIPCHK(hipEventRecord(in.released, st));   // the input set may be written again (stream3 waits on this)
+    C.m_set[slot] = X;
+    C.m_pend[slot][0] = in.nc;
+    C.m_pend[slot][1] = in.ns;
+    C.m_nfull[slot] = in.nf;
+    C.n_mc += in.nc;                  // the map can grow by at most the frame's stacks until its sizes arrive
+    C.n_ms += in.ns;
     C.have_map_input = false;
     C.map_frame_count++;
     C.m_issued++;
@@ -465,7 +482,7 @@ void mapping_complete(Ctx& C, aloam_map_result* R) {
     const int* cnt = H->round_cnt + 2 * ALOAM_MAX_ROUNDS;
     std::memcpy(r.lm, H->lm_sum + ALOAM_MAX_ROUNDS, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
     const int* mapn = H->map_n;
-    const int* stackn = H->stack_n;
+    const int* stackn = H->stack_n + 2 * C.m_set[slot];
     const unsigned long long* cand = H->cand;
     const bool later = C.m_issued > C.m_done;      // a later frame is still in flight
     C.n_mc = mapn[0] + (later ? C.m_pend[slot ^ 1][0] : 0);
@@ -510,23 +527,76 @@ void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
     S.have_map_input = false;
 }
 
+hipStream_t make_stream(Ctx& C, bool side) {
+    const std::vector<unsigned>& m = side && !C.cu_mask_side.empty() ? C.cu_mask_side : C.cu_mask;
+    hipStream_t st = nullptr;
+    if (m.empty()) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    else HIPCHK(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()));
+    return st;
+}
+
+void set_side_cu_mask(Ctx& C, const unsigned* mask, int nwords) {
+    HIPCHK(hipSetDevice(C.device));
+    C.cu_mask_side.assign(mask, mask + std::max(nwords, 0));
+    if (C.stream3) {
+        HIPCHK(hipStreamSynchronize(C.stream3));
+        (void)hipStreamDestroy(C.stream3);
+        C.stream3 = nullptr;
+    }
+}
+
+void use_input_set(Ctx& C, int t) {
+    C.in_cur = t;
+    const Ctx::MapInSet& m = C.mset[t];
+    C.d_map_corner_in = m.corner; C.d_map_surf_in = m.surf; C.d_map_full_in = m.full; C.d_map_in_n = m.n;
+    C.n_map_corner_in = m.nc; C.n_map_surf_in = m.ns; C.n_map_full_in = m.nf;
+}
+
+// The stacks of input set t (VoxelGrid of the corner / surf clouds, laserMapping.cpp:542-550) on stream3:
+// they depend on the hand-off only, so they run while the previous frame still occupies the stream.
+static void prepare_stacks(Ctx& C, int t) {
+    Ctx::MapInSet& m = C.mset[t];
+    voxel_grid_sorted_on(C, C.stream3, C.ksv, m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
+                         C.d_out->stack_n + 2 * t + 0, false);
+    voxel_grid_sorted_on(C, C.stream3, C.ksv, m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
+                         C.d_out->stack_n + 2 * t + 1, false);
+    HIPCHK(hipEventRecord(m.ready, C.stream3));
+    m.stacks = true;
+}
+
+// A hand-off into the other input set, on stream3 (after the frame that last read that set): one copy
+// launch for the clouds, counts and pose, `copied` recorded behind it, then the set's stacks.
 void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
     HIPCHK(hipSetDevice(C.device));
     if (s.n[0] > MAXL * LINE_LSHARP_CAP || s.n[1] > C.cap_in || s.n[2] > C.cap_in)
         throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
-    C.n_map_corner_in = s.n[0]; C.n_map_surf_in = s.n[1]; C.n_map_full_in = s.n[2];
+    const int t = C.in_cur ^ 1;
+    Ctx::MapInSet& m = C.mset[t];
+    // ALOAM_SIDE_STACKS=1: copy + stack VoxelGrid on stream3, overlapping the previous frame. Measured on
+    // one MI355X (2-stage pipeline): +4% without CU partitions (916 vs 881 scans/s) but -30% with them
+    // (715-757 vs 1019-1027, also with stream3 on CUs of its own) — a third busy CU-masked queue per
+    // context costs more than the overlap gains. Default: both on the context's stream (stream order
+    // then protects the set the previous frame reads).
+    static const bool side = getenv("ALOAM_SIDE_STACKS") && atoi(getenv("ALOAM_SIDE_STACKS")) == 1;
+    if (side && !C.stream3) C.stream3 = make_stream(C, true);
+    hipStream_t fs = side ? C.stream3 : C.stream;
+    HIPCHK(hipStreamWaitEvent(fs, m.released, 0));
+    m.nc = s.n[0]; m.ns = s.n[1]; m.nf = s.n[2];
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = s.pose[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = s.pose[4 + k];
     ForwardJob j;
     for (int c = 0; c < 3; c++) j.src[c] = s.src[c], j.n[c] = s.n[c];
-    j.dst[0] = C.d_map_corner_in; j.dst[1] = C.d_map_surf_in; j.dst[2] = C.d_map_full_in;
-    j.counts = C.d_map_in_n;
-    j.pose_dst = (double*)((char*)C.d_map + offsetof(MapState, q_wodom));
+    j.dst[0] = m.corner; j.dst[1] = m.surf; j.dst[2] = m.full;
+    j.counts = m.n;
+    j.pose_dst = m.pose;
     std::memcpy(j.pose, s.pose, sizeof(j.pose));
     const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
-    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, C.stream>>>(j);
+    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, fs>>>(j);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(copied, C.stream));
+    if (copied) HIPCHK(hipEventRecord(copied, fs));
+    if (side) prepare_stacks(C, t);
+    else m.stacks = false;
+    use_input_set(C, t);
     C.have_map_input = true;
 }
 
@@ -600,6 +670,7 @@ aloam_ctx* aloam_create(const aloam_params* p, int device) {
         if (C->h_out) (void)hipHostFree(C->h_out);
         if (C->h_mout[0]) (void)hipHostFree(C->h_mout[0]);
         if (C->stream2) (void)hipStreamDestroy(C->stream2);
+        if (C->stream3) (void)hipStreamDestroy(C->stream3);
         if (C->stream) (void)hipStreamDestroy(C->stream);
         delete C;
         return nullptr;
@@ -614,18 +685,24 @@ void aloam_destroy(aloam_ctx* ctx) {
     (void)hipSetDevice(C->device);
     if (C->stream) (void)hipStreamSynchronize(C->stream);
     if (C->stream2) (void)hipStreamSynchronize(C->stream2);
+    if (C->stream3) (void)hipStreamSynchronize(C->stream3);
     if (C->ev_ready) for (int i = 0; i < Ctx::NEV; i++) (void)hipEventDestroy(C->ev[i]);
     for (auto& g : C->graphs) if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
     for (auto e : C->ev_mdone) if (e) (void)hipEventDestroy(e);
+    for (auto& m : C->mset) {
+        if (m.ready) (void)hipEventDestroy(m.ready);
+        if (m.released) (void)hipEventDestroy(m.released);
+    }
     s2m_release(*C);
     for (auto& b : C->bufs) (void)hipFree(b.p);
     if (C->h_bar_err) (void)hipHostFree(C->h_bar_err);
     if (C->h_out) (void)hipHostFree(C->h_out);
     if (C->h_mout[0]) (void)hipHostFree(C->h_mout[0]);
     if (C->stream2) (void)hipStreamDestroy(C->stream2);
+    if (C->stream3) (void)hipStreamDestroy(C->stream3);
     if (C->stream) (void)hipStreamDestroy(C->stream);
     delete C;
 }
@@ -769,13 +846,16 @@ int aloam_set_mapping_input(aloam_ctx* ctx, const float* corner, int nc, const f
     API_BEGIN(ctx)
     if (nc < 0 || ns < 0 || !q || !t) throw ApiError{ALOAM_E_ARG, "bad mapping input"};
     if (nc > MAXL * LINE_LSHARP_CAP || ns > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
-    if (nc > 0) HIPCHK(hipMemcpyAsync(C.d_map_corner_in, corner, sizeof(float4) * nc, hipMemcpyHostToDevice, C.stream));
-    if (ns > 0) HIPCHK(hipMemcpyAsync(C.d_map_surf_in, surf, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
-    C.n_map_corner_in = nc; C.n_map_surf_in = ns; C.n_map_full_in = 0;
-    set_counts2(C, C.d_map_in_n, nc, ns);
+    const int ti = C.in_cur ^ 1;          // the other input set (stream order protects the frame that read it)
+    Ctx::MapInSet& m = C.mset[ti];
+    if (nc > 0) HIPCHK(hipMemcpyAsync(m.corner, corner, sizeof(float4) * nc, hipMemcpyHostToDevice, C.stream));
+    if (ns > 0) HIPCHK(hipMemcpyAsync(m.surf, surf, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
+    m.nc = nc; m.ns = ns; m.nf = 0; m.stacks = false;
+    set_counts2(C, m.n, nc, ns);
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = q[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = t[k];
-    HIPCHK(hipMemcpyAsync((char*)C.d_map + offsetof(MapState, q_wodom), C.h_map.q_wodom, sizeof(double) * 7, hipMemcpyHostToDevice, C.stream));
+    HIPCHK(hipMemcpyAsync(m.pose, C.h_map.q_wodom, sizeof(double) * 7, hipMemcpyHostToDevice, C.stream));
+    use_input_set(C, ti);
     sync(C);
     C.have_map_input = true;
     API_END
@@ -848,25 +928,12 @@ int aloam_forward_mapping_input(aloam_ctx* src, aloam_ctx* dst) {
     if (!S.have_map_input) throw ApiError{ALOAM_E_STATE, "source has no published odometry output"};
     if (S.n_map_corner_in > MAXL * LINE_LSHARP_CAP || S.n_map_surf_in > C.cap_in || S.n_map_full_in > C.cap_in)
         throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
-    hipStream_t st = C.stream;   // the source's stream is idle: its API calls return synchronised
-    C.n_map_corner_in = S.n_map_corner_in; C.n_map_surf_in = S.n_map_surf_in; C.n_map_full_in = S.n_map_full_in;
-    for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = S.h_map.q_wodom[k];
-    for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = S.h_map.t_wodom[k];
-    // the three clouds, their counts and the odometry pose in ONE launch (this hand-off sits on the
-    // mapping stage's critical path: five separate copies / kernels cost ~15 us more)
-    ForwardJob j;
-    j.src[0] = S.d_map_corner_in; j.src[1] = S.d_map_surf_in; j.src[2] = S.d_map_full_in;
-    j.dst[0] = C.d_map_corner_in; j.dst[1] = C.d_map_surf_in; j.dst[2] = C.d_map_full_in;
-    j.n[0] = C.n_map_corner_in; j.n[1] = C.n_map_surf_in; j.n[2] = C.n_map_full_in;
-    j.counts = C.d_map_in_n;
-    j.pose_dst = (double*)((char*)C.d_map + offsetof(MapState, q_wodom));   // q_wodom[4], t_wodom[3] adjacent
-    std::memcpy(j.pose, C.h_map.q_wodom, sizeof(j.pose));
-    const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
-    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
-    HIPCHK(hipGetLastError());
-    handoff_done(S, C);
-    C.have_map_input = true;
-    S.have_map_input = false;
+    // the source's stream is idle (its API calls return synchronised); the clouds, their counts and the
+    // odometry pose go over in ONE launch (five separate copies / kernels cost ~15 us more)
+    MapSnapshot snap;
+    snapshot_mapping_input(S, &snap);
+    forward_snapshot(C, snap, C.ev_handoff);
+    HIPCHK(hipStreamWaitEvent(S.stream, C.ev_handoff, 0));   // the source publishes again only after the copy
     API_END
 }
 
@@ -911,10 +978,10 @@ int aloam_voxel_grid(aloam_ctx* ctx, const float* pts, int n, float leaf, aloam_
     if (n < 0 || (n > 0 && !pts) || !out || !(leaf > 0)) throw ApiError{ALOAM_E_ARG, "bad voxel input"};
     if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "too many points"};
     if (n) HIPCHK(hipMemcpyAsync(C.d_in, pts, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
-    set_counts2(C, C.d_map_in_n, n, 0);
-    voxel_grid_sorted(C, C.d_in, C.d_map_in_n, n, leaf, C.d_cl, C.d_stack_n);
+    set_counts2(C, C.d_tmp_n, n, 0);
+    voxel_grid_sorted(C, C.d_in, C.d_tmp_n, n, leaf, C.d_cl, C.d_tmp_n + 1);
     int nout = 0;
-    HIPCHK(hipMemcpyAsync(&nout, C.d_stack_n, sizeof(int), hipMemcpyDeviceToHost, C.stream));
+    HIPCHK(hipMemcpyAsync(&nout, C.d_tmp_n + 1, sizeof(int), hipMemcpyDeviceToHost, C.stream));
     sync(C);
     d2h_cloud(C, C.d_cl, nout, out);
     sync(C);
@@ -928,10 +995,10 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
     if (n > C.cap_in || nq > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "too many points"};
     if (n) HIPCHK(hipMemcpyAsync(C.d_in, pts, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
     if (nq) HIPCHK(hipMemcpyAsync(C.d_cl, queries, sizeof(float4) * nq, hipMemcpyHostToDevice, C.stream));
-    set_counts2(C, C.d_map_in_n, n, 0);
+    set_counts2(C, C.d_tmp_n, n, 0);
     Grid g = C.g_surf_last;      // borrow the odometry surf grid's storage with the requested radius
     g.min_cell = radius * 1.025f;
-    grid_build(C, g, C.d_in, C.d_map_in_n, std::max(n, 1), nullptr, nullptr);
+    grid_build(C, g, C.d_in, C.d_tmp_n, std::max(n, 1), nullptr, nullptr);
     int* d_idx = (int*)C.d_scratch_i;
     float* d_d2 = (float*)(C.d_scratch_i + (size_t)nq * k);
     if ((size_t)nq * k * 2 > 3 * (size_t)C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "too many queries"};
@@ -994,18 +1061,15 @@ int aloam_set_cu_mask(aloam_ctx* ctx, const unsigned* mask, int nwords) {
     if (nwords > 0 && n == 0) throw ApiError{ALOAM_E_ARG, "CU mask selects no CU"};
     HIPCHK(hipStreamSynchronize(C.stream));
     HIPCHK(hipStreamSynchronize(C.stream2));
-    hipStream_t s1 = nullptr, s2 = nullptr;
-    if (nwords > 0) {
-        HIPCHK(hipExtStreamCreateWithCUMask(&s1, (uint32_t)nwords, mask));
-        HIPCHK(hipExtStreamCreateWithCUMask(&s2, (uint32_t)nwords, mask));
-    } else {
-        HIPCHK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-    }
+    if (C.stream3) HIPCHK(hipStreamSynchronize(C.stream3));
+    C.cu_mask.assign(mask, mask + nwords);
+    hipStream_t s1 = make_stream(C), s2 = make_stream(C), s3 = C.stream3 ? make_stream(C, true) : nullptr;
     (void)hipStreamDestroy(C.stream);
     (void)hipStreamDestroy(C.stream2);
+    if (C.stream3) (void)hipStreamDestroy(C.stream3);
     C.stream = s1;
     C.stream2 = s2;
+    C.stream3 = s3;
     C.n_cus = nwords > 0 ? n : prop.multiProcessorCount;
     API_END
 }

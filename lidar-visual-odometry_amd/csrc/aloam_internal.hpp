@@ -91,7 +91,7 @@ struct DevOut {
     int round_cnt[4 * ALOAM_MAX_ROUNDS];
     aloam_lm_summary lm_sum[2 * ALOAM_MAX_ROUNDS];
     int map_n[2];
-    int stack_n[2];
+    int stack_n[4];                  // [set][corner, surf]
     unsigned long long cand[2];
     MapState map;
 };
@@ -186,11 +186,28 @@ struct Ctx {
     int* d_cube_off = nullptr;                           // [2][CUBE_N + 1]
     unsigned char* d_cube_valid = nullptr;               // [CUBE_N]
     Grid g_map_corner, g_map_surf;
+    // mapping input, double-buffered (MapInSet): odometry publishes / a hand-off is forwarded into the set
+    // frame k does not read; the current set is mset[in_cur], aliased by the d_map_*_in / n_map_*_in fields
+    struct MapInSet {
+        float4 *corner = nullptr, *surf = nullptr, *full = nullptr;
+        int* n = nullptr;                  // device [2]: corner / surf counts
+        double* pose = nullptr;            // device [8]: q_wodom[4], t_wodom[3] (laser_odom_to_init)
+        float4 *cstack = nullptr, *sstack = nullptr;   // the frame's VoxelGrid'ed stacks (:542-550)
+        int nc = 0, ns = 0, nf = 0;        // host counts
+        bool stacks = false;               // stacks already voxelised on stream3 (event `ready`)
+        hipEvent_t ready = nullptr;        // stream3: stacks of this set done
+        hipEvent_t released = nullptr;     // stream: the last frame reading this set done
+    };
+    MapInSet mset[2];
+    int in_cur = 0;
     float4 *d_map_corner_in = nullptr, *d_map_surf_in = nullptr, *d_map_full_in = nullptr;
-    float4 *d_map_corner_alt = nullptr, *d_map_surf_alt = nullptr, *d_map_full_alt = nullptr;   // publish ping-pong
     int n_map_corner_in = 0, n_map_surf_in = 0, n_map_full_in = 0;
-    float4 *d_cstack = nullptr, *d_sstack = nullptr;
-    int* d_stack_n = nullptr;                            // [2]
+    hipStream_t stream3 = nullptr;       // mapping: forward + stack VoxelGrid of the next hand-off (created on first use)
+    std::vector<unsigned> cu_mask;       // aloam_set_cu_mask (empty: all CUs), applied to stream / stream2
+    std::vector<unsigned> cu_mask_side;  // stream3's CUs (empty: cu_mask); disjoint from cu_mask keeps the
+                                         // cross-workgroup LM kernels of `stream` co-resident
+    KindScratch ksv;                     // stack VoxelGrid scratch of stream3
+    int* d_tmp_n = nullptr;              // [2] counts scratch of the utility entry points
     int* d_nbr = nullptr;                                // [queries][5] neighbour slots
     float4* d_registered = nullptr;
     int n_registered = 0;
@@ -205,7 +222,7 @@ struct Ctx {
     float4* d_ins_pts = nullptr; int* d_ins_val = nullptr; int* d_ins_val2 = nullptr;
     float4* d_map_tmp = nullptr;                         // per-cube filter output (map capacity)
     unsigned long long* d_seg_keys = nullptr;            // per-cube filter key scratch (4 x map capacity)
-    int* d_map_in_n = nullptr;                           // [2] corner / surf input counts (device)
+    int* d_map_in_n = nullptr;                           // [2] corner / surf input counts of mset[in_cur] (device)
     int* d_last_n = nullptr;                             // [2] corner_last / surf_last counts (device)
     unsigned long long* d_cand = nullptr;                // [2] candidate counters (profiling)
 
@@ -222,8 +239,9 @@ struct Ctx {
     long m_issued = 0, m_done = 0;
     int m_pend[2][2] = {{0, 0}, {0, 0}};  // corner / surf stack upper bounds of the frame (map growth)
     int m_nfull[2] = {0, 0};
+    int m_set[2] = {0, 0};               // input set of the frame
     struct GraphSlot { const void* key[2] = {nullptr, nullptr}; int n = -1; hipGraphExec_t exec = nullptr; };
-    GraphSlot graphs[3];             // 0,1: odometry rounds (last-cloud buffer parity), 2: mapping rounds
+    GraphSlot graphs[4];             // 0,1: odometry rounds (last-cloud buffer parity), 2,3: mapping rounds (input set)
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling
     int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
@@ -277,13 +295,15 @@ void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, i
 size_t voxel_sort_tmp_bytes(int cap);
 size_t cube_sort_tmp_bytes(int cap);
 // lane 0: C.stream + the primary scratch; lane 1: C.stream2 + the second scratch set
+void voxel_grid_sorted_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* pts, const int* d_n, int cap_n, float leaf,
+                          float4* out, int* d_nout, bool hdr_armed);
 void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane = 0,
                        bool hdr_armed = false);
 unsigned* voxel_hdr(Ctx& C, int lane);   // bb[6] + nrun of the lane's VoxelGrid header (device)
 void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit, int lane = 0);
 void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so far
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
-void map_frame_launch(Ctx& C, aloam_map_result* R);
+void map_frame_launch(Ctx& C, int input_set);
 void* dalloc(Ctx& C, size_t bytes);
 // the odometry -> mapping hand-off as a value: published buffers (valid until the publish after next),
 // counts and pose; the native pipeline forwards it from its mapping thread (aloam_api.hip)
@@ -293,6 +313,9 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied);
 // laserMapping split in two so the host can issue frame k while the GPU still runs frame k-1 (at most
 // two frames in flight; every launch size of frame k is an upper bound known before k-1 completes)
 void mapping_issue(Ctx& C);
+void use_input_set(Ctx& C, int t);
+hipStream_t make_stream(Ctx& C, bool side = false);   // a stream on the context's (side) CU mask
+void set_side_cu_mask(Ctx& C, const unsigned* mask, int nwords);   // mset[t] becomes the current mapping input (aliases updated)
 void mapping_complete(Ctx& C, aloam_map_result* R);
 // scan-to-map registration + shard communicator (k_s2m.hip)
 void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns, int flags);

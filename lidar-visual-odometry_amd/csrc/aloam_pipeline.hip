@@ -251,15 +251,22 @@ aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int sta
         const int F = env ? std::atoi(env) : ncu / 2;
         const char* env3 = std::getenv("ALOAM_PIPE_CU_SPLIT3");
         const int F3 = env3 ? std::atoi(env3) : F / 3;
-        if (F > 0 && F < ncu && (stages == 2 || (F3 > 0 && F3 < F))) {
+        if (F > 0 && F < ncu && (stages == 2 || (F3 > 0 && F3 <= F))) {   // F3 == F: both front stages on [0, F)
             auto range = [&](int a, int b) {
                 std::vector<unsigned> m(nw, 0u);
                 for (int c = a; c < b; c++) m[c / 32] |= 1u << (c % 32);
                 return m;
             };
-            const std::vector<unsigned> mf = range(0, stages == 3 ? F3 : F), mo = range(F3, F), mm = range(F, ncu);
+            // 2 stages with ALOAM_SIDE_STACKS=1 (opt-in, see forward_snapshot): the mapping context's stream3
+            // may get the last ALOAM_PIPE_SIDE_CUS CUs of its range to itself (default 0 = shared; measured
+            // 715-757 scans/s with 8-32 CUs of its own vs 736 shared: not the cause of the slowdown)
+            const char* envs = std::getenv("ALOAM_PIPE_SIDE_CUS");
+            const int SIDE = stages == 2 ? std::max(0, std::min(envs ? std::atoi(envs) : 0, (ncu - F) / 2)) : 0;
+            const std::vector<unsigned> mf = range(0, stages == 3 ? F3 : F), mo = range(F3 == F ? 0 : F3, F),
+                                        mm = range(F, ncu - SIDE), mside = range(ncu - SIDE, ncu);
             if (aloam_set_cu_mask(P->front, mf.data(), nw) || (stages == 3 && aloam_set_cu_mask(P->odom, mo.data(), nw)) ||
-                aloam_set_cu_mask(P->back, mm.data(), nw)) {
+                aloam_set_cu_mask(P->back, mm.data(), nw) ||
+                (SIDE > 0 && guarded([&] { aloam::set_side_cu_mask(*(aloam::Ctx*)P->back, mside.data(), nw); }, P->err))) {
                 aloam_destroy(P->back);
                 if (stages == 3) aloam_destroy(P->odom);
                 aloam_destroy(P->front);

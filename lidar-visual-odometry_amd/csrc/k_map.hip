@@ -44,7 +44,8 @@ __device__ inline float4 associate_to_map(const double* par, float4 p) {   // :1
 
 // also zeroes this frame's mapping round counters and arms the stacks' VoxelGrid headers (saves three
 // launches on the host-issue-bound part of the frame)
-__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* round_cnt, unsigned* vox_bb0, unsigned* vox_bb1) {
+__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* round_cnt, unsigned* vox_bb0, unsigned* vox_bb1,
+                              const double* pose_in) {
     __shared__ int valid_num;
     if (threadIdx.x < 2 * ALOAM_MAX_ROUNDS) round_cnt[threadIdx.x] = 0;
     if (threadIdx.x < 8) {                      // VoxHdr {bb[6], nrun, pad} of both lanes
@@ -52,6 +53,8 @@ __global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* round
         if (threadIdx.x < 7) { vox_bb0[threadIdx.x] = v; vox_bb1[threadIdx.x] = v; }
     }
     if (threadIdx.x == 0) {
+        for (int k = 0; k < 4; k++) m->q_wodom[k] = pose_in[k];      // the input set's laser_odom_to_init
+        for (int k = 0; k < 3; k++) m->t_wodom[k] = pose_in[4 + k];
         // transformAssociateToMap (:142-146)
         const dquat qm{m->q_wmap_wodom[0], m->q_wmap_wodom[1], m->q_wmap_wodom[2], m->q_wmap_wodom[3]};
         const dquat qo{m->q_wodom[0], m->q_wodom[1], m->q_wodom[2], m->q_wodom[3]};
@@ -688,53 +691,60 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
 // The whole laserMapping frame; results are read back by the caller (aloam_api.hip).
 static const int g_exp = getenv("ALOAM_EXP") ? atoi(getenv("ALOAM_EXP")) : 0;   // profiling experiments only
 static int g_map_exp() { return g_exp; }
-void map_frame_launch(Ctx& C, aloam_map_result* R) {
+void map_frame_launch(Ctx& C, int X) {
     hipStream_t st = C.stream;
-    (void)R;
-    const int ub_c = C.n_map_corner_in, ub_s = C.n_map_surf_in;
-    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, voxel_hdr(C, 0), voxel_hdr(C, 1));
+    Ctx::MapInSet& in = C.mset[X];
+    int* stack_n = C.d_out->stack_n + 2 * X;
+    const int ub_c = in.nc, ub_s = in.ns;
+    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, voxel_hdr(C, 0), voxel_hdr(C, 1),
+                                     in.pose);
     k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
     const GridBuild gb[2] = {{&C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid},
                              {&C.g_map_surf, C.d_ms, C.d_map_n + 1, std::max(C.n_ms, 1), C.d_ms_cube, C.d_cube_valid}};
     grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
-    // stacks (:542-550)
-    fork_lane1(C);
-    voxel_grid_sorted(C, C.d_map_corner_in, C.d_map_in_n + 0, ub_c, C.P.mapping_line_resolution, C.d_cstack, C.d_stack_n + 0, 0, true);
-    voxel_grid_sorted(C, C.d_map_surf_in, C.d_map_in_n + 1, ub_s, C.P.mapping_plane_resolution, C.d_sstack, C.d_stack_n + 1, 1, true);
-    join_lane1(C);
+    // stacks (:542-550): voxelised on stream3 when the input came as a hand-off, else here in two lanes
+    if (in.stacks) {
+        HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
+    } else {
+        fork_lane1(C);
+        voxel_grid_sorted(C, in.corner, in.n + 0, ub_c, C.P.mapping_line_resolution, in.cstack, stack_n + 0, 0, true);
+        voxel_grid_sorted(C, in.surf, in.n + 1, ub_s, C.P.mapping_plane_resolution, in.sstack, stack_n + 1, 1, true);
+        join_lane1(C);
+    }
+    in.stacks = false;
     const int nq = ub_c + ub_s;
     C.t_rounds_issued = std::chrono::steady_clock::now();
     if (nq > 0) {
         if (nq > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity exceeded"};
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
-        // every size comes from the device (stack counts, grids, gate): one fixed launch sequence
-        auto issue = [&C, st, rounds](bool marks, int live_hint) {
+        // every size comes from the device (stack counts, grids, gate): one fixed launch sequence per set
+        auto issue = [&C, st, rounds, &in, stack_n](bool marks, int live_hint) {
             for (int it = 0; it < rounds; it++) {
                 if (marks) prof_mark(C, 6 + 2 * (ALOAM_MAX_ROUNDS + it));
                 k_map_assoc<<<ASSOC_BLOCKS, 256, 0, st>>>(
-                    C.d_cstack, C.d_sstack, C.d_stack_n,
+                    in.cstack, in.sstack, stack_n,
                     C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
                     C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
                     C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it, C.profiling ? C.d_cand : nullptr, g_exp);
                 if (marks) prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
                 lm_run(C, C.d_factors, C.cap_factors, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize,
-                       C.d_stack_n, live_hint);
+                       stack_n, live_hint);
             }
         };
         const int hint = C.map_slots_hint > 0 ? C.map_slots_hint : 4096;
         if (C.profiling || !C.use_graphs) issue(true, hint);
-        else run_graph(C, 2, nullptr, nullptr, rounds, [&] { issue(false, hint); });
+        else run_graph(C, 2 + X, in.cstack, in.sstack, rounds, [&] { issue(false, hint); });
     }
     k_map_update<<<1, 1, 0, st>>>(C.d_map);
     if (!(g_exp & 4)) {              // (profiling experiment 4: skip the map update — results invalid)
         fork_lane1(C);
-        rebuild_map(C, 0, ub_c, C.d_cstack, C.d_stack_n + 0, C.P.mapping_line_resolution);
-        rebuild_map(C, 1, ub_s, C.d_sstack, C.d_stack_n + 1, C.P.mapping_plane_resolution);
+        rebuild_map(C, 0, ub_c, in.cstack, stack_n + 0, C.P.mapping_line_resolution);
+        rebuild_map(C, 1, ub_s, in.sstack, stack_n + 1, C.P.mapping_plane_resolution);
         join_lane1(C);
     }
-    if (C.n_map_full_in > 0)
-        k_map_register<<<(C.n_map_full_in + MB - 1) / MB, MB, 0, st>>>(C.d_map_full_in, C.n_map_full_in, C.d_map, C.d_registered);
+    if (in.nf > 0)
+        k_map_register<<<(in.nf + MB - 1) / MB, MB, 0, st>>>(in.full, in.nf, C.d_map, C.d_registered);
     HIPCHK(hipGetLastError());
 }
 

@@ -114,8 +114,11 @@ unsigned* voxel_hdr(Ctx& C, int lane) {   // the lane's VoxHdr lives behind its 
 
 void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane,
                        bool hdr_armed) {
-    hipStream_t st = lane ? C.stream2 : C.stream;
-    KindScratch& K = C.ks[lane];
+    voxel_grid_sorted_on(C, lane ? C.stream2 : C.stream, C.ks[lane], pts, d_n, cap_n, leaf, out, d_nout, hdr_armed);
+}
+
+void voxel_grid_sorted_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* pts, const int* d_n, int cap_n, float leaf,
+                          float4* out, int* d_nout, bool hdr_armed) {
     if (cap_n <= 0) { HIPCHK(hipMemsetAsync(d_nout, 0, sizeof(int), st)); return; }
     if (cap_n > C.cap_voxel) throw ApiError{ALOAM_E_CAPACITY, "voxel grid capacity exceeded"};
     VoxHdr* h = (VoxHdr*)(K.vvals2 + C.cap_voxel);   // header lives behind the value buffer

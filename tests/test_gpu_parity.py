@@ -313,6 +313,48 @@ def test_pipeline_matches_single_context(lvo, stages):
         np.testing.assert_allclose(m["q_w_curr"], m_ref["q_w_curr"], rtol=1e-9, atol=1e-12)
 
 
+_SIDE_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from lvo_amd_loader import lvo
+synth = lvo.synth
+p = lvo.abi.default_params(16)
+pipe = lvo.Pipeline(p)
+mps = []
+for k in range(7):
+    od, mp = pipe.push(synth.scan("vlp16", k))
+    if mp is not None:
+        mps.append(list(mp["t_w_curr"]) + list(mp["q_w_curr"]))
+for od, mp in pipe.flush():
+    if mp is not None:
+        mps.append(list(mp["t_w_curr"]) + list(mp["q_w_curr"]))
+pipe.close()
+print(json.dumps(mps))
+"""
+
+
+def test_pipeline_side_stream_stacks(lvo):
+    """ALOAM_SIDE_STACKS=1 (opt-in): hand-off copy and stack VoxelGrid on the mapping context's third
+    stream, overlapping the previous frame, over double-buffered input sets — same trajectory."""
+    import json
+    import os
+    import subprocess
+    import sys
+    p = abi.default_params(16)
+    ref = lvo.Context(p)
+    ro = [ref.process_scan(synth.scan("vlp16", k))[1] for k in range(7)]
+    ref.close()
+    env = dict(os.environ, ALOAM_SIDE_STACKS="1")
+    out = subprocess.run([sys.executable, "-c", _SIDE_SCRIPT, os.path.dirname(os.path.abspath(__file__))], env=env,
+                         capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    mps = json.loads(out.stdout.strip().splitlines()[-1])
+    assert len(mps) == 7
+    for m, m_ref in zip(mps, ro):
+        np.testing.assert_allclose(m[:3], m_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(m[3:], m_ref["q_w_curr"], rtol=1e-9, atol=1e-12)
+
+
 def test_pipeline_errors_and_timing(lvo):
     """The native pipeline reports stage errors through aloam_pipeline_last_error and stays usable;
     with profiling on, every stage's HIP-event timing of its last job is available."""
