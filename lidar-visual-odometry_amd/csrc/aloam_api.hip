@@ -38,16 +38,21 @@ void prof_mark(Ctx& C, int idx) {
 __global__ void k_set2(int* dst, int a, int b) { dst[0] = a; dst[1] = b; }
 void set_counts2(Ctx& C, int* dst, int a, int b) { k_set2<<<1, 1, 0, C.stream>>>(dst, a, b); }
 struct Vec7 { double v[7]; };
-struct ForwardJob { const float4* src[3]; float4* dst[3]; int n[3]; int* counts; double* pose_dst; double pose[7];
-                   const double* pose_src = nullptr; };   // pose_src (device) overrides pose
-// y = cloud (corner, surf, full): grid-stride copy; block (0, 0) also writes the counts and the pose
+// clouds 0-2: corner, surf, full (host counts n); 3-4 (optional): the VoxelGrid'ed corner / surf stacks,
+// n = upper bound, the live count read from ndev on the device and copied to stack_counts
+struct ForwardJob { const float4* src[5] = {}; float4* dst[5] = {}; int n[5] = {}; const int* ndev[5] = {};
+                    int* counts = nullptr; int* stack_counts = nullptr; double* pose_dst = nullptr; double pose[7] = {};
+                    const double* pose_src = nullptr; };   // pose_src (device) overrides pose
+// y = cloud: grid-stride copy; block (0, 0) also writes the counts and the pose
 __global__ void k_forward_map_input(ForwardJob j) {
     const int c = blockIdx.y;
     const float4* __restrict__ src = j.src[c];
     float4* __restrict__ dst = j.dst[c];
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < j.n[c]; i += gridDim.x * blockDim.x) dst[i] = src[i];
+    const int n = j.ndev[c] ? min(j.n[c], *j.ndev[c]) : j.n[c];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
     if (blockIdx.x == 0 && c == 0) {
         if (threadIdx.x < 2) j.counts[threadIdx.x] = j.n[threadIdx.x];
+        if (threadIdx.x < 2 && j.stack_counts) j.stack_counts[threadIdx.x] = min(j.n[3 + threadIdx.x], *j.ndev[3 + threadIdx.x]);
         if (threadIdx.x < 7) j.pose_dst[threadIdx.x] = j.pose_src ? j.pose_src[threadIdx.x] : j.pose[threadIdx.x];
     }
 }
@@ -224,6 +229,7 @@ void run_graph(Ctx& C, int slot, const void* k0, const void* k1, int n, const st
     if (!g.exec || g.key[0] != k0 || g.key[1] != k1 || g.n != n) {
         if (g.exec) { (void)hipGraphExecDestroy(g.exec); g.exec = nullptr; }
         hipGraph_t graph = nullptr;
+        std::lock_guard<std::mutex> lk(C.capture_mu);
         HIPCHK(hipStreamBeginCapture(C.stream, hipStreamCaptureModeThreadLocal));
         try {
             issue();
@@ -389,6 +395,20 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
         k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
         HIPCHK(hipGetLastError());
+        if (C.publish_stacks) {
+            // the mapping stacks (laserMapping.cpp:542-550) depend on this publish only: voxelised here on
+            // the otherwise idle stream2 (overlapping this context's next scan) and handed over with the
+            // clouds, which takes them off the mapping stage's critical path
+            fork_lane1(C);
+            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
+                                 C.d_out->stack_n + 2 * t + 0, false);
+            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
+                                 C.d_out->stack_n + 2 * t + 1, false);
+            HIPCHK(hipEventRecord(m.ready, C.stream2));
+            m.stacks_pub = true;
+        } else {
+            m.stacks_pub = false;
+        }
         use_input_set(C, t);
         C.have_map_input = true;
     }
@@ -446,6 +466,11 @@ void mapping_issue(Ctx& C) {
     C.have_map_input = false;
     C.map_frame_count++;
     C.m_issued++;
+}
+
+bool mapping_ready(Ctx& C) {
+    if (C.m_done == C.m_issued) return false;
+    return hipEventQuery(C.ev_mdone[(int)(C.m_done & 1)]) == hipSuccess;
 }
 
 void mapping_complete(Ctx& C, aloam_map_result* R) {
@@ -521,6 +546,11 @@ static void do_mapping(Ctx& C, aloam_map_result* R) {
 void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
     if (!S.have_map_input) throw ApiError{ALOAM_E_STATE, "source has no published odometry output"};
     o->src[0] = S.d_map_corner_in; o->src[1] = S.d_map_surf_in; o->src[2] = S.d_map_full_in;
+    const Ctx::MapInSet& m = S.mset[S.in_cur];
+    o->has_stacks = m.stacks_pub;
+    o->stk[0] = m.cstack; o->stk[1] = m.sstack;
+    o->stk_n = S.d_out->stack_n + 2 * S.in_cur;
+    o->stk_ready = m.ready;
     o->n[0] = S.n_map_corner_in; o->n[1] = S.n_map_surf_in; o->n[2] = S.n_map_full_in;
     for (int k = 0; k < 4; k++) o->pose[k] = S.h_map.q_wodom[k];
     for (int k = 0; k < 3; k++) o->pose[4 + k] = S.h_map.t_wodom[k];
@@ -590,11 +620,25 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
     j.counts = m.n;
     j.pose_dst = m.pose;
     std::memcpy(j.pose, s.pose, sizeof(j.pose));
+    int ncl = 3;
+    if (s.has_stacks) {               // stacks voxelised by the source (its stream2): copied with the clouds
+        HIPCHK(hipStreamWaitEvent(fs, s.stk_ready, 0));
+        for (int k = 0; k < 2; k++) {
+            j.src[3 + k] = s.stk[k];
+            j.dst[3 + k] = k ? m.sstack : m.cstack;
+            j.n[3 + k] = s.n[k];
+            j.ndev[3 + k] = s.stk_n + k;
+        }
+        j.stack_counts = C.d_out->stack_n + 2 * t;
+        ncl = 5;
+    }
     const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
-    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, fs>>>(j);
+    k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), ncl), 256, 0, fs>>>(j);
     HIPCHK(hipGetLastError());
     if (copied) HIPCHK(hipEventRecord(copied, fs));
-    if (side) prepare_stacks(C, t);
+    m.stacks_pub = s.has_stacks;      // present in this set once `ready` (recorded behind the copy) fires
+    if (s.has_stacks) HIPCHK(hipEventRecord(m.ready, fs));
+    if (side && !s.has_stacks) prepare_stacks(C, t);
     else m.stacks = false;
     use_input_set(C, t);
     C.have_map_input = true;
@@ -850,7 +894,7 @@ int aloam_set_mapping_input(aloam_ctx* ctx, const float* corner, int nc, const f
     Ctx::MapInSet& m = C.mset[ti];
     if (nc > 0) HIPCHK(hipMemcpyAsync(m.corner, corner, sizeof(float4) * nc, hipMemcpyHostToDevice, C.stream));
     if (ns > 0) HIPCHK(hipMemcpyAsync(m.surf, surf, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
-    m.nc = nc; m.ns = ns; m.nf = 0; m.stacks = false;
+    m.nc = nc; m.ns = ns; m.nf = 0; m.stacks = false; m.stacks_pub = false;
     set_counts2(C, m.n, nc, ns);
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = q[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = t[k];

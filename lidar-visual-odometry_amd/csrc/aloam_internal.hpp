@@ -6,6 +6,7 @@
 #include <chrono>
 #include <functional>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/aloam_hip.h"
@@ -195,6 +196,8 @@ struct Ctx {
         float4 *cstack = nullptr, *sstack = nullptr;   // the frame's VoxelGrid'ed stacks (:542-550)
         int nc = 0, ns = 0, nf = 0;        // host counts
         bool stacks = false;               // stacks already voxelised on stream3 (event `ready`)
+        bool stacks_pub = false;           // stacks present in cstack / sstack (voxelised at publish, or
+                                           // copied in with a hand-off); counts in DevOut::stack_n[2 set]
         hipEvent_t ready = nullptr;        // stream3: stacks of this set done
         hipEvent_t released = nullptr;     // stream: the last frame reading this set done
     };
@@ -203,6 +206,7 @@ struct Ctx {
     float4 *d_map_corner_in = nullptr, *d_map_surf_in = nullptr, *d_map_full_in = nullptr;
     int n_map_corner_in = 0, n_map_surf_in = 0, n_map_full_in = 0;
     hipStream_t stream3 = nullptr;       // mapping: forward + stack VoxelGrid of the next hand-off (created on first use)
+    bool publish_stacks = false;         // odometry publish also voxelises the mapping stacks (pipeline front)
     std::vector<unsigned> cu_mask;       // aloam_set_cu_mask (empty: all CUs), applied to stream / stream2
     std::vector<unsigned> cu_mask_side;  // stream3's CUs (empty: cu_mask); disjoint from cu_mask keeps the
                                          // cross-workgroup LM kernels of `stream` co-resident
@@ -243,6 +247,10 @@ struct Ctx {
     struct GraphSlot { const void* key[2] = {nullptr, nullptr}; int n = -1; hipGraphExec_t exec = nullptr; };
     GraphSlot graphs[4];             // 0,1: odometry rounds (last-cloud buffer parity), 2,3: mapping rounds (input set)
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling
+    // held while `stream` is being captured: another thread making its stream wait on an event of this
+    // context (the pipeline front on a hand-off's `copied`) must not do so mid-capture, or HIP fails the
+    // wait with hipErrorStreamCaptureIsolation
+    std::mutex capture_mu;
     int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
     std::chrono::steady_clock::time_point t_rounds_issued{};   // host-issue profiling (ALOAM_HOST_TIMING)
@@ -307,7 +315,13 @@ void map_frame_launch(Ctx& C, int input_set);
 void* dalloc(Ctx& C, size_t bytes);
 // the odometry -> mapping hand-off as a value: published buffers (valid until the publish after next),
 // counts and pose; the native pipeline forwards it from its mapping thread (aloam_api.hip)
-struct MapSnapshot { const float4* src[3]; int n[3]; double pose[7]; };
+struct MapSnapshot {
+    const float4* src[3]; int n[3]; double pose[7];
+    bool has_stacks = false;           // the source voxelised the stacks (publish_stacks): copied along
+    const float4* stk[2] = {nullptr, nullptr};
+    const int* stk_n = nullptr;        // device [2]
+    hipEvent_t stk_ready = nullptr;    // source stream2: stacks done
+};
 void snapshot_mapping_input(Ctx& S, MapSnapshot* out);
 void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied);
 // laserMapping split in two so the host can issue frame k while the GPU still runs frame k-1 (at most
@@ -317,6 +331,7 @@ void use_input_set(Ctx& C, int t);
 hipStream_t make_stream(Ctx& C, bool side = false);   // a stream on the context's (side) CU mask
 void set_side_cu_mask(Ctx& C, const unsigned* mask, int nwords);   // mset[t] becomes the current mapping input (aliases updated)
 void mapping_complete(Ctx& C, aloam_map_result* R);
+bool mapping_ready(Ctx& C);          // the oldest frame in flight has finished on the GPU
 // scan-to-map registration + shard communicator (k_s2m.hip)
 void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns, int flags);
 void s2m_set_queries(Ctx& C, const float* corner, int ncq, const float* surf, int nsq, int flags);

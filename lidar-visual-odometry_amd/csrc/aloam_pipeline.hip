@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 #include <condition_variable>
@@ -102,7 +104,14 @@ struct MapServer {
     std::string err[2];
     hipEvent_t copied[2] = {nullptr, nullptr};   // after the copy of hand-off j (index j & 1)
     long returned = 0;                           // results handed to the caller
+    // ALOAM_PIPE_TIMING (profiling aid): host-side stage occupancy, printed at destroy
+    double t_fwd = 0, t_issue = 0, t_complete = 0, t_idle = 0, t_front = 0, t_take = 0;
+    long n_srv = 0, n_front = 0;
 };
+static const bool g_pipe_timing = std::getenv("ALOAM_PIPE_TIMING") != nullptr;
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 }  // namespace
 
 struct aloam_pipeline {
@@ -159,13 +168,16 @@ void map_server(aloam_pipeline* P) {
     long inflight = -1;
     auto complete = [&](long j) {
         const int i = (int)(j & 1);
+        const double t0 = g_pipe_timing ? now_us() : 0;
         const int rc = guarded([&] { aloam::mapping_complete(B, &S.res[i]); }, S.err[i]);
+        if (g_pipe_timing) S.t_complete += now_us() - t0;
         if (!rc && P->profiling) aloam_get_timing(P->back, &S.tim[i]);
         S.rc[i] = rc;
         S.done.store(j + 1, std::memory_order_release);
     };
     for (long j = 0;;) {
         int spins = 0;
+        const double ti = g_pipe_timing ? now_us() : 0;
         while (S.posted.load(std::memory_order_acquire) <= j) {
             if (inflight >= 0) { complete(inflight); inflight = -1; continue; }
             if (S.quit.load(std::memory_order_acquire)) return;
@@ -176,9 +188,15 @@ void map_server(aloam_pipeline* P) {
         }
         const int i = (int)(j & 1);
         std::string e;
+        double t1 = 0, t2 = 0;
+        if (g_pipe_timing) { t1 = now_us(); S.t_idle += t1 - ti; }
         int rc = guarded([&] { aloam::forward_snapshot(B, S.snap[i], S.copied[i]); }, e);
         S.issued.store(j + 1, std::memory_order_release);
+        if (g_pipe_timing) { t2 = now_us(); S.t_fwd += t2 - t1; }
+        // a frame that has already finished is handed back before the ~0.5 ms of launch issue below
+        if (inflight >= 0 && aloam::mapping_ready(B)) { complete(inflight); inflight = -1; }
         if (!rc) rc = guarded([&] { aloam::mapping_issue(B); }, e);
+        if (g_pipe_timing) { S.t_issue += now_us() - t2; S.n_srv++; }
         if (inflight >= 0) { complete(inflight); inflight = -1; }
         if (rc) {
             S.err[i] = e;
@@ -276,6 +294,9 @@ aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int sta
         }
     }
     if (stages == 2) {
+        // the front voxelises the mapping stacks of each publish on its stream2 (ALOAM_PIPE_FRONT_STACKS=0: off)
+        const char* fsenv = std::getenv("ALOAM_PIPE_FRONT_STACKS");
+        ((aloam::Ctx*)P->front)->publish_stacks = !fsenv || std::atoi(fsenv) != 0;
         for (auto& e : P->ms.copied)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
         P->ms.th = std::thread(map_server, P);
@@ -295,6 +316,12 @@ void aloam_pipeline_destroy(aloam_pipeline* P) {
         }
         P->ms.cv.notify_one();
         if (P->ms.th.joinable()) P->ms.th.join();
+        const MapServer& S = P->ms;
+        if (g_pipe_timing && S.n_srv > 0 && S.n_front > 0)
+            std::fprintf(stderr, "[aloam pipe] per scan (us): front process %.1f, front wait-for-result %.1f | server: "
+                         "idle %.1f, forward %.1f, issue %.1f, complete(wait+read) %.1f  (%ld / %ld)\n",
+                         S.t_front / S.n_front, S.t_take / S.n_front, S.t_idle / S.n_srv, S.t_fwd / S.n_srv,
+                         S.t_issue / S.n_srv, S.t_complete / S.n_srv, S.n_front, S.n_srv);
         for (auto& e : P->ms.copied) if (e) (void)hipEventDestroy(e);
     } else {
         P->wm.stop();
@@ -344,13 +371,21 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
             // this scan may publish into the buffer set hand-off seq-2 was taken from: its copy must be
             // issued (host) and finished (GPU) first
             while (S.issued.load(std::memory_order_acquire) < seq - 1) std::this_thread::yield();
-            if (hipSetDevice(F.device) != hipSuccess || hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0) != hipSuccess) {
-                P->err = "hipStreamWaitEvent failed";
+            hipError_t e = hipSetDevice(F.device);
+            if (e == hipSuccess) {
+                std::lock_guard<std::mutex> lk(((aloam::Ctx*)P->back)->capture_mu);   // not while mapping captures
+                e = hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0);
+            }
+            if (e != hipSuccess) {
+                P->err = std::string("hipStreamWaitEvent failed: ") + hipGetErrorName(e) + " (hand-off " +
+                         std::to_string(seq - 2) + ", server rc " + std::to_string(S.rc[seq & 1]) + " " + S.err[seq & 1] + ")";
                 return ALOAM_E_HIP;
             }
         }
         aloam_odom_result o{};
+        const double tf0 = g_pipe_timing ? now_us() : 0;
         rc = aloam_process_scan(P->front, xyzr, n, flags | ALOAM_NO_MAPPING, &o, nullptr);
+        if (g_pipe_timing) { S.t_front += now_us() - tf0; S.n_front++; }
         if (rc) return fail(P, P->front, rc);
         if (P->profiling) aloam_get_timing(P->front, &P->t_stage[0]), P->t_stage[1] = P->t_stage[0];
         *have_od = 1;
@@ -371,7 +406,12 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
             posted = true;
         }
         // the previous scan's mapping result (the job before the one just posted)
-        if (S.returned < S.posted.load(std::memory_order_relaxed) - (posted ? 1 : 0)) return take_result(P, mp, have_mp);
+        if (S.returned < S.posted.load(std::memory_order_relaxed) - (posted ? 1 : 0)) {
+            const double tt0 = g_pipe_timing ? now_us() : 0;
+            const int trc = take_result(P, mp, have_mp);
+            if (g_pipe_timing) S.t_take += now_us() - tt0;
+            return trc;
+        }
         return ALOAM_OK;
     }
     // three stages: scanRegistration here, odometry and mapping of earlier scans in the workers

@@ -696,6 +696,9 @@ void map_frame_launch(Ctx& C, int X) {
     Ctx::MapInSet& in = C.mset[X];
     int* stack_n = C.d_out->stack_n + 2 * X;
     const int ub_c = in.nc, ub_s = in.ns;
+    // an input set written on another stream (stream3 hand-off, or this context's stream2 stacks): its
+    // clouds, pose and stacks are complete at `ready` — wait before the first kernel that reads the pose
+    if (in.stacks_pub || in.stacks) HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
     k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, voxel_hdr(C, 0), voxel_hdr(C, 1),
                                      in.pose);
     k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
@@ -704,7 +707,11 @@ void map_frame_launch(Ctx& C, int X) {
     grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
     // stacks (:542-550): voxelised on stream3 when the input came as a hand-off, else here in two lanes
-    if (in.stacks) {
+    if (in.stacks_pub) {
+        // present already: voxelised at this context's own publish (stream2), or at the source's and
+        // copied in (this stream or stream3); `ready` is recorded behind either
+        HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
+    } else if (in.stacks) {
         HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
     } else {
         fork_lane1(C);
@@ -713,6 +720,7 @@ void map_frame_launch(Ctx& C, int X) {
         join_lane1(C);
     }
     in.stacks = false;
+    in.stacks_pub = false;
     const int nq = ub_c + ub_s;
     C.t_rounds_issued = std::chrono::steady_clock::now();
     if (nq > 0) {

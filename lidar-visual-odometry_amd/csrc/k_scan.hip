@@ -345,7 +345,8 @@ __device__ void dev_std_sort(int* first, int* last, CurvLess less) {
 // One workgroup (1024 threads) per scan line: (:277-408)
 constexpr int LT = 1024;
 constexpr int LINE_HDR = 256;                          // LDS header (LineShared) ahead of the line arrays
-constexpr size_t line_lds_bytes() { return LINE_HDR + (size_t)LINE_LDS_CAP * (4 * 4 + 4 + 8 + 2) + (LINE_LDS_CAP / 32 + 2) * 4; }
+constexpr size_t line_gapw_end() { return LINE_HDR + (size_t)LINE_LDS_CAP * (4 * 4 + 4 + 8 + 2) + (LINE_LDS_CAP / 32 + 2) * 4; }
+constexpr size_t line_lds_bytes() { return ((line_gapw_end() + 15) & ~(size_t)15) + (size_t)LINE_LDS_CAP * 8; }   // + sort output
 
 __device__ inline void suppress_neighbours(int ind, const float* X, const float* Y, const float* Z, volatile int8_t* picked) {
     for (int l = 1; l <= 5; l++) {
@@ -438,6 +439,51 @@ __device__ void bitonic_sort_reg4(unsigned long long* k, int n2) {
     __syncthreads();
 }
 
+// Ascending sort of n2 (a multiple of 64) u64 keys held in LDS into out[] (LDS): every 64-key chunk is
+// bitonic-sorted inside one wave (lane exchanges only), then each real key's rank is its position in
+// its chunk plus, per other chunk, the number of that chunk's keys below it (chunk bounds first, else
+// a 6-step binary search). No block-wide compare-exchange stages: the 2048-key bitonic network's ~60
+// dependent LDS/permute stages took ~27 us per line, this ~3-5 us. Keys other than the ~0 padding must
+// be distinct. Ends with a barrier.
+__device__ void chunk_rank_sort(unsigned long long* keys, unsigned long long* out, int n2) {
+    const int lane = lane_id(), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const int nch = n2 / WAVE;
+    for (int c = wv; c < nch; c += nw) {
+        unsigned long long v = keys[c * WAVE + lane];
+#pragma unroll
+        for (int size = 2; size <= WAVE; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const unsigned long long o = __shfl_xor(v, stride, WAVE);
+                const bool asc = (lane & size) == 0, lower = (lane & stride) == 0;
+                v = (lower == asc) ? (v < o ? v : o) : (v < o ? o : v);
+            }
+        }
+        keys[c * WAVE + lane] = v;
+        out[c * WAVE + lane] = ~0ull;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n2; e += blockDim.x) {
+        const unsigned long long x = keys[e];
+        if (x == ~0ull) continue;
+        const int c = e / WAVE;
+        int rank = e % WAVE;
+        for (int c2 = 0; c2 < nch; c2++) {
+            if (c2 == c) continue;
+            const unsigned long long* k = keys + c2 * WAVE;
+            if (k[WAVE - 1] < x) { rank += WAVE; continue; }
+            if (!(k[0] < x)) continue;
+            int lo = 0;
+#pragma unroll
+            for (int st = WAVE / 2; st >= 1; st >>= 1)
+                if (k[lo + st - 1] < x) lo += st;
+            rank += lo;
+        }
+        out[rank] = x;
+    }
+    __syncthreads();
+}
+
 #ifdef ALOAM_LF_TIMING
 __device__ unsigned long long g_lf_ts[64][8];      // micro-benchmark only: per-line phase stamps
 #define LF_TS(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts[blockIdx.x][k] = wall_clock64(); } while (0)
@@ -491,6 +537,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     int8_t* label;
     unsigned* gapw;         // bit i of word i/32: pair (i, i+1) is a suppression stop
     unsigned long long* keys;
+    unsigned long long* sorted = nullptr;   // LDS lines: chunk_rank_sort output
     if constexpr (!big) {
         X = (float*)smem;
         Y = X + LINE_LDS_CAP;
@@ -501,6 +548,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         picked = (int8_t*)(keys + LINE_LDS_CAP);
         label = (int8_t*)(picked + LINE_LDS_CAP);
         gapw = (unsigned*)(label + LINE_LDS_CAP);
+        sorted = (unsigned long long*)(smem_raw + ((line_gapw_end() + 15) & ~(size_t)15));
     } else {
         float* gx = (float*)g_xyz;     // 4 floats per cloud point of scratch
         X = gx + off0;
@@ -563,12 +611,12 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         }
         __syncthreads();
         LF_TS3(1);
-        bitonic_sort_reg4(keys, n2);
+        chunk_rank_sort(keys, sorted, n2);
         LF_TS3(2);
         for (int i = threadIdx.x; i < M; i += LT) {
-            const unsigned long long key = keys[i];
+            const unsigned long long key = sorted[i];
             S[s - off0 + i] = s + (int)(key & 0xfffu);
-            if (i > 0 && (keys[i - 1] >> 12) == (key >> 12)) {          // exact tie: sorted slots s+i-1, s+i
+            if (i > 0 && (sorted[i - 1] >> 12) == (key >> 12)) {        // exact tie: sorted slots s+i-1, s+i
                 atomicMin(&s_tlo[(int)(key >> 44)], s + i - 1);
                 atomicMax(&s_thi[(int)(key >> 44)], s + i);
             }
@@ -824,8 +872,13 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     }
     __syncthreads();
     LF_TS(4);
-    if (!big && n2 >= 256) bitonic_sort_reg4(keys, n2);
-    else bitonic_sort_u64(keys, n2);
+    if (!big && n2 >= WAVE) {
+        chunk_rank_sort(keys, sorted, n2);
+        for (int t = threadIdx.x; t < n2; t += LT) keys[t] = sorted[t];
+        __syncthreads();
+    } else {
+        bitonic_sort_u64(keys, n2);
+    }
     LF_TS(5);
     // run heads -> centroids; run r's head position stored in S[nc + r] region? reuse Cv as int
     int* heads = (int*)Cv;   // curvature no longer needed
