@@ -136,6 +136,8 @@ static void allocate(Ctx& C) {
     HIPCHK(hipHostGetDevicePointer((void**)&C.d_bar_err, C.h_bar_err, 0));
     C.d_lm_sum = C.d_out->lm_sum;
     C.d_round_cnt = C.d_out->round_cnt;
+    C.d_odom_spread = (int*)dalloc(C, sizeof(int) * ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE);
+    C.d_map_spread = (int*)dalloc(C, sizeof(int) * ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE);
     C.d_last_n = (int*)dalloc(C, sizeof(int) * 2);
     C.d_last_sorted = (int*)dalloc(C, sizeof(int) * 2);
     C.d_odom_nq = (int*)dalloc(C, sizeof(int) * 2);
@@ -338,7 +340,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     } else {
         r.optimized = 1;
         r.rounds = rounds;
-        HIPCHK(hipMemsetAsync(C.d_round_cnt, 0, sizeof(int) * 2 * ALOAM_MAX_ROUNDS, st));
+        HIPCHK(hipMemsetAsync(C.d_odom_spread, 0, sizeof(int) * ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, st));
         const int nslots = C.n_sharp + C.n_flat;
         if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
         set_counts2(C, C.d_odom_nq, C.n_sharp, C.n_flat);

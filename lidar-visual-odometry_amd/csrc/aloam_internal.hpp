@@ -17,6 +17,7 @@ constexpr int MAXL = 128;            // scan lines supported on device
 constexpr int LINE_SHARP_CAP = 12;   // 2 per segment x 6   (scanRegistration.cpp:301)
 constexpr int LINE_LSHARP_CAP = 120; // 20 per segment x 6  (:307)
 constexpr int LINE_FLAT_CAP = 24;    // 4 per segment x 6   (:359)
+constexpr int ODOM_CNT_SLOTS = 64, ODOM_CNT_STRIDE = 16;   // odometry search counters: 64 lines of 64 B per round
 constexpr int LINE_LDS_CAP = 4096;   // points per line kept in LDS (larger lines use global scratch)
 constexpr int CUBE_W = 21, CUBE_H = 21, CUBE_D = 11, CUBE_N = 21 * 21 * 11;  // laserMapping.cpp:74-82
 constexpr int GRID_MAX_CELLS = 1 << 23;
@@ -171,6 +172,8 @@ struct Ctx {
     int* h_bar_err = nullptr;        // mapped pinned host word
     aloam_lm_summary* d_lm_sum = nullptr;   // [ALOAM_MAX_ROUNDS]
     int* d_round_cnt = nullptr;             // [ALOAM_MAX_ROUNDS][2] correspondences per round
+    int* d_odom_spread = nullptr;           // [ALOAM_MAX_ROUNDS][ODOM_CNT_SLOTS][ODOM_CNT_STRIDE] search counters
+    int* d_map_spread = nullptr;            // the same for the mapping association
 
     // ---- laserMapping ----
     MapState* d_map = nullptr;

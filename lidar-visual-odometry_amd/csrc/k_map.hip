@@ -44,10 +44,10 @@ __device__ inline float4 associate_to_map(const double* par, float4 p) {   // :1
 
 // also zeroes this frame's mapping round counters and arms the stacks' VoxelGrid headers (saves three
 // launches on the host-issue-bound part of the frame)
-__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* round_cnt, unsigned* vox_bb0, unsigned* vox_bb1,
+__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* spread, unsigned* vox_bb0, unsigned* vox_bb1,
                               const double* pose_in) {
     __shared__ int valid_num;
-    if (threadIdx.x < 2 * ALOAM_MAX_ROUNDS) round_cnt[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE; i += blockDim.x) spread[i] = 0;
     if (threadIdx.x < 8) {                      // VoxHdr {bb[6], nrun, pad} of both lanes
         const unsigned v = threadIdx.x < 3 ? 0xffffffffu : 0u;
         if (threadIdx.x < 7) { vox_bb0[threadIdx.x] = v; vox_bb1[threadIdx.x] = v; }
@@ -216,8 +216,11 @@ __device__ __forceinline__ void assoc_slots(
     if (round_cnt) {
         const int tc = wave_sum_i(cnt_c), ts = wave_sum_i(cnt_s);
         if (lane_id() == 0) {
-            if (tc) atomicAdd(&round_cnt[0], tc);
-            if (ts) atomicAdd(&round_cnt[1], ts);
+            // spread over ODOM_CNT_SLOTS cache lines (folded by k_map_update): one address per counter
+            // serialises every wave's atomic
+            int* rc = round_cnt + ((blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) & (ODOM_CNT_SLOTS - 1)) * ODOM_CNT_STRIDE;
+            if (tc) atomicAdd(&rc[0], tc);
+            if (ts) atomicAdd(&rc[1], ts);
         }
     }
     if (cand_count) {
@@ -376,7 +379,15 @@ __global__ void k_map_invalidate(aloam_factor* out, int n) {
 }
 
 // transformUpdate (:148-152)
-__global__ void k_map_update(MapState* m) {
+__global__ void k_map_update(MapState* m, const int* __restrict__ spread, int rounds, int* round_cnt) {
+    if ((int)threadIdx.x < 2 * rounds) {      // fold the spread correspondence counters of the rounds
+        const int r = threadIdx.x >> 1, t = threadIdx.x & 1;
+        const int* b = spread + (size_t)r * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE + t;
+        int sum = 0;
+        for (int k = 0; k < ODOM_CNT_SLOTS; k++) sum += b[k * ODOM_CNT_STRIDE];
+        round_cnt[2 * r + t] = sum;
+    }
+    if (threadIdx.x != 0) return;
     const dquat qw{m->parameters[0], m->parameters[1], m->parameters[2], m->parameters[3]};
     const dquat qo{m->q_wodom[0], m->q_wodom[1], m->q_wodom[2], m->q_wodom[3]};
     const dquat qm = qmul(qw, qinv(qo));
@@ -699,7 +710,7 @@ void map_frame_launch(Ctx& C, int X) {
     // an input set written on another stream (stream3 hand-off, or this context's stream2 stacks): its
     // clouds, pose and stacks are complete at `ready` — wait before the first kernel that reads the pose
     if (in.stacks_pub || in.stacks) HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
-    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS, voxel_hdr(C, 0), voxel_hdr(C, 1),
+    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_map_spread, voxel_hdr(C, 0), voxel_hdr(C, 1),
                                      in.pose);
     k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
     const GridBuild gb[2] = {{&C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid},
@@ -734,7 +745,7 @@ void map_frame_launch(Ctx& C, int X) {
                     in.cstack, in.sstack, stack_n,
                     C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
                     C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
-                    C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS + 2 * it, C.profiling ? C.d_cand : nullptr, g_exp);
+                    C.d_map_spread + (size_t)it * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, C.profiling ? C.d_cand : nullptr, g_exp);
                 if (marks) prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
                 lm_run(C, C.d_factors, C.cap_factors, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize,
                        stack_n, live_hint);
@@ -744,7 +755,8 @@ void map_frame_launch(Ctx& C, int X) {
         if (C.profiling || !C.use_graphs) issue(true, hint);
         else run_graph(C, 2 + X, in.cstack, in.sstack, rounds, [&] { issue(false, hint); });
     }
-    k_map_update<<<1, 1, 0, st>>>(C.d_map);
+    k_map_update<<<1, 64, 0, st>>>(C.d_map, C.d_map_spread, std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS),
+                                   C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS);
     if (!(g_exp & 4)) {              // (profiling experiment 4: skip the map update — results invalid)
         fork_lane1(C);
         rebuild_map(C, 0, ub_c, in.cstack, stack_n + 0, C.P.mapping_line_resolution);
