@@ -171,7 +171,9 @@ struct GridJobs { GridJob j[4]; };
 __global__ void k_gm_bbox(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
     __shared__ unsigned sh[6];
+    __shared__ int shc;
     if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    if (threadIdx.x == 0) shc = 0;
     __syncthreads();
     const int n = *g.d_n;
     unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
@@ -188,9 +190,11 @@ __global__ void k_gm_bbox(GridJobs J) {
         if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
     }
     cnt = wave_sum_i(cnt);
-    if (lane_id() == 0 && cnt) atomicAdd(&g.desc->n_acc, cnt);
+    if (lane_id() == 0 && cnt) atomicAdd(&shc, cnt);
     __syncthreads();
+    // one global atomic per block and counter (same-address atomics serialise)
     if (threadIdx.x < 3) { atomicMin(&g.desc->bb[threadIdx.x], sh[threadIdx.x]); atomicMax(&g.desc->bb[3 + threadIdx.x], sh[3 + threadIdx.x]); }
+    if (threadIdx.x == 3 && shc) atomicAdd(&g.desc->n_acc, shc);
 }
 __global__ void k_gm_count(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
