@@ -117,8 +117,10 @@ __device__ inline float ori_branch2(float ori, float endOri) {   // (:225-236)
 __global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta* meta, int N_SCANS, float gmin, float gmax,
                                   int* __restrict__ sid, float* __restrict__ ori_out, int* hist, int nb, ScanMeta* meta_w) {
     __shared__ int h[MAXL];
+    __shared__ int jmin;
     const int n = meta->n_cl;
     for (int i = threadIdx.x; i < N_SCANS; i += SB) h[i] = 0;
+    if (threadIdx.x == 0) jmin = 0x7fffffff;
     __syncthreads();
     int j = blockIdx.x * SB + threadIdx.x;
     if (j < n) {
@@ -131,11 +133,14 @@ __global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta*
             Oris o = start_end_ori(cl, n);
             bool passed;
             ori_branch1(ori, o.start, &passed);
-            if (passed) atomicMin(&meta_w->jstar, j);
+            if (passed) atomicMin(&jmin, j);
             atomicAdd(&h[s], 1);
         }
     }
     __syncthreads();
+    // one global atomic per block (about half the points pass: a per-point atomicMin on one address
+    // serialised the kernel)
+    if (threadIdx.x == 0 && jmin != 0x7fffffff) atomicMin(&meta_w->jstar, jmin);
     if (blockIdx.x < nb)
         for (int i = threadIdx.x; i < N_SCANS; i += SB) hist[i * nb + blockIdx.x] = h[i];
 }
