@@ -340,7 +340,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     } else {
         r.optimized = 1;
         r.rounds = rounds;
-        HIPCHK(hipMemsetAsync(C.d_odom_spread, 0, sizeof(int) * ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, st));
+        // (search counters: zero from allocation / re-zeroed by the previous scan's k_odom_compose)
         const int nslots = C.n_sharp + C.n_flat;
         if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
         set_counts2(C, C.d_odom_nq, C.n_sharp, C.n_flat);

@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(256) k_odom_search(
 
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582); threads 0..2R-1 first fold the
 // spread correspondence counters of the R rounds into round_cnt
-__global__ void k_odom_compose(OdomState* o, const int* __restrict__ spread, int rounds, int* round_cnt) {
+__global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int rounds, int* round_cnt) {
     if ((int)threadIdx.x < 2 * rounds) {
         const int r = threadIdx.x >> 1, t = threadIdx.x & 1;
         const int* b = spread + (size_t)r * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE + t;
@@ -335,6 +335,8 @@ __global__ void k_odom_compose(OdomState* o, const int* __restrict__ spread, int
         for (int k = 0; k < ODOM_CNT_SLOTS; k++) sum += b[k * ODOM_CNT_STRIDE];
         round_cnt[2 * r + t] = sum;
     }
+    __syncthreads();   // then re-zero the counters for the next scan (no memset launch on the front)
+    for (int i = threadIdx.x; i < rounds * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE; i += blockDim.x) spread[i] = 0;
     if (threadIdx.x != 0) return;
     dquat qw{o->q_w[0], o->q_w[1], o->q_w[2], o->q_w[3]};
     dquat ql{o->para[0], o->para[1], o->para[2], o->para[3]};
