@@ -319,14 +319,14 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
 
 // the odometry's kd-tree rebuild (laserOdometry.cpp:640-641): 1-NN grids + scan-line-layered
 // window grids of the last clouds, one batched build, and whether the clouds are line-ordered
-static void build_last_grids(Ctx& C) {
+static void build_last_grids(Ctx& C, bool flags_preset = false) {
     const GridBuild b[4] = {
         {&C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
         {&C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr},
         {&C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
         {&C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr}};
     grid_build_multi(C, b, 4);
-    odom_last_sorted(C);
+    odom_last_sorted(C, flags_preset);
 }
 
 static void do_odometry(Ctx& C, aloam_odom_result* R) {
@@ -363,7 +363,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
                      : (C.graphs[0].exec ? 1 : 0);
             run_graph(C, slot, C.d_corner_last, C.d_surf_last, rounds, [&] { issue(false, hint); });
         }
-        odom_compose(C);
+        odom_compose(C, C.n_lsharp, C.n_lflat);
     }
     // the current less-sharp / less-flat become the last clouds (:627-641)
     std::swap(C.d_lsharp, C.d_corner_last);
@@ -371,8 +371,8 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     C.features_swapped = true;
     C.n_corner_last = C.n_lsharp;
     C.n_surf_last = C.n_lflat;
-    set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);
-    build_last_grids(C);
+    if (!r.optimized) set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);   // else set by k_odom_compose
+    build_last_grids(C, r.optimized != 0);
     const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
     r.publish_to_mapping = (C.odom_frame_count % skip == 0);
     if (r.publish_to_mapping) C.odom_frame_count = 0;

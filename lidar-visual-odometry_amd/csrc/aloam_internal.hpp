@@ -293,9 +293,9 @@ void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float ra
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);
-void odom_compose(Ctx& C);
+void odom_compose(Ctx& C, int last_corner_n, int last_surf_n);   // also sets d_last_n, d_last_sorted
 // nslots = host upper bound; d_nslots2 (optional, device int[2]) = live slots as a sum of two counts
-void odom_last_sorted(Ctx& C);
+void odom_last_sorted(Ctx& C, bool flags_preset = false);
 // runs issue() through a cached HIP graph of C.stream keyed by (k0, k1, n) in slot
 void run_graph(Ctx& C, int slot, const void* k0, const void* k1, int n, const std::function<void()>& issue);
 void lm_init(Ctx& C);   // one-time kernel attributes (before any graph capture)

@@ -327,7 +327,8 @@ __global__ void __launch_bounds__(256) k_odom_search(
 
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582); threads 0..2R-1 first fold the
 // spread correspondence counters of the R rounds into round_cnt
-__global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int rounds, int* round_cnt) {
+__global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int rounds, int* round_cnt, int* last_n, int lc, int ls,
+                               int* last_sorted) {
     if ((int)threadIdx.x < 2 * rounds) {
         const int r = threadIdx.x >> 1, t = threadIdx.x & 1;
         const int* b = spread + (size_t)r * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE + t;
@@ -338,6 +339,10 @@ __global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int round
     __syncthreads();   // then re-zero the counters for the next scan (no memset launch on the front)
     for (int i = threadIdx.x; i < rounds * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE; i += blockDim.x) spread[i] = 0;
     if (threadIdx.x != 0) return;
+    // the next scan's last-cloud counts and the line-order flags k_line_sorted clears (two k_set2 launches
+    // fewer on the front stage; the rounds above already read the previous counts)
+    last_n[0] = lc; last_n[1] = ls;
+    last_sorted[0] = 1; last_sorted[1] = 1;
     dquat qw{o->q_w[0], o->q_w[1], o->q_w[2], o->q_w[3]};
     dquat ql{o->para[0], o->para[1], o->para[2], o->para[3]};
     dvec3 r = qrot(qw, {o->para[4], o->para[5], o->para[6]});
@@ -366,14 +371,15 @@ void odom_round_search(Ctx& C, int round) {
 }
 
 // after the last clouds change: whether each is ordered by scan line (selects grid_window)
-void odom_last_sorted(Ctx& C) {
-    set_counts2(C, C.d_last_sorted, 1, 1);
+void odom_last_sorted(Ctx& C, bool flags_preset) {
+    if (!flags_preset) set_counts2(C, C.d_last_sorted, 1, 1);
     k_line_sorted<<<dim3(64, 2), 256, 0, C.stream>>>(C.d_corner_last, C.d_last_n + 0, C.d_surf_last, C.d_last_n + 1, C.d_last_sorted);
     HIPCHK(hipGetLastError());
 }
 
-void odom_compose(Ctx& C) {
-    k_odom_compose<<<1, 64, 0, C.stream>>>(C.d_odom, C.d_odom_spread, std::min(C.P.odom_rounds, ALOAM_MAX_ROUNDS), C.d_round_cnt);
+void odom_compose(Ctx& C, int lc, int ls) {
+    k_odom_compose<<<1, 64, 0, C.stream>>>(C.d_odom, C.d_odom_spread, std::min(C.P.odom_rounds, ALOAM_MAX_ROUNDS), C.d_round_cnt,
+                                           C.d_last_n, lc, ls, C.d_last_sorted);
     HIPCHK(hipGetLastError());
 }
 
