@@ -35,6 +35,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md §L2: 4 MiB per XCD, ~34.5 TB/s aggregate
 METRIC = "scans/sec + ms/iter (odom+mapping), KITTI HDL-64; ATE vs ref"
 
 
@@ -346,9 +347,11 @@ def main():
                                   if args.stages == 3 else " (front end k+1 || mapping k, 2 contexts)")
                                  if args.mode == "pipeline" else ""),
         },
+        # C3 search: ~20k queries against a ~0.1M-point map per launch; the launch is a chain of dependent
+        # gathers (latency-bound), so the HBM fraction is context, not a bound
         "roofline": {
             "kernel": "k_map_assoc (mapping 5-NN search + line/plane fit, 8 lanes per query)",
-            "bound": "hbm",
+            "bound": "latency",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -356,34 +359,40 @@ def main():
             "traffic": None,
             "avg_launch_us": round(avg_launch_ms * 1000.0, 3),
             "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
+            "note": "frac = algorithmic bytes / t against the HBM peak, for context only (latency-bound launch)",
         },
     }
 
     if rank == 0 and args.c4_launches > 0:
         c4 = c4_search(lvo, torch, dev, args.c4_launches)
         ach = c4["bytes"] / (c4["ms"] * 1e-3) / 1e9
-        # the search roofline is judged on C4; the C3 kernel is latency-bound (see roofline_c3)
+        traffic = None if args.no_traffic else c4_traffic()
+        hbm_ach = traffic / (c4["ms"] * 1e-3) / 1e9 if traffic else None
+        # the search roofline is judged on C4; the C3 kernel is latency-bound (roofline_c3).
+        # Bound from the evidence: the 33 MB map stays on die (FETCH_SIZE << algorithmic bytes, TCC hit rate
+        # 88%, profiles/), so the candidate stream is served by the L2s and the ceiling is their aggregate
+        # bandwidth; the HBM view (measured traffic / t against 8 TB/s) is reported beside it.
         result["roofline_c3"] = result["roofline"]
         result["roofline"] = {
             "kernel": "k_knn_group<5,8> (mapping 5-NN correspondence search, exact radius 1 m)",
             "config": f"C4: 128-line sweep ({c4['queries']} queries) vs {c4['map_points']}-point local map (BASELINE configs[3])",
-            "bound": "hbm",
+            "bound": "l2",
             "achieved": round(ach, 1),
-            "peak": HBM_PEAK_GBS,
+            "peak": L2_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": None if args.no_traffic else c4_traffic(),
+            "frac": round(ach / L2_PEAK_GBS, 4),
+            "traffic": traffic,
             "avg_launch_us": round(c4["ms"] * 1000.0, 2),
             "algorithmic_bytes_per_launch": round(c4["bytes"], 0),
-            "note": "algorithmic bytes = sum_q(16 + 16|C27(q)|) + 8kQ (SURVEY §8(d)); the 33 MB map stays in "
-                    "L2/Infinity Cache, so the candidate stream is served on-die and B/t can exceed HBM peak; "
-                    "traffic = rocprofv3 FETCH_SIZE per launch (KiB x1024 x2 for gfx950; Infinity-Cache hits included)",
+            "hbm": {"achieved": round(hbm_ach, 1) if hbm_ach else None, "peak": HBM_PEAK_GBS,
+                    "frac": round(hbm_ach / HBM_PEAK_GBS, 5) if hbm_ach else None,
+                    "note": "measured memory-side bytes (traffic) / t: the HBM roofline does not bind this kernel"},
+            "note": "algorithmic bytes = sum_q(16 + 16|C27(q)|) + 8kQ (SURVEY §8(d)), C27 = the map points in the 27 "
+                    "cells of edge 1.025 m around q, counted by the kernel; achieved = bytes / t (HIP events on the "
+                    "library stream); peak = aggregate L2 bandwidth (MI355X_MICROARCH.md); traffic = rocprofv3 "
+                    "FETCH_SIZE per launch (KiB x1024 x2 for gfx950; Infinity-Cache hits included)",
             "queries_per_s": round(c4["queries"] / (c4["ms"] * 1e-3), 0),
             "found5_frac": round(c4["found5"], 4),
-            # where the candidate stream is actually served from (MI355X_MICROARCH.md: L2 4 MiB per XCD,
-            # 34.5 TB/s aggregate; random rows of a 38 MB table from the Infinity Cache: 8.6 TB/s chip-wide)
-            "cache_roofline": {"level": "L2 + Infinity Cache (33 MB map)", "achieved_TBps": round(ach / 1000.0, 2),
-                               "infinity_cache_gather_TBps": 8.6, "l2_aggregate_TBps": 34.5},
         }
 
     if args.c4_reg_steps > 0:

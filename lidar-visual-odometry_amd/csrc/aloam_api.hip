@@ -318,7 +318,10 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
 }
 
 // the odometry's kd-tree rebuild (laserOdometry.cpp:640-641): 1-NN grids + scan-line-layered
-// window grids of the last clouds, one batched build, and whether the clouds are line-ordered
+// window grids of the last clouds, one batched build, and whether the clouds are line-ordered.
+// flags_preset = true ONLY right after odom_compose on the same stream: k_odom_compose sets
+// d_last_n and re-arms d_last_sorted (= 1, 1) for k_line_sorted to clear; any other caller passes
+// false (d_last_n set by the caller, the flags re-armed here).
 static void build_last_grids(Ctx& C, bool flags_preset = false) {
     const GridBuild b[4] = {
         {&C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
@@ -340,7 +343,10 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     } else {
         r.optimized = 1;
         r.rounds = rounds;
-        // (search counters: zero from allocation / re-zeroed by the previous scan's k_odom_compose)
+        // search counters: zero from allocation / re-zeroed by the previous scan's k_odom_compose; a scan
+        // that threw between its rounds and its compose left them dirty, so clear them here instead
+        if (C.odom_spread_dirty)
+            HIPCHK(hipMemsetAsync(C.d_odom_spread, 0, sizeof(int) * ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, st));
         const int nslots = C.n_sharp + C.n_flat;
         if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
         set_counts2(C, C.d_odom_nq, C.n_sharp, C.n_flat);
@@ -355,6 +361,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
                 lm_run(C, C.d_factors, cap_slots, C.d_odom->para, it, nullptr, C.d_odom_nq, live_hint);
             }
         };
+        C.odom_spread_dirty = true;
         if (C.profiling || !C.use_graphs) {
             issue(true, hint);
         } else {   // two cached graphs: the last-cloud buffers alternate between scans
@@ -363,7 +370,8 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
                      : (C.graphs[0].exec ? 1 : 0);
             run_graph(C, slot, C.d_corner_last, C.d_surf_last, rounds, [&] { issue(false, hint); });
         }
-        odom_compose(C, C.n_lsharp, C.n_lflat);
+        odom_compose(C, C.n_lsharp, C.n_lflat);   // pairs with build_last_grids(C, true) below
+        C.odom_spread_dirty = false;
     }
     // the current less-sharp / less-flat become the last clouds (:627-641)
     std::swap(C.d_lsharp, C.d_corner_last);

@@ -151,6 +151,7 @@ struct Ctx {
 
     // ---- laserOdometry ----
     bool odom_inited = false;
+    bool odom_spread_dirty = false;  // search counters written since the last k_odom_compose re-zeroed them
     int odom_frame_count = 0;
     OdomState* d_odom = nullptr;
     OdomState h_odom{};
@@ -166,8 +167,8 @@ struct Ctx {
     double* d_partials = nullptr;
     unsigned long long* d_lm_recs = nullptr;  // 2 x 64 x 32 u64: LM pass partial records + tags (double-buffered)
     unsigned long long* d_lm_seq = nullptr;   // LM launch sequence number (record tags = seq*256 + pass + 1)
-    int map_slots_hint = 0;
-    int* d_last_sorted = nullptr;    // [2]: corner_last / surf_last ordered by scan line          // last mapping frame's stack sizes (LM grid sizing only)
+    int map_slots_hint = 0;          // last mapping frame's stack sizes (LM grid sizing only)
+    int* d_last_sorted = nullptr;    // [2]: corner_last / surf_last ordered by scan line
     int* d_bar_err = nullptr;        // set if a grid barrier timed out (device view of h_bar_err)
     int* h_bar_err = nullptr;        // mapped pinned host word
     aloam_lm_summary* d_lm_sum = nullptr;   // [ALOAM_MAX_ROUNDS]

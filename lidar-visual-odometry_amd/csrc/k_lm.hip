@@ -577,8 +577,9 @@ void lm_init(Ctx& C) {
 void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round, const int* gate, const int* d_nslots2,
             int live_hint) {
     aloam_lm_summary* out = C.d_lm_sum + round;
-    // Grid size from the expected live slot count (exact for odometry; last frame's stack sizes for
-    // mapping, whose live count is only known on the device): ~1 slot per thread keeps the
+    // Grid size from the expected live slot count (the current scan's count for odometry, last frame's
+    // stack sizes for mapping, whose live count is only known on the device; a captured round graph
+    // keeps the G of the scan it was captured on, since its key has no size): ~1 slot per thread keeps the
     // evaluation short (fp64 latency-bound), capped so the per-pass grid barrier stays cheap.
     // Correctness never depends on G: the kernel splits the device-side count over the grid.
     const int est = std::max(1, std::min(nslots, live_hint > 0 ? live_hint + live_hint / 4 : nslots));

@@ -326,7 +326,9 @@ __global__ void __launch_bounds__(256) k_odom_search(
 }
 
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582); threads 0..2R-1 first fold the
-// spread correspondence counters of the R rounds into round_cnt
+// spread correspondence counters of the R rounds into round_cnt. Also writes the next scan's
+// last-cloud counts (last_n) and re-arms the line-order flags: the caller must follow it with
+// build_last_grids(C, true) (odom_last_sorted with flags_preset), which relies on both.
 __global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int rounds, int* round_cnt, int* last_n, int lc, int ls,
                                int* last_sorted) {
     if ((int)threadIdx.x < 2 * rounds) {
@@ -370,7 +372,9 @@ void odom_round_search(Ctx& C, int round) {
     HIPCHK(hipGetLastError());
 }
 
-// after the last clouds change: whether each is ordered by scan line (selects grid_window)
+// after the last clouds change: whether each is ordered by scan line (selects grid_window).
+// flags_preset: the flags were re-armed to 1 by k_odom_compose just before (odom_compose and
+// build_last_grids(C, true) always come as a pair); otherwise they are re-armed here.
 void odom_last_sorted(Ctx& C, bool flags_preset) {
     if (!flags_preset) set_counts2(C, C.d_last_sorted, 1, 1);
     k_line_sorted<<<dim3(64, 2), 256, 0, C.stream>>>(C.d_corner_last, C.d_last_n + 0, C.d_surf_last, C.d_last_n + 1, C.d_last_sorted);
