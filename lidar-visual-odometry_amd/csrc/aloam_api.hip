@@ -124,6 +124,11 @@ static void allocate(Ctx& C) {
     const int layers = std::min(MAXL, std::max(P.scan_line, 1));
     grid_alloc(C, C.g_corner_win, capLS, 2.5f * 1.025f, layers, false, true);   // window search: 2-D cells x scan line
     grid_alloc(C, C.g_surf_win, N, 2.5f * 1.025f, layers, false, true);
+    // fine grids for the first 1-NN phase: most nearest neighbours lie well inside one fine cell, whose
+    // 3x3x3 block streams a few hundred candidates instead of the coarse block's thousands
+    static const float fine = getenv("ALOAM_ODOM_FINE") ? (float)atof(getenv("ALOAM_ODOM_FINE")) : 0.85f;   // tuning knob
+    grid_alloc(C, C.g_corner_fine, capLS, fine > 0.f ? fine : 2.5f * 1.025f);
+    grid_alloc(C, C.g_surf_fine, N, fine > 0.f ? fine : 2.5f * 1.025f);
     C.cap_factors = capLS + N;
     C.d_factors = (aloam_factor*)dalloc(C, sizeof(aloam_factor) * C.cap_factors);
     C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);
@@ -323,12 +328,14 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
 // d_last_n and re-arms d_last_sorted (= 1, 1) for k_line_sorted to clear; any other caller passes
 // false (d_last_n set by the caller, the flags re-armed here).
 static void build_last_grids(Ctx& C, bool flags_preset = false) {
-    const GridBuild b[4] = {
+    const GridBuild b[6] = {
         {&C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
         {&C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr},
         {&C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
-        {&C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr}};
-    grid_build_multi(C, b, 4);
+        {&C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr},
+        {&C.g_corner_fine, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
+        {&C.g_surf_fine, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr}};
+    grid_build_multi(C, b, 6);
     odom_last_sorted(C, flags_preset);
 }
 

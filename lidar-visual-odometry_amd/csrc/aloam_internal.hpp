@@ -159,6 +159,7 @@ struct Ctx {
     int n_corner_last = 0, n_surf_last = 0;
     Grid g_corner_last, g_surf_last;
     Grid g_corner_win, g_surf_win;  // scan-line-layered grids of the last clouds (window search)
+    Grid g_corner_fine, g_surf_fine;  // fine grids of the last clouds (first 1-NN phase, k_odom.hip)
     Grid g_knn;                     // aloam_knn_device (grown on demand)
     int* d_knn_n = nullptr;
     aloam_factor* d_factors = nullptr;
@@ -288,7 +289,8 @@ struct ApiError {
 void scan_registration_launch(Ctx& C, const float4* in, int n);
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of, const unsigned char* cube_valid);
 struct GridBuild { Grid* g; const float4* pts; const int* d_n; int cap_n; const int* cube_of; const unsigned char* cube_valid; };
-void grid_build_multi(Ctx& C, const GridBuild* b, int n);   // up to 4 grids in one set of launches
+constexpr int GRID_MULTI_MAX = 6;
+void grid_build_multi(Ctx& C, const GridBuild* b, int n);   // up to GRID_MULTI_MAX grids in one set of launches
 void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2,
                        unsigned long long* cand);
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);

@@ -159,14 +159,14 @@ void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, c
 }
 
 // ------------------------------------------------------------------------------------------
-// Batched builds: up to 4 grids in the same 6 launches (blockIdx.y = grid). The bbox is reset by the
+// Batched builds: up to GRID_MULTI_MAX grids in the same 6 launches (blockIdx.y = grid). The bbox is reset by the
 // scatter of the previous build (and once at allocation), so no init launch is needed.
 struct GridJob {
     GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx; int* pcell;
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
     float min_cell; int nlayers; int w_index; int flat;
 };
-struct GridJobs { GridJob j[4]; };
+struct GridJobs { GridJob j[GRID_MULTI_MAX]; };
 
 __global__ void k_gm_bbox(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
@@ -272,7 +272,7 @@ __global__ void k_gm_scatter(GridJobs J) {
 
 void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     if (nj <= 0) return;
-    if (nj > 4) throw ApiError{ALOAM_E_ARG, "grid_build_multi: at most 4 grids"};
+    if (nj > GRID_MULTI_MAX) throw ApiError{ALOAM_E_ARG, "grid_build_multi: too many grids"};
     hipStream_t st = C.stream;
     GridJobs J{};
     int cap = 1;

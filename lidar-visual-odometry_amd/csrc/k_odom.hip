@@ -12,24 +12,62 @@
 
 namespace aloam {
 
-// Exact 1-NN within d^2 < 25 (laserOdometry.cpp:386-389) in two phases on a grid of edge g = 2.56 m:
-// the query cell's 3x3x3 block holds every point closer than g, so a best distance < 0.99 g found
-// there is final; otherwise the 5x5x5 block (>= 2g = 5.1 m around the query) is searched.
-__device__ inline int wave_nn1(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
-                               const int* __restrict__ sidx, float qx, float qy, float qz, int* out_idx, float* out_d2,
-                               RowSet<9>& r9, RowSet<25>& r25) {
-    int pos, idx;
-    float d2;
-    const float acc = 0.99f * gd.cell;
-    int f = wave_knn_rows<1, 9>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, spts, sidx, qx, qy, qz,
-                                25.0f, 1, &pos, &d2, &idx, nullptr, r9);
-    if (!(f && d2 < acc * acc))
-        f = wave_knn_rows<1, 25>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, spts, sidx, qx, qy, qz,
-                                 25.0f, 2, &pos, &d2, &idx, nullptr, r25);
-    if (!f) return 0;
-    *out_idx = idx;
-    *out_d2 = d2;
-    return 1;
+// Exact 1-NN of one query by one wave over the (2m+1)^3 cell block of a grid: every lane keeps the
+// (d^2, original index) minimum of the candidates it streams (4 points + 4 indices in flight), one
+// 64-bit wave-min merges them, and the winning lane hands out the point itself (its w = intensity,
+// i.e. the scan line), so the caller needs no reload of the closest point.
+template <int MAXR>
+__device__ __forceinline__ bool wave_nn_rows(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
+                                             const int* __restrict__ sidx, float qx, float qy, float qz, float r2, int m,
+                                             int* out_idx, float* out_d2, float4* out_pt, RowSet<MAXR>& rs) {
+    const int lane = lane_id();
+    const int total = build_rows<MAXR>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, qx, qy, qz, m, rs);
+    unsigned long long best = ~0ull;
+    float4 bp = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
+        int pp[4], id[4];
+        float4 vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = t0 + u * WAVE + lane;
+            const int pos = row_pos<MAXR>(rs, min(t, total - 1));
+            pp[u] = t < total ? pos : -1;
+            vv[u] = load_or(spts, pp[u], pp[u] >= 0, make_float4(0, 0, 0, 0));
+            id[u] = load_or(sidx, pp[u], pp[u] >= 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float d2 = sqdist(vv[u].x, vv[u].y, vv[u].z, qx, qy, qz);
+            const unsigned long long key = dist_key(d2, id[u]);
+            if (pp[u] >= 0 && d2 < r2 && key < best) { best = key; bp = vv[u]; }
+        }
+    }
+    const unsigned long long mn = wave_min_u64(best);
+    if (mn == ~0ull) return false;
+    const int w = __ffsll((long long)__ballot(best == mn)) - 1;
+    *out_idx = (int)(mn & 0xffffffffu);
+    *out_d2 = __uint_as_float((unsigned)(mn >> 32));
+    *out_pt = make_float4(readlane_f(bp.x, w), readlane_f(bp.y, w), readlane_f(bp.z, w), readlane_f(bp.w, w));
+    return true;
+}
+
+// Exact 1-NN within d^2 < 25 (laserOdometry.cpp:386-389) in up to three phases: the query cell's 3x3x3
+// block of a grid with cells of edge g holds every point closer than g, so a best distance < 0.99 g
+// found there is final. Phase 1 uses the fine grid (most neighbours lie within a fraction of a metre),
+// phase 2 the 2.56 m grid's 3x3x3 block, phase 3 its 5x5x5 block (>= 2g = 5.1 m around the query).
+struct OdomGrid { const GridDesc* d; const int* cs; const float4* sp; const int* si; };
+__device__ inline int wave_nn1(const OdomGrid& fine, const OdomGrid& coarse, float qx, float qy, float qz, int* out_idx,
+                               float* out_d2, float4* out_pt, RowSet<9>& r9, RowSet<25>& r25) {
+    const GridDesc gf = *fine.d, gc = *coarse.d;
+    if (gf.cell < gc.cell) {
+        const float acc = 0.99f * gf.cell;
+        if (wave_nn_rows<9>(gf, fine.cs, fine.sp, fine.si, qx, qy, qz, 25.0f, 1, out_idx, out_d2, out_pt, r9) && *out_d2 < acc * acc)
+            return 1;
+    }
+    const float acc = 0.99f * gc.cell;
+    if (wave_nn_rows<9>(gc, coarse.cs, coarse.sp, coarse.si, qx, qy, qz, 25.0f, 1, out_idx, out_d2, out_pt, r9) && *out_d2 < acc * acc)
+        return 1;
+    return wave_nn_rows<25>(gc, coarse.cs, coarse.sp, coarse.si, qx, qy, qz, 25.0f, 2, out_idx, out_d2, out_pt, r25) ? 1 : 0;
 }
 
 __device__ inline int line_of(float intensity) { return int(intensity); }
@@ -171,13 +209,18 @@ __device__ __forceinline__ int build_rows_layers(const GridDesc& gd, const int* 
 // the minimum in scan order is the (d^2, j) minimum going forward and the (d^2, -j) minimum going
 // backward; backward replaces forward only when strictly closer — the serial loop's result.
 template <int MODE>
-__device__ inline void grid_window(const GridDesc& gd, const int* __restrict__ start, const float4* __restrict__ spts,
-                                   const int* __restrict__ sidx, int closest, int cid, float sx, float sy, float sz,
-                                   int* ind2, int* ind3, RowSet<32>& rs) {
+__device__ inline void grid_window(const OdomGrid& wg, int closest, int cid, float sx, float sy, float sz,
+                                   int* ind2, int* ind3, float4* p2, float4* p3, RowSet<32>& rs) {
     const int lane = lane_id();
-    const int total = build_rows_layers(gd, start, sx, sy, cid - 2, cid + 2, MODE == 0 ? cid : -1000, rs);
-    // sets: 0 = fwd ind2, 1 = bwd ind2, 2 = fwd ind3, 3 = bwd ind3 (corner: ind2 sets only)
-    unsigned long long k[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    const GridDesc gd = *wg.d;
+    const int total = build_rows_layers(gd, wg.cs, sx, sy, cid - 2, cid + 2, MODE == 0 ? cid : -1000, rs);
+    // sets: 0 = fwd ind2, 1 = bwd ind2, 2 = fwd ind3, 3 = bwd ind3 (corner: ind2 sets only); each lane
+    // keeps its minimum key per set and that candidate's point
+    constexpr int NSET = MODE == 0 ? 2 : 4;
+    unsigned long long k[NSET];
+    float4 kp[NSET];
+#pragma unroll
+    for (int s = 0; s < NSET; s++) { k[s] = ~0ull; kp[s] = make_float4(0.f, 0.f, 0.f, 0.f); }
     for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
         int pp[4];
         float4 vv[4];
@@ -187,8 +230,8 @@ __device__ inline void grid_window(const GridDesc& gd, const int* __restrict__ s
             const int t = t0 + u * WAVE + lane;
             const int pos = row_pos<32>(rs, min(t, total - 1));
             pp[u] = t < total ? pos : -1;
-            vv[u] = load_or(spts, pp[u], pp[u] >= 0, make_float4(0, 0, 0, 0));
-            jj[u] = load_or(sidx, pp[u], pp[u] >= 0, 0);
+            vv[u] = load_or(wg.sp, pp[u], pp[u] >= 0, make_float4(0, 0, 0, 0));
+            jj[u] = load_or(wg.si, pp[u], pp[u] >= 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -199,29 +242,42 @@ __device__ inline void grid_window(const GridDesc& gd, const int* __restrict__ s
             const bool fwd = j > closest, bwd = j < closest;
             if (!fwd && !bwd) continue;
             const unsigned long long kf = dist_key(d, j), kb = dist_key(d, (int)(0x7fffffffu - (unsigned)j));
+            bool t[NSET];
             if (MODE == 0) {
-                if (fwd && line > cid && line <= cid + 2) k[0] = min(k[0], kf);
-                if (bwd && line < cid && line >= cid - 2) k[1] = min(k[1], kb);
+                t[0] = fwd && line > cid && line <= cid + 2 && kf < k[0];
+                t[1] = bwd && line < cid && line >= cid - 2 && kb < k[1];
             } else {
-                if (fwd && line == cid) k[0] = min(k[0], kf);
-                if (bwd && line == cid) k[1] = min(k[1], kb);
-                if (fwd && line > cid && line <= cid + 2) k[2] = min(k[2], kf);
-                if (bwd && line < cid && line >= cid - 2) k[3] = min(k[3], kb);
+                t[0] = fwd && line == cid && kf < k[0];
+                t[1] = bwd && line == cid && kb < k[1];
+                t[2] = fwd && line > cid && line <= cid + 2 && kf < k[2];
+                t[3] = bwd && line < cid && line >= cid - 2 && kb < k[3];
             }
+#pragma unroll
+            for (int s = 0; s < NSET; s++)
+                if (t[s]) { k[s] = (s & 1) ? kb : kf; kp[s] = vv[u]; }
         }
     }
     int res[2] = {-1, -1};
+    float4 rp[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
 #pragma unroll
-    for (int s = 0; s < (MODE == 0 ? 1 : 2); s++) {
+    for (int s = 0; s < NSET / 2; s++) {
         const unsigned long long f = wave_min_u64(k[2 * s]), b = wave_min_u64(k[2 * s + 1]);
         float best = 25.0f;
-        int idx = -1;
-        if (f != ~0ull) { best = __uint_as_float((unsigned)(f >> 32)); idx = (int)(f & 0xffffffffu); }
-        if (b != ~0ull && __uint_as_float((unsigned)(b >> 32)) < best) idx = (int)(0x7fffffffu - (unsigned)(b & 0xffffffffu));
+        int idx = -1, from = -1;
+        if (f != ~0ull) { best = __uint_as_float((unsigned)(f >> 32)); idx = (int)(f & 0xffffffffu); from = 0; }
+        if (b != ~0ull && __uint_as_float((unsigned)(b >> 32)) < best) { idx = (int)(0x7fffffffu - (unsigned)(b & 0xffffffffu)); from = 1; }
+        if (from >= 0) {   // the winning lane hands out its point (wave-uniform branch)
+            const unsigned long long won = from == 0 ? f : b;
+            const float4 mine = from == 0 ? kp[2 * s] : kp[2 * s + 1];
+            const int w = __ffsll((long long)__ballot((from == 0 ? k[2 * s] : k[2 * s + 1]) == won)) - 1;
+            rp[s] = make_float4(readlane_f(mine.x, w), readlane_f(mine.y, w), readlane_f(mine.z, w), readlane_f(mine.w, w));
+        }
         res[s] = idx;
     }
     *ind2 = res[0];
     *ind3 = res[1];
+    *p2 = rp[0];
+    *p3 = rp[1];
 }
 
 // 1 if the cloud's scan line (int(intensity)) never decreases with the index
@@ -233,15 +289,14 @@ __global__ void k_line_sorted(const float4* __restrict__ a, const int* na, const
         if (line_of(cl[j + 1].w) < line_of(cl[j].w)) flag[blockIdx.y] = 0;
 }
 
+// the six search grids of the last clouds: 1-NN (coarse, fine) and scan-line window, corner and surf
+struct OdomGrids { OdomGrid nn_c, nn_s, fine_c, fine_s, win_c, win_s; };
+
 __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     const float4* __restrict__ sharp, const float4* __restrict__ flat,
     const float4* __restrict__ corner_last, int n_cl, const float4* __restrict__ surf_last, int n_sl,
-    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
-    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
-    const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
-    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s,
-    RowSet<9>& r9, RowSet<25>& r25, RowSet<32>& r32, int exp) {
+    const OdomGrids& G, const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt,
+    const int* line_sorted, RowSet<9>& r9, RowSet<25>& r25, RowSet<32>& r32, int exp) {
     const int lane = lane_id();
     const bool is_corner = qi < n_sharp;
     const float4 pi = is_corner ? sharp[qi] : flat[qi - n_sharp];
@@ -259,31 +314,34 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     const int n = is_corner ? n_cl : n_sl;
     int closest = -1;
     float d2 = 0.f;
+    float4 pc = make_float4(0.f, 0.f, 0.f, 0.f);   // the closest point (cl[closest])
     int found;
-    if (exp & 1) { found = n > 0; closest = (qi * 37) % max(n, 1); }
-    else if (is_corner) found = n > 0 ? wave_nn1(*gdc, cs_c, sp_c, si_c, sx, sy, sz, &closest, &d2, r9, r25) : 0;
-    else found = n > 0 ? wave_nn1(*gds, cs_s, sp_s, si_s, sx, sy, sz, &closest, &d2, r9, r25) : 0;
+    if (exp & 1) { found = n > 0; closest = (qi * 37) % max(n, 1); pc = cl[closest]; }
+    else if (is_corner) found = n > 0 ? wave_nn1(G.fine_c, G.nn_c, sx, sy, sz, &closest, &d2, &pc, r9, r25) : 0;
+    else found = n > 0 ? wave_nn1(G.fine_s, G.nn_s, sx, sy, sz, &closest, &d2, &pc, r9, r25) : 0;
     if (exp & 2) found = 0;
     if (found) {
-        const int cid = line_of(cl[closest].w);
+        const int cid = line_of(pc.w);
         int i2, i3;
+        float4 p2, p3;
         const bool by_grid = line_sorted[is_corner ? 0 : 1] != 0;
         if (is_corner) {
-            if (by_grid) grid_window<0>(*wdc, ws_c, wp_c, wi_c, closest, cid, sx, sy, sz, &i2, &i3, r32);
-            else window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+            if (by_grid) grid_window<0>(G.win_c, closest, cid, sx, sy, sz, &i2, &i3, &p2, &p3, r32);
+            else { window_search<0>(cl, n, closest, cid, sx, sy, sz, &i2, &i3); if (i2 >= 0) p2 = cl[i2]; }
             if (i2 >= 0) {
-                const float4 a = cl[closest], b = cl[i2];
                 f.type = 0;
-                f.a[0] = a.x; f.a[1] = a.y; f.a[2] = a.z;
-                f.b[0] = b.x; f.b[1] = b.y; f.b[2] = b.z;
+                f.a[0] = pc.x; f.a[1] = pc.y; f.a[2] = pc.z;
+                f.b[0] = p2.x; f.b[1] = p2.y; f.b[2] = p2.z;
             }
         } else {
-            if (by_grid) grid_window<1>(*wds, ws_s, wp_s, wi_s, closest, cid, sx, sy, sz, &i2, &i3, r32);
-            else window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+            if (by_grid) grid_window<1>(G.win_s, closest, cid, sx, sy, sz, &i2, &i3, &p2, &p3, r32);
+            else {
+                window_search<1>(cl, n, closest, cid, sx, sy, sz, &i2, &i3);
+                if (i2 >= 0 && i3 >= 0) { p2 = cl[i2]; p3 = cl[i3]; }
+            }
             if (i2 >= 0 && i3 >= 0) {
-                const float4 pj = cl[closest], pl = cl[i2], pm = cl[i3];
                 // LidarPlaneFactor ctor (lidarFactor.hpp:64-65)
-                dvec3 jj{pj.x, pj.y, pj.z}, ll{pl.x, pl.y, pl.z}, mm{pm.x, pm.y, pm.z};
+                dvec3 jj{pc.x, pc.y, pc.z}, ll{p2.x, p2.y, p2.z}, mm{p3.x, p3.y, p3.z};
                 dvec3 nn = dcross({jj.x - ll.x, jj.y - ll.y, jj.z - ll.z}, {jj.x - mm.x, jj.y - mm.y, jj.z - mm.z});
                 double z = nn.x * nn.x + nn.y * nn.y + nn.z * nn.z;
                 if (z > 0) { double s = sqrt(z); nn = {nn.x / s, nn.y / s, nn.z / s}; }
@@ -307,12 +365,8 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
 __global__ void __launch_bounds__(256) k_odom_search(
     const float4* __restrict__ sharp, const float4* __restrict__ flat, const int* __restrict__ n_q,
     const float4* __restrict__ corner_last, const float4* __restrict__ surf_last, const int* __restrict__ n_last,
-    const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
-    const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt, const int* line_sorted,
-    const GridDesc* __restrict__ wdc, const int* __restrict__ ws_c, const float4* __restrict__ wp_c, const int* __restrict__ wi_c,
-    const GridDesc* __restrict__ wds, const int* __restrict__ ws_s, const float4* __restrict__ wp_s, const int* __restrict__ wi_s,
-    int exp) {
+    const OdomGrids G, const OdomState* __restrict__ odom, aloam_factor* __restrict__ out, int* round_cnt,
+    const int* line_sorted, int exp) {
     __shared__ RowSet<9> rows9[256 / WAVE];
     __shared__ RowSet<25> rows25[256 / WAVE];
     __shared__ RowSet<32> rows32[256 / WAVE];
@@ -320,9 +374,8 @@ __global__ void __launch_bounds__(256) k_odom_search(
     const int n_cl = n_last[0], n_sl = n_last[1];
     const int w = threadIdx.x / WAVE;
     for (int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; qi < nq; qi += gridDim.x * (blockDim.x / WAVE))
-        odom_query(qi, n_sharp, sharp, flat, corner_last, n_cl, surf_last, n_sl, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s,
-                   odom, out, round_cnt, line_sorted, wdc, ws_c, wp_c, wi_c, wds, ws_s, wp_s, wi_s, rows9[w], rows25[w], rows32[w],
-                   exp);
+        odom_query(qi, n_sharp, sharp, flat, corner_last, n_cl, surf_last, n_sl, G, odom, out, round_cnt, line_sorted,
+                   rows9[w], rows25[w], rows32[w], exp);
 }
 
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582); threads 0..2R-1 first fold the
@@ -362,13 +415,12 @@ void odom_round_search(Ctx& C, int round) {
     // counts themselves are on the device, so the launch stays graph-replayable)
     const int lines = std::max(1, std::min(MAXL, C.P.scan_line));
     const int nb = (lines * (LINE_SHARP_CAP + LINE_FLAT_CAP) * WAVE + threads - 1) / threads;
+    auto og = [](const Grid& g) { return OdomGrid{g.desc, g.cell_start, g.pts, g.idx}; };
+    const OdomGrids G{og(C.g_corner_last), og(C.g_surf_last), og(C.g_corner_fine), og(C.g_surf_fine), og(C.g_corner_win),
+                      og(C.g_surf_win)};
     k_odom_search<<<nb, threads, 0, C.stream>>>(
-        C.d_sharp, C.d_flat, C.d_odom_nq, C.d_corner_last, C.d_surf_last, C.d_last_n,
-        C.g_corner_last.desc, C.g_corner_last.cell_start, C.g_corner_last.pts, C.g_corner_last.idx,
-        C.g_surf_last.desc, C.g_surf_last.cell_start, C.g_surf_last.pts, C.g_surf_last.idx,
-        C.d_odom, C.d_factors, C.d_odom_spread + (size_t)round * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, C.d_last_sorted,
-        C.g_corner_win.desc, C.g_corner_win.cell_start, C.g_corner_win.pts, C.g_corner_win.idx,
-        C.g_surf_win.desc, C.g_surf_win.cell_start, C.g_surf_win.pts, C.g_surf_win.idx, g_odom_exp);
+        C.d_sharp, C.d_flat, C.d_odom_nq, C.d_corner_last, C.d_surf_last, C.d_last_n, G,
+        C.d_odom, C.d_factors, C.d_odom_spread + (size_t)round * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, C.d_last_sorted, g_odom_exp);
     HIPCHK(hipGetLastError());
 }
 
