@@ -350,7 +350,7 @@ def main():
         # C3 search: ~20k queries against a ~0.1M-point map per launch; the launch is a chain of dependent
         # gathers (latency-bound), so the HBM fraction is context, not a bound
         "roofline": {
-            "kernel": "k_map_assoc (mapping 5-NN search + line/plane fit, 8 lanes per query)",
+            "kernel": "k_map_assoc (mapping 5-NN search, 8 lanes per query; the fits run in k_map_fit)",
             "bound": "latency",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,

@@ -126,7 +126,7 @@ static void allocate(Ctx& C) {
     grid_alloc(C, C.g_surf_win, N, 2.5f * 1.025f, layers, false, true);
     // fine grids for the first 1-NN phase: most nearest neighbours lie well inside one fine cell, whose
     // 3x3x3 block streams a few hundred candidates instead of the coarse block's thousands
-    static const float fine = getenv("ALOAM_ODOM_FINE") ? (float)atof(getenv("ALOAM_ODOM_FINE")) : 0.85f;   // tuning knob
+    static const float fine = getenv("ALOAM_ODOM_FINE") ? (float)atof(getenv("ALOAM_ODOM_FINE")) : 1.28f;   // tuning knob (0.5-1.28 measured, 1.28 best)
     grid_alloc(C, C.g_corner_fine, capLS, fine > 0.f ? fine : 2.5f * 1.025f);
     grid_alloc(C, C.g_surf_fine, N, fine > 0.f ? fine : 2.5f * 1.025f);
     C.cap_factors = capLS + N;

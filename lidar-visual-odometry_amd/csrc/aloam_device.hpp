@@ -173,6 +173,21 @@ __host__ __device__ inline unsigned f2ord_h(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// Per-wave phase stamps for profiling builds only (-DALOAM_WSTAMP_<KERNEL>): lane 0 of each wave
+// writes wall_clock64() (100 MHz) into slot k of its wave's row; aloam_dbg_wstamps() copies the table
+// of the kernel's last launch out. In the product build WSTAMP(k) is empty.
+constexpr int WSTAMP_WAVES = 8192, WSTAMP_SLOTS = 8;
+#define WSTAMP_DEFINE_TABLE                                                                                 \
+    __device__ unsigned long long g_wstamp[WSTAMP_WAVES * WSTAMP_SLOTS];                                   \
+    extern "C" int aloam_dbg_wstamps(unsigned long long* out) {                                            \
+        return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamp), sizeof(g_wstamp));                      \
+    }
+#define WSTAMP_ON(k)                                                                                       \
+    do {                                                                                                   \
+        const unsigned w_ = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;                                \
+        if ((threadIdx.x & (WAVE - 1)) == 0 && w_ < WSTAMP_WAVES) g_wstamp[w_ * WSTAMP_SLOTS + (k)] = wall_clock64(); \
+    } while (0)
+
 // float L2^2 in the reference's order: ((dx*dx + dy*dy) + dz*dz)  (FLANN L2_Simple, laserOdometry.cpp:404-409)
 __device__ inline float sqdist(float ax, float ay, float az, float bx, float by, float bz) {
     float dx = ax - bx, dy = ay - by, dz = az - bz;
@@ -368,11 +383,11 @@ __device__ __forceinline__ int thread_knn27(const float ox, const float oy, cons
 // block. The 9 row bounds are loaded together (same addresses across the group: one coalesced
 // round trip) into a per-group LDS table tab[20] (row base - prefix, prefix); the rows are
 // flattened, lane l streams candidates l, l+GS, ... tracking its row incrementally (candidates
-// only move forward), 4 loads in flight, and keeps a sorted top-K by (d2, index); K rounds of a
+// only move forward), U loads in flight, and keeps a sorted top-K by (d2, index); K rounds of a
 // group min over 64-bit keys merge the lanes' lists. IDXW: the grid stores each point's original
 // index in w (no second load per candidate). Same total order as the wave / thread versions;
 // every lane returns the same result.
-template <int K, int GS, bool IDXW>
+template <int K, int GS, bool IDXW, int U = 4>
 __device__ __forceinline__ int group_knn27(const float ox, const float oy, const float oz, const float inv_cell,
                                            const int gdx, const int gdy, const int gdz,
                                            const int* __restrict__ start, const float4* __restrict__ spts,
@@ -409,11 +424,11 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
 #pragma unroll
     for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
     int row = 0, base = tab[0], nxt = tab[10];
-    for (int t0 = gl; t0 < total; t0 += 4 * GS) {
-        float4 v[4];
-        int id[4], ps[4];
+    for (int t0 = gl; t0 < total; t0 += U * GS) {
+        float4 v[U];
+        int id[U], ps[U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             const int t = t0 + u * GS;
             int p = -1;
             if (t < total) {
@@ -426,7 +441,7 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
             if (!IDXW) id[u] = load_or(sidx, p, p >= 0, 0x7fffffff);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
             if (!(d2 < r2) || d2 > bd[K - 1]) continue;
             const int iu = IDXW ? __float_as_int(v[u].w) : id[u];

@@ -23,6 +23,12 @@
 #include "eigen_small.hpp"
 
 namespace aloam {
+#ifdef ALOAM_WSTAMP_MAP
+WSTAMP_DEFINE_TABLE
+#define WSTAMP(k) WSTAMP_ON(k)
+#else
+#define WSTAMP(k) do { } while (0)
+#endif
 
 void prof_mark(Ctx& C, int idx);
 void segment_voxel_launch(Ctx& C, const float4* pts, const int* off, const int* seg_list, const int* nseg_p, int max_seg,
@@ -124,6 +130,7 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
             pts[j][0] = v.x; pts[j][1] = v.y; pts[j][2] = v.z;
             cx = cx + pts[j][0]; cy = cy + pts[j][1]; cz = cz + pts[j][2];
         }
+        WSTAMP(6);
         cx = cx / 5.0; cy = cy / 5.0; cz = cz / 5.0;
         double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -151,6 +158,7 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
             A[j * 3] = P[j][0]; A[j * 3 + 1] = P[j][1]; A[j * 3 + 2] = P[j][2];
             b[j] = -1;
         }
+        WSTAMP(6);
         double n[3];
         colpiv_qr_5x3(A, b, n);
         const double negOA = 1 / sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
@@ -173,22 +181,25 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
 // surround map's 1.025 m grid (group_knn27), then the group's first lane fits the line / plane
 // and writes the factor record. Correspondence counts and (profiling) candidate counts are
 // aggregated per wave before the atomics.
-constexpr int AG = 8;     // lanes per query (measured best of 4 / 8 / 16 at C3)
+constexpr int AG = 8;     // lanes per query of the scan-to-map registration (k_s2m_assoc); k_map_assoc: g_map_ag
 constexpr int ASSOC_BLOCKS = 512;   // fixed launch (graph-replayable); waves stride over the stacks
+constexpr int FIT_BLOCKS = 160;     // k_map_fit: 40960 lanes, one stack point each at C3 sizes
 // slots [s0, s1) of the compact slot space (corner stack at [0, nc), surf stack at [nc, nc + ns) — the
 // reference's AddResidualBlock order), pose `par` (laserMapping.cpp:129 parameters)
+template <int G, int U>
 __device__ __forceinline__ void assoc_slots(
     const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int nc, const int s0, const int s1, const double* par,
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp, int (*tabs)[20]) {
-    const bool lead = (lane_id() & (AG - 1)) == 0;
-    const int per_wave = WAVE / AG;
+    aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp, int (*tabs)[20],
+    int* __restrict__ nbr = nullptr) {
+    const bool lead = (lane_id() & (G - 1)) == 0;
+    const int per_wave = WAVE / G;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
     int cnt_c = 0, cnt_s = 0;
     unsigned long long ncand_sum = 0;
     for (int base = s0 + wave * per_wave; base < s1; base += nwaves * per_wave) {   // wave-uniform trip count
-        const int qi = base + (lane_id() / AG);
+        const int qi = base + (lane_id() / G);
         const bool live = qi < s1;
         const bool corner = qi < nc;
         const int li = corner ? qi : qi - nc;
@@ -196,21 +207,30 @@ __device__ __forceinline__ void assoc_slots(
         const GridDesc gd = corner ? *gdc : *gds;
         const float4 sel = associate_to_map(par, po);
         const float4* sp = corner ? sp_c : sp_s;
+        WSTAMP(2);
         int pos[5], idx[5], ncand = 0;
         float d2[5];
         int found = 5;
         if (exp & 1) { for (int k = 0; k < 5; k++) pos[k] = (li * 7 + k) % 64; }
-        else found = group_knn27<5, AG, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
-                                              corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand,
-                                              tabs[threadIdx.x / AG], gd.n);
+        else found = group_knn27<5, G, true, U>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
+                                                 corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand,
+                                                 tabs[threadIdx.x / G], gd.n);
+        WSTAMP(3);
         if (live && lead) {
-            aloam_factor f;
-            f.type = -1; f.pad = 0;
-            if (found == 5 && !(exp & 2)) fit_factor(corner, po, sp, pos, f);
-            out[qi] = f;
-            if (f.type >= 0) { if (corner) cnt_c++; else cnt_s++; }
+            if (nbr) {   // neighbours only: k_map_fit fits them one query per lane
+#pragma unroll
+                for (int k = 0; k < 5; k++) nbr[(size_t)qi * 5 + k] = (found == 5 && !(exp & 2)) ? pos[k] : -1;
+            } else {
+                aloam_factor f;
+                f.type = -1; f.pad = 0;
+                if (found == 5 && !(exp & 2)) fit_factor(corner, po, sp, pos, f);
+                WSTAMP(7);
+                out[qi] = f;
+                if (f.type >= 0) { if (corner) cnt_c++; else cnt_s++; }
+            }
             ncand_sum += ncand;
         }
+        WSTAMP(4);
     }
     // wave-aggregated counters
     if (round_cnt) {
@@ -229,20 +249,60 @@ __device__ __forceinline__ void assoc_slots(
     }
 }
 
+template <int G, int U>
 __global__ void __launch_bounds__(256) k_map_assoc(
     const float4* __restrict__ cstack, const float4* __restrict__ sstack, const int* stack_n,
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
-    const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp) {
-    __shared__ int tabs[256 / AG][20];
+    const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, int* __restrict__ nbr,
+    unsigned long long* cand_count, int exp) {
+    __shared__ int tabs[256 / G][20];
+    WSTAMP(0);
     // the solver reads nc + ns from the device
     if (!m->optimize) return;
     const int nc = stack_n[0], ns = stack_n[1];
     double par[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
-    assoc_slots(cstack, sstack, nc, 0, nc + ns, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, round_cnt, cand_count,
-                exp, tabs);
+    WSTAMP(1);
+    assoc_slots<G, U>(cstack, sstack, nc, 0, nc + ns, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, round_cnt,
+                      cand_count, exp, tabs, nbr);
+    WSTAMP(5);
+}
+
+// The fits of a mapping round, one stack point per lane (the fp64 eigen / QR fits are long serial
+// chains: run on the 8-lane groups of the search they kept 7 of 8 lanes idle): line / plane fit of
+// the 5 neighbours k_map_assoc found (:585-620, :650-686) -> factor record in slot order, and the
+// round's correspondence counts (wave-aggregated, spread over ODOM_CNT_SLOTS cache lines).
+__global__ void __launch_bounds__(256) k_map_fit(const float4* __restrict__ cstack, const float4* __restrict__ sstack,
+                                                 const int* stack_n, const float4* __restrict__ sp_c, const float4* __restrict__ sp_s,
+                                                 const MapState* __restrict__ m, const int* __restrict__ nbr,
+                                                 aloam_factor* __restrict__ out, int* round_cnt) {
+    if (!m->optimize) return;
+    const int nc = stack_n[0], nq = stack_n[0] + stack_n[1];
+    int cnt_c = 0, cnt_s = 0;
+    const int stride = gridDim.x * blockDim.x;
+    for (int i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~(WAVE - 1)); i0 < nq; i0 += stride) {   // whole waves
+        const int qi = i0 + lane_id();
+        if (qi >= nq) continue;
+        const bool corner = qi < nc;
+        int pos[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) pos[k] = nbr[(size_t)qi * 5 + k];
+        aloam_factor f;
+        f.type = -1; f.pad = 0;
+        const float4 po = corner ? cstack[qi] : sstack[qi - nc];
+        f.cp[0] = po.x; f.cp[1] = po.y; f.cp[2] = po.z;
+        if (pos[4] >= 0) fit_factor(corner, po, corner ? sp_c : sp_s, pos, f);
+        out[qi] = f;
+        if (f.type >= 0) { if (corner) cnt_c++; else cnt_s++; }
+    }
+    const int tc = wave_sum_i(cnt_c), ts = wave_sum_i(cnt_s);
+    if (lane_id() == 0) {
+        int* rc = round_cnt + ((blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) & (ODOM_CNT_SLOTS - 1)) * ODOM_CNT_STRIDE;
+        if (tc) atomicAdd(&rc[0], tc);
+        if (ts) atomicAdd(&rc[1], ts);
+    }
 }
 
 // Scan-to-map registration association (aloam_s2m_*). Each wave takes 8 NB stack points per pass:
@@ -701,6 +761,10 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
 
 // The whole laserMapping frame; results are read back by the caller (aloam_api.hip).
 static const int g_exp = getenv("ALOAM_EXP") ? atoi(getenv("ALOAM_EXP")) : 0;   // profiling experiments only
+static const int g_assoc_blocks = getenv("ALOAM_ASSOC_BLOCKS") ? atoi(getenv("ALOAM_ASSOC_BLOCKS")) : ASSOC_BLOCKS;   // tuning knob
+static const int g_fit_split = getenv("ALOAM_FIT_SPLIT") ? atoi(getenv("ALOAM_FIT_SPLIT")) : 0;   // tuning knob
+static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 16;   // tuning knob: lanes per query (8 / 16 / 32: 25.5 / 19.9 / 29.0 us at C3)
+static const int g_map_u = getenv("ALOAM_MAP_U") ? atoi(getenv("ALOAM_MAP_U")) : 4;     // tuning knob: loads in flight
 static int g_map_exp() { return g_exp; }
 void map_frame_launch(Ctx& C, int X) {
     hipStream_t st = C.stream;
@@ -741,11 +805,18 @@ void map_frame_launch(Ctx& C, int X) {
         auto issue = [&C, st, rounds, &in, stack_n](bool marks, int live_hint) {
             for (int it = 0; it < rounds; it++) {
                 if (marks) prof_mark(C, 6 + 2 * (ALOAM_MAX_ROUNDS + it));
-                k_map_assoc<<<ASSOC_BLOCKS, 256, 0, st>>>(
+                int* cnt = C.d_map_spread + (size_t)it * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE;
+                auto kern = g_map_ag == 16 ? (g_map_u == 8 ? k_map_assoc<16, 8> : k_map_assoc<16, 4>)
+                          : g_map_ag == 32 ? (g_map_u == 8 ? k_map_assoc<32, 8> : k_map_assoc<32, 4>)
+                                           : (g_map_u == 8 ? k_map_assoc<8, 8> : k_map_assoc<8, 4>);
+                kern<<<g_assoc_blocks, 256, 0, st>>>(
                     in.cstack, in.sstack, stack_n,
                     C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
-                    C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors,
-                    C.d_map_spread + (size_t)it * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, C.profiling ? C.d_cand : nullptr, g_exp);
+                    C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors, cnt,
+                    g_fit_split ? C.d_nbr : nullptr, C.profiling ? C.d_cand : nullptr, g_exp);
+                if (g_fit_split)
+                    k_map_fit<<<FIT_BLOCKS, 256, 0, st>>>(in.cstack, in.sstack, stack_n, C.g_map_corner.pts, C.g_map_surf.pts, C.d_map,
+                                                         C.d_nbr, C.d_factors, cnt);
                 if (marks) prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
                 lm_run(C, C.d_factors, C.cap_factors, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize,
                        stack_n, live_hint);

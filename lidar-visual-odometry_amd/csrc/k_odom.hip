@@ -10,7 +10,16 @@
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 
+#ifndef ODOM_U
+#define ODOM_U 4   // candidate loads in flight per lane in the 1-NN and window searches
+#endif
 namespace aloam {
+#ifdef ALOAM_WSTAMP_ODOM
+WSTAMP_DEFINE_TABLE
+#define WSTAMP(k) WSTAMP_ON(k)
+#else
+#define WSTAMP(k) do { } while (0)
+#endif
 
 // Exact 1-NN of one query by one wave over the (2m+1)^3 cell block of a grid: every lane keeps the
 // (d^2, original index) minimum of the candidates it streams (4 points + 4 indices in flight), one
@@ -24,11 +33,11 @@ __device__ __forceinline__ bool wave_nn_rows(const GridDesc& gd, const int* __re
     const int total = build_rows<MAXR>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, start, qx, qy, qz, m, rs);
     unsigned long long best = ~0ull;
     float4 bp = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
-        int pp[4], id[4];
-        float4 vv[4];
+    for (int t0 = 0; t0 < total; t0 += ODOM_U * WAVE) {
+        int pp[ODOM_U], id[ODOM_U];
+        float4 vv[ODOM_U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < ODOM_U; u++) {
             const int t = t0 + u * WAVE + lane;
             const int pos = row_pos<MAXR>(rs, min(t, total - 1));
             pp[u] = t < total ? pos : -1;
@@ -36,7 +45,7 @@ __device__ __forceinline__ bool wave_nn_rows(const GridDesc& gd, const int* __re
             id[u] = load_or(sidx, pp[u], pp[u] >= 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < ODOM_U; u++) {
             const float d2 = sqdist(vv[u].x, vv[u].y, vv[u].z, qx, qy, qz);
             const unsigned long long key = dist_key(d2, id[u]);
             if (pp[u] >= 0 && d2 < r2 && key < best) { best = key; bp = vv[u]; }
@@ -221,12 +230,12 @@ __device__ inline void grid_window(const OdomGrid& wg, int closest, int cid, flo
     float4 kp[NSET];
 #pragma unroll
     for (int s = 0; s < NSET; s++) { k[s] = ~0ull; kp[s] = make_float4(0.f, 0.f, 0.f, 0.f); }
-    for (int t0 = 0; t0 < total; t0 += 4 * WAVE) {
-        int pp[4];
-        float4 vv[4];
-        int jj[4];
+    for (int t0 = 0; t0 < total; t0 += ODOM_U * WAVE) {
+        int pp[ODOM_U];
+        float4 vv[ODOM_U];
+        int jj[ODOM_U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < ODOM_U; u++) {
             const int t = t0 + u * WAVE + lane;
             const int pos = row_pos<32>(rs, min(t, total - 1));
             pp[u] = t < total ? pos : -1;
@@ -234,7 +243,7 @@ __device__ inline void grid_window(const OdomGrid& wg, int closest, int cid, flo
             jj[u] = load_or(wg.si, pp[u], pp[u] >= 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < ODOM_U; u++) {
             if (pp[u] < 0) continue;
             const float d = sqdist(vv[u].x, vv[u].y, vv[u].z, sx, sy, sz);
             if (!(d < 25.0f)) continue;
@@ -307,6 +316,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     const float sx = (float)(r.x + 1.0 * odom->para[4]);
     const float sy = (float)(r.y + 1.0 * odom->para[5]);
     const float sz = (float)(r.z + 1.0 * odom->para[6]);
+    WSTAMP(2);
     aloam_factor f;
     f.type = -1; f.pad = 0;
     f.cp[0] = pi.x; f.cp[1] = pi.y; f.cp[2] = pi.z;
@@ -320,6 +330,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
     else if (is_corner) found = n > 0 ? wave_nn1(G.fine_c, G.nn_c, sx, sy, sz, &closest, &d2, &pc, r9, r25) : 0;
     else found = n > 0 ? wave_nn1(G.fine_s, G.nn_s, sx, sy, sz, &closest, &d2, &pc, r9, r25) : 0;
     if (exp & 2) found = 0;
+    WSTAMP(3);
     if (found) {
         const int cid = line_of(pc.w);
         int i2, i3;
@@ -351,6 +362,7 @@ __device__ __forceinline__ void odom_query(int qi, int n_sharp,
             }
         }
     }
+    WSTAMP(4);
     if (lane == 0) {
         out[qi] = f;
         // per-round counters spread over ODOM_CNT_SLOTS cache lines (summed by k_odom_compose): one
@@ -370,12 +382,15 @@ __global__ void __launch_bounds__(256) k_odom_search(
     __shared__ RowSet<9> rows9[256 / WAVE];
     __shared__ RowSet<25> rows25[256 / WAVE];
     __shared__ RowSet<32> rows32[256 / WAVE];
+    WSTAMP(0);
     const int n_sharp = n_q[0], nq = n_q[0] + n_q[1];
     const int n_cl = n_last[0], n_sl = n_last[1];
     const int w = threadIdx.x / WAVE;
+    WSTAMP(1);
     for (int qi = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE; qi < nq; qi += gridDim.x * (blockDim.x / WAVE))
         odom_query(qi, n_sharp, sharp, flat, corner_last, n_cl, surf_last, n_sl, G, odom, out, round_cnt, line_sorted,
                    rows9[w], rows25[w], rows32[w], exp);
+    WSTAMP(5);
 }
 
 // t_w += q_w * t_lc ; q_w = q_w * q_lc   (laserOdometry.cpp:581-582); threads 0..2R-1 first fold the

@@ -8,7 +8,7 @@ mkdir -p $R/gpurun_out
 for spec in "$@"; do
   name=${spec%%:*}; envs=${spec#*:}
   cd /tmp && export TMPDIR=/tmp
-  env $envs timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/kexp_$name -o run --output-format csv -- python3 $R/bench.py --mode serial --steps 20 --no-cpu --c4-launches 0 --c4-reg-steps 0 --no-traffic > $R/gpurun_out/kexp_$name.log 2>&1
+  env $envs timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/kexp_$name -o run --output-format csv -- python3 $R/bench.py --mode ${KEXP_MODE:-serial} --steps 20 --no-cpu --c4-launches 0 --c4-reg-steps 0 --no-traffic > $R/gpurun_out/kexp_$name.log 2>&1
   cd $R
   python3 - $name >> gpurun_out/kexp_summary.txt <<'PY'
 import csv, sys
