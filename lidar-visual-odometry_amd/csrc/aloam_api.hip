@@ -225,6 +225,9 @@ static void allocate(Ctx& C) {
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_fwd, hipEventDisableTiming));
+    HIPCHK(hipHostMalloc((void**)&C.h_meta_pin, sizeof(ScanMeta), hipHostMallocDefault));
+    std::memset(C.h_meta_pin, 0, sizeof(ScanMeta));
     for (auto& e : C.ev_mdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
     C.ev_ready = true;
@@ -280,14 +283,25 @@ static float ev_ms(Ctx& C, int a, int b) {
     return ms;
 }
 
-static void read_meta(Ctx& C) {
-    HIPCHK(hipMemcpyAsync(&C.h_meta, C.d_meta, sizeof(ScanMeta), hipMemcpyDeviceToHost, C.stream));
-    sync(C);
+// scanRegistration's counts reach the host without a sync of their own: the copy is queued behind the
+// registration kernels and read at the next sync of the stream (ensure_meta, or the odometry's result sync)
+static void queue_meta(Ctx& C) {
+    HIPCHK(hipMemcpyAsync(C.h_meta_pin, C.d_meta, sizeof(ScanMeta), hipMemcpyDeviceToHost, C.stream));
+    C.meta_pending = true;
+}
+static void apply_meta(Ctx& C) {   // the stream has been synchronised since queue_meta
+    C.h_meta = *C.h_meta_pin;
     C.n_full = C.h_meta.counts[0];
     C.n_sharp = C.h_meta.counts[1];
     C.n_lsharp = C.h_meta.counts[2];
     C.n_flat = C.h_meta.counts[3];
     C.n_lflat = C.h_meta.counts[4];
+    C.meta_pending = false;
+}
+static void ensure_meta(Ctx& C) {
+    if (!C.meta_pending) return;
+    sync(C);
+    apply_meta(C);
 }
 
 // sensor_msgs/PointCloud2 blob -> float4 (x, y, z, 0): x, y, z float32 at byte offsets 0, 4, 8 of each
@@ -315,8 +329,11 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     prof_mark(C, 0);
     scan_registration_launch(C, in, n);
     prof_mark(C, 1);
-    read_meta(C);
-    if (C.profiling) C.timing.scan_registration_ms = ev_ms(C, 0, 1);
+    queue_meta(C);
+    if (C.profiling) {
+        ensure_meta(C);
+        C.timing.scan_registration_ms = ev_ms(C, 0, 1);
+    }
     C.have_features = true;
     C.features_from_host = false;
     C.features_swapped = false;
@@ -327,14 +344,17 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
 // flags_preset = true ONLY right after odom_compose on the same stream: k_odom_compose sets
 // d_last_n and re-arms d_last_sorted (= 1, 1) for k_line_sorted to clear; any other caller passes
 // false (d_last_n set by the caller, the flags re-armed here).
-static void build_last_grids(Ctx& C, bool flags_preset = false) {
+// cap_c / cap_s: launch-size bounds of the two clouds (the counts themselves are read on the device;
+// -1 = the host counts)
+static void build_last_grids(Ctx& C, bool flags_preset = false, int cap_c = -1, int cap_s = -1) {
+    const int nc = std::max(cap_c >= 0 ? cap_c : C.n_corner_last, 1), ns = std::max(cap_s >= 0 ? cap_s : C.n_surf_last, 1);
     const GridBuild b[6] = {
-        {&C.g_corner_last, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
-        {&C.g_surf_last, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr},
-        {&C.g_corner_win, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
-        {&C.g_surf_win, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr},
-        {&C.g_corner_fine, C.d_corner_last, C.d_last_n + 0, std::max(C.n_corner_last, 1), nullptr, nullptr},
-        {&C.g_surf_fine, C.d_surf_last, C.d_last_n + 1, std::max(C.n_surf_last, 1), nullptr, nullptr}};
+        {&C.g_corner_last, C.d_corner_last, C.d_last_n + 0, nc, nullptr, nullptr},
+        {&C.g_surf_last, C.d_surf_last, C.d_last_n + 1, ns, nullptr, nullptr},
+        {&C.g_corner_win, C.d_corner_last, C.d_last_n + 0, nc, nullptr, nullptr},
+        {&C.g_surf_win, C.d_surf_last, C.d_last_n + 1, ns, nullptr, nullptr},
+        {&C.g_corner_fine, C.d_corner_last, C.d_last_n + 0, nc, nullptr, nullptr},
+        {&C.g_surf_fine, C.d_surf_last, C.d_last_n + 1, ns, nullptr, nullptr}};
     grid_build_multi(C, b, 6);
     odom_last_sorted(C, flags_preset);
 }
@@ -345,8 +365,14 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     hipStream_t st = C.stream;
     prof_mark(C, 2);
     const int rounds = std::min(C.P.odom_rounds, ALOAM_MAX_ROUNDS);
+    // With scanRegistration's counts still in flight (meta_pending, aloam_process_scan) nothing below
+    // waits for them: the rounds, the compose and the grid builds read every count on the device (the
+    // host's stale counts only size grid-stride launches), and the one sync of the scan comes after the
+    // grid builds, where the counts and the odometry results arrive together.
+    const bool pend = C.meta_pending;
     if (!C.odom_inited) {
         C.odom_inited = true;       // laserOdometry.cpp:355-358
+        ensure_meta(C);             // first scan: the last-cloud counts are set from the host below
     } else {
         r.optimized = 1;
         r.rounds = rounds;
@@ -354,12 +380,17 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         // that threw between its rounds and its compose left them dirty, so clear them here instead
         if (C.odom_spread_dirty)
             HIPCHK(hipMemsetAsync(C.d_odom_spread, 0, sizeof(int) * ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE, st));
-        const int nslots = C.n_sharp + C.n_flat;
-        if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
-        set_counts2(C, C.d_odom_nq, C.n_sharp, C.n_flat);
+        int hint;
+        if (pend) {                 // d_odom_nq written by k_concat; slot counts bounded by the per-line caps
+            hint = C.last_nslots > 0 ? C.last_nslots : MAXL * (LINE_SHARP_CAP + LINE_FLAT_CAP) / 4;
+        } else {                    // features from the host / another context
+            const int nslots = C.n_sharp + C.n_flat;
+            if (nslots > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity"};
+            set_counts2(C, C.d_odom_nq, C.n_sharp, C.n_flat);
+            hint = nslots;
+        }
         // the rounds read every size from the device, so the same launches serve every scan
         const int cap_slots = MAXL * (LINE_SHARP_CAP + LINE_FLAT_CAP);
-        const int hint = nslots;
         auto issue = [&C, rounds, cap_slots](bool marks, int live_hint) {
             for (int it = 0; it < rounds; it++) {
                 if (marks) prof_mark(C, 6 + 2 * it);
@@ -377,22 +408,43 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
                      : (C.graphs[0].exec ? 1 : 0);
             run_graph(C, slot, C.d_corner_last, C.d_surf_last, rounds, [&] { issue(false, hint); });
         }
-        odom_compose(C, C.n_lsharp, C.n_lflat);   // pairs with build_last_grids(C, true) below
+        // pairs with build_last_grids(C, true) below; the new last-cloud counts from the device meta
+        odom_compose(C, C.n_lsharp, C.n_lflat, pend ? C.d_meta->counts : nullptr);
         C.odom_spread_dirty = false;
     }
     // the current less-sharp / less-flat become the last clouds (:627-641)
     std::swap(C.d_lsharp, C.d_corner_last);
     std::swap(C.d_lflat, C.d_surf_last);
     C.features_swapped = true;
-    C.n_corner_last = C.n_lsharp;
+    C.n_corner_last = C.n_lsharp;   // (stale while pend: fixed after the sync below)
     C.n_surf_last = C.n_lflat;
     if (!r.optimized) set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);   // else set by k_odom_compose
     build_last_grids(C, r.optimized != 0);
+    prof_mark(C, 3);
+    // results: odom state, round counts and LM summaries in one copy into the pinned mirror (+ the
+    // scan's counts, queued behind scanRegistration): the scan's one sync
+    HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, offsetof(DevOut, map_n), hipMemcpyDeviceToHost, st));
+    sync(C);
+    if (pend) {
+        apply_meta(C);
+        C.n_corner_last = C.n_lsharp;
+        C.n_surf_last = C.n_lflat;
+    }
+    C.last_nslots = C.n_sharp + C.n_flat;
+    C.h_odom = C.h_out->odom;
+    const int* cnt = C.h_out->round_cnt;
+    std::memcpy(r.lm, C.h_out->lm_sum, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
+    if (!r.optimized) std::memset(r.lm, 0, sizeof(r.lm));
+    for (int i = 0; i < r.rounds; i++) { r.corner_correspondence[i] = cnt[2 * i]; r.plane_correspondence[i] = cnt[2 * i + 1]; }
+    for (int k = 0; k < 4; k++) { r.q_w_curr[k] = C.h_odom.q_w[k]; r.q_last_curr[k] = C.h_odom.para[k]; }
+    for (int k = 0; k < 3; k++) { r.t_w_curr[k] = C.h_odom.t_w[k]; r.t_last_curr[k] = C.h_odom.para[4 + k]; }
     const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
     r.publish_to_mapping = (C.odom_frame_count % skip == 0);
     if (r.publish_to_mapping) C.odom_frame_count = 0;
     C.odom_frame_count++;
     if (r.publish_to_mapping) {   // /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3, pose
+        for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = r.q_w_curr[k];
+        for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = r.t_w_curr[k];
         // publish into the other input set: a hand-off taken by value (MapSnapshot) stays valid until the
         // publish after next, and a mapping frame of this context keeps reading its own set
         const int t = C.in_cur ^ 1;
@@ -412,6 +464,8 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
         k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
         HIPCHK(hipGetLastError());
+        // the call returns before this copy ends: a hand-off of this set waits on ev_fwd
+        HIPCHK(hipEventRecord(C.ev_fwd, st));
         if (C.publish_stacks) {
             // the mapping stacks (laserMapping.cpp:542-550) depend on this publish only: voxelised here on
             // the otherwise idle stream2 (overlapping this context's next scan) and handed over with the
@@ -428,22 +482,6 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         }
         use_input_set(C, t);
         C.have_map_input = true;
-    }
-    prof_mark(C, 3);
-    // results
-    // odom state, round counts and LM summaries: one copy into the pinned mirror
-    HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, offsetof(DevOut, map_n), hipMemcpyDeviceToHost, st));
-    sync(C);
-    C.h_odom = C.h_out->odom;
-    const int* cnt = C.h_out->round_cnt;
-    std::memcpy(r.lm, C.h_out->lm_sum, sizeof(aloam_lm_summary) * ALOAM_MAX_ROUNDS);
-    if (!r.optimized) std::memset(r.lm, 0, sizeof(r.lm));
-    for (int i = 0; i < r.rounds; i++) { r.corner_correspondence[i] = cnt[2 * i]; r.plane_correspondence[i] = cnt[2 * i + 1]; }
-    for (int k = 0; k < 4; k++) { r.q_w_curr[k] = C.h_odom.q_w[k]; r.q_last_curr[k] = C.h_odom.para[k]; }
-    for (int k = 0; k < 3; k++) { r.t_w_curr[k] = C.h_odom.t_w[k]; r.t_last_curr[k] = C.h_odom.para[4 + k]; }
-    if (r.publish_to_mapping) {   // (the device copy of this pose was written by k_forward_map_input)
-        for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = r.q_w_curr[k];
-        for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = r.t_w_curr[k];
     }
     if (C.profiling) {
         C.timing.odometry_ms = ev_ms(C, 2, 3);
@@ -568,6 +606,7 @@ void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
     o->stk[0] = m.cstack; o->stk[1] = m.sstack;
     o->stk_n = S.d_out->stack_n + 2 * S.in_cur;
     o->stk_ready = m.ready;
+    o->fwd_done = S.ev_fwd;
     o->n[0] = S.n_map_corner_in; o->n[1] = S.n_map_surf_in; o->n[2] = S.n_map_full_in;
     for (int k = 0; k < 4; k++) o->pose[k] = S.h_map.q_wodom[k];
     for (int k = 0; k < 3; k++) o->pose[4 + k] = S.h_map.t_wodom[k];
@@ -628,6 +667,7 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
     if (side && !C.stream3) C.stream3 = make_stream(C, true);
     hipStream_t fs = side ? C.stream3 : C.stream;
     HIPCHK(hipStreamWaitEvent(fs, m.released, 0));
+    if (s.fwd_done) HIPCHK(hipStreamWaitEvent(fs, s.fwd_done, 0));   // the source's publish copy
     m.nc = s.n[0]; m.ns = s.n[1]; m.nf = s.n[2];
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = s.pose[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = s.pose[4 + k];
@@ -752,6 +792,8 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
+    if (C->ev_fwd) (void)hipEventDestroy(C->ev_fwd);
+    if (C->h_meta_pin) (void)hipHostFree(C->h_meta_pin);
     for (auto e : C->ev_mdone) if (e) (void)hipEventDestroy(e);
     for (auto& m : C->mset) {
         if (m.ready) (void)hipEventDestroy(m.ready);
@@ -776,6 +818,7 @@ const char* aloam_last_error(const aloam_ctx* ctx) {
 int aloam_scan_registration(aloam_ctx* ctx, const float* xyzr, int n, int flags) {
     API_BEGIN(ctx)
     do_scan_registration(C, xyzr, n, flags);
+    ensure_meta(C);
     API_END
 }
 
@@ -798,6 +841,7 @@ int aloam_scan_registration_pc2(aloam_ctx* ctx, const void* data, int n, int poi
         HIPCHK(hipGetLastError());
     }
     do_scan_registration(C, (const float*)C.d_in, n, ALOAM_INPUT_DEVICE);
+    ensure_meta(C);
     API_END
 }
 

@@ -115,6 +115,7 @@ struct Ctx {
     hipStream_t stream2 = nullptr;   // mapping: the surf half of the per-kind work runs here (fork/join)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_handoff = nullptr; // device-to-device hand-offs: the source stream waits on it
+    hipEvent_t ev_fwd = nullptr;     // after the publish copy of aloam_odometry (it returns before that copy ends)
     bool profiling = false;
     aloam_timing timing{};
     std::vector<DevBuf> bufs;
@@ -141,6 +142,9 @@ struct Ctx {
     float4* d_line_lf = nullptr;   // per-line less-flat centroids at line offsets
     ScanMeta* d_meta = nullptr;
     ScanMeta h_meta{};
+    ScanMeta* h_meta_pin = nullptr;  // pinned landing slot of the async meta copy
+    bool meta_pending = false;       // scanRegistration's counts are in flight to h_meta_pin (no sync yet)
+    int last_nslots = 0;             // the previous scan's odometry factor count (LM grid hint)
     // scanRegistration outputs (the "current" features)
     float4 *d_sharp = nullptr, *d_lsharp = nullptr, *d_flat = nullptr, *d_lflat = nullptr;
     int *d_sharp_idx = nullptr, *d_lsharp_idx = nullptr, *d_flat_idx = nullptr;
@@ -296,7 +300,9 @@ void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float ra
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
 void set_counts2(Ctx& C, int* dst, int a, int b);
-void odom_compose(Ctx& C, int last_corner_n, int last_surf_n);   // also sets d_last_n, d_last_sorted
+// also sets d_last_n (from dcnt[2], dcnt[4] when dcnt = the device ScanMeta counts, else the host values)
+// and re-arms d_last_sorted
+void odom_compose(Ctx& C, int last_corner_n, int last_surf_n, const int* dcnt = nullptr);
 // nslots = host upper bound; d_nslots2 (optional, device int[2]) = live slots as a sum of two counts
 void odom_last_sorted(Ctx& C, bool flags_preset = false);
 // runs issue() through a cached HIP graph of C.stream keyed by (k0, k1, n) in slot
@@ -327,6 +333,7 @@ struct MapSnapshot {
     const float4* stk[2] = {nullptr, nullptr};
     const int* stk_n = nullptr;        // device [2]
     hipEvent_t stk_ready = nullptr;    // source stream2: stacks done
+    hipEvent_t fwd_done = nullptr;     // source stream: the publish copy into src[] done
 };
 void snapshot_mapping_input(Ctx& S, MapSnapshot* out);
 void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied);

@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(256) k_odom_search(
 // last-cloud counts (last_n) and re-arms the line-order flags: the caller must follow it with
 // build_last_grids(C, true) (odom_last_sorted with flags_preset), which relies on both.
 __global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int rounds, int* round_cnt, int* last_n, int lc, int ls,
-                               int* last_sorted) {
+                               const int* dcnt, int* last_sorted) {
     if ((int)threadIdx.x < 2 * rounds) {
         const int r = threadIdx.x >> 1, t = threadIdx.x & 1;
         const int* b = spread + (size_t)r * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE + t;
@@ -411,7 +411,7 @@ __global__ void k_odom_compose(OdomState* o, int* __restrict__ spread, int round
     if (threadIdx.x != 0) return;
     // the next scan's last-cloud counts and the line-order flags k_line_sorted clears (two k_set2 launches
     // fewer on the front stage; the rounds above already read the previous counts)
-    last_n[0] = lc; last_n[1] = ls;
+    last_n[0] = dcnt ? dcnt[2] : lc; last_n[1] = dcnt ? dcnt[4] : ls;   // scanRegistration's less-sharp / less-flat counts
     last_sorted[0] = 1; last_sorted[1] = 1;
     dquat qw{o->q_w[0], o->q_w[1], o->q_w[2], o->q_w[3]};
     dquat ql{o->para[0], o->para[1], o->para[2], o->para[3]};
@@ -448,9 +448,9 @@ void odom_last_sorted(Ctx& C, bool flags_preset) {
     HIPCHK(hipGetLastError());
 }
 
-void odom_compose(Ctx& C, int lc, int ls) {
+void odom_compose(Ctx& C, int lc, int ls, const int* dcnt) {
     k_odom_compose<<<1, 64, 0, C.stream>>>(C.d_odom, C.d_odom_spread, std::min(C.P.odom_rounds, ALOAM_MAX_ROUNDS), C.d_round_cnt,
-                                           C.d_last_n, lc, ls, C.d_last_sorted);
+                                           C.d_last_n, lc, ls, dcnt, C.d_last_sorted);
     HIPCHK(hipGetLastError());
 }
 

@@ -936,7 +936,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
 __global__ void k_concat(const float4* __restrict__ cloud, const int* line_sharp, const int* line_lsharp,
                          const int* line_flat, const int* line_cnt, const float4* line_lf, int N_SCANS, ScanMeta* meta,
                          float4* sharp, int* sharp_idx, float4* lsharp, int* lsharp_idx, float4* flat, int* flat_idx,
-                         float4* lflat) {
+                         float4* lflat, int* odom_nq) {
     const int line = blockIdx.x;
     int o[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
     for (int l = 0; l < N_SCANS; l++) {
@@ -964,14 +964,16 @@ __global__ void k_concat(const float4* __restrict__ cloud, const int* line_sharp
     if (line == 0 && threadIdx.x == 0) {
         meta->counts[0] = meta->cloud_size;
         meta->counts[1] = tot[0]; meta->counts[2] = tot[1]; meta->counts[3] = tot[2]; meta->counts[4] = tot[3];
+        odom_nq[0] = tot[0]; odom_nq[1] = tot[2];   // the odometry's query counts (sharp, flat), no host round trip
     }
 }
 
-__global__ void k_meta_init(ScanMeta* m, int n_in) {
+__global__ void k_meta_init(ScanMeta* m, int n_in, int* odom_nq) {
     m->n_in = n_in;
     m->jstar = 0x7fffffff;
     m->cloud_size = 0;
     for (int i = 0; i < 5; i++) m->counts[i] = 0;
+    odom_nq[0] = 0; odom_nq[1] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -981,7 +983,7 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
     hipStream_t st = C.stream;
     const int nb = (n + SB - 1) / SB;
     const float thres = (float)P.minimum_range;
-    k_meta_init<<<1, 1, 0, st>>>(C.d_meta, n);
+    k_meta_init<<<1, 1, 0, st>>>(C.d_meta, n, C.d_odom_nq);
     if (n > 0) {
         k_filter_count<<<nb, SB, 0, st>>>(in, n, P.input_is_dense, thres, C.d_blk);
         k_scan_small<<<1, 1024, 0, st>>>(C.d_blk, nb, &C.d_meta->n_cl);
@@ -1003,7 +1005,7 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
                                                   C.d_line_flat, C.d_line_cnt, C.d_line_lf);
         k_concat<<<N_SCANS, 256, 0, st>>>(C.d_cloud, C.d_line_sharp, C.d_line_lsharp, C.d_line_flat, C.d_line_cnt,
                                           C.d_line_lf, N_SCANS, C.d_meta, C.d_sharp, C.d_sharp_idx, C.d_lsharp,
-                                          C.d_lsharp_idx, C.d_flat, C.d_flat_idx, C.d_lflat);
+                                          C.d_lsharp_idx, C.d_flat, C.d_flat_idx, C.d_lflat, C.d_odom_nq);
     }
     HIPCHK(hipGetLastError());
 }
