@@ -59,7 +59,10 @@ struct LMState {
     double cost, initial_cost;
     double scale[6], diag[6];
     double radius, decrease_factor, x_norm, mcc, step_norm;
+    double delta[6];               // the last step in tangent space (k_lm_coop: its model cost change and
+                                   // norm are computed off the critical path, lm_post)
     int reuse_diag, iteration, done, termination, successful, nres;
+    int pending, invalid;          // lm_post owed for `delta`; the step it checked was invalid (mcc < 0)
     unsigned ticket;
 };
 

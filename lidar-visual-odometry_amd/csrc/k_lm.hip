@@ -23,7 +23,7 @@ constexpr int NACC = 29;         // 21 JtJ + 6 Jtr + cost + residual-block count
 // One factor type per instantiation: every branch is resolved at compile time, so r/J stay in
 // registers (a run-time type switch over shared r/J arrays made the compiler sink their stores into
 // dynamically indexed scratch).
-template <int TY>
+template <int TY, bool FAST = false>
 __device__ __forceinline__ int eval_factor_t(const aloam_factor& f, const dquat& q, const double* t, double r[3], double J[3][6]) {
     const dvec3 cp{f.cp[0], f.cp[1], f.cp[2]};
     dvec3 pr, lp;
@@ -41,10 +41,11 @@ __device__ __forceinline__ int eval_factor_t(const aloam_factor& f, const dquat&
         const dvec3 nu = dcross(u, v);
         const dvec3 w{a.x - b.x, a.y - b.y, a.z - b.z};
         const double n = sqrt(w.x * w.x + w.y * w.y + w.z * w.z);
-        r[0] = nu.x / n; r[1] = nu.y / n; r[2] = nu.z / n;
         // d nu = dlp x w, dlp/dtheta_k = -2 pr x e_k, dlp/dt_k = e_k:
         //   J_rot[i][k] = (2 pr_i w_k - 2 (pr.w) delta_ik) / n ,  J_t[i][k] = (e_k x w)_i / n
         const double inv = 1.0 / n;
+        if constexpr (FAST) { r[0] = nu.x * inv; r[1] = nu.y * inv; r[2] = nu.z * inv; }   // one division, not four
+        else { r[0] = nu.x / n; r[1] = nu.y / n; r[2] = nu.z / n; }
         const double pw2 = 2.0 * (pr.x * w.x + pr.y * w.y + pr.z * w.z);
         const double prv[3] = {pr.x, pr.y, pr.z}, wv[3] = {w.x, w.y, w.z};
 #pragma unroll
@@ -107,6 +108,9 @@ __device__ inline double huber_scale(double s, double* rho0) {
     return 1.0;
 }
 
+// one residual row's normal-equation terms; fused multiply-adds (one rounding per term instead of two:
+// the normal equations are a rounding-level restatement of Ceres' QR anyway, and this halves the fp64
+// issue of the accumulation, the longest part of a factor's evaluation)
 __device__ __forceinline__ void add_row(const double* J, double r, double sc, double* acc) {
     double Ji[6];
 #pragma unroll
@@ -116,16 +120,16 @@ __device__ __forceinline__ void add_row(const double* J, double r, double sc, do
 #pragma unroll
     for (int a = 0; a < 6; a++)
 #pragma unroll
-        for (int b = a; b < 6; b++) acc[k++] += Ji[a] * Ji[b];
+        for (int b = a; b < 6; b++) { acc[k] = fma(Ji[a], Ji[b], acc[k]); k++; }
 #pragma unroll
-    for (int a = 0; a < 6; a++) acc[21 + a] += Ji[a] * ri;
+    for (int a = 0; a < 6; a++) acc[21 + a] = fma(Ji[a], ri, acc[21 + a]);
 }
 
 template <int TY>
 __device__ __forceinline__ void accumulate_t(const aloam_factor& f, const dquat& q, const double* t, double* acc) {
     double r[3], J[3][6];
     constexpr int m = (TY == 1 || TY == 2) ? 1 : 3;
-    eval_factor_t<TY>(f, q, t, r, J);
+    eval_factor_t<TY, true>(f, q, t, r, J);
     double rho0, sc;
     if constexpr (m == 1) {
         sc = huber_scale(r[0] * r[0], &rho0);
@@ -388,6 +392,189 @@ __device__ __forceinline__ void lm_tail(LMState* st, const double* tot, int pass
     lm_next_step(st, out, max_iter);
 }
 
+// ---- the persistent solver's tail with a short critical path -------------------------------------
+// The tail of k_lm_coop runs on one lane while the grid waits, so only what the next pass needs is
+// computed there: the accept / reject decision, the trust radius and the next candidate. The step's
+// model cost change (mcc, its validity test) and norm, and the norm of an accepted x, are needed one
+// pass later only: lm_post computes them on another wave while the next pass's partials are exchanged.
+// A step that lm_post finds invalid (mcc < 0, StepIsInvalid) is then handled by the next tail exactly
+// as the immediate check would have (radius / decrease_factor, new step, iteration consumed); only its
+// speculative evaluation pass is wasted. Same decisions and state sequence as lm_tail up to rounding.
+__device__ __forceinline__ void chol_solve6_packed(const double* Ml, const double* rhs, double* y, bool* okp) {
+    // Ml: lower triangle packed by rows (i, j <= i) at i(i+1)/2 + j
+    double L[21], inv[6];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        double s = Ml[j * (j + 1) / 2 + j];
+#pragma unroll
+        for (int k = 0; k < j; k++) s = fma(-L[j * (j + 1) / 2 + k], L[j * (j + 1) / 2 + k], s);
+        ok = ok && (s > 0.0);
+        inv[j] = rsqrt_nr(s);
+        L[j * (j + 1) / 2 + j] = s * inv[j];
+#pragma unroll
+        for (int i = j + 1; i < 6; i++) {
+            double v = Ml[i * (i + 1) / 2 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) v = fma(-L[i * (i + 1) / 2 + k], L[j * (j + 1) / 2 + k], v);
+            L[i * (i + 1) / 2 + j] = v * inv[j];
+        }
+    }
+    double z[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double v = rhs[i];
+#pragma unroll
+        for (int k = 0; k < i; k++) v = fma(-L[i * (i + 1) / 2 + k], z[k], v);
+        z[i] = v * inv[i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        double v = z[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) v = fma(-L[k * (k + 1) / 2 + i], y[k], v);
+        y[i] = v * inv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) ok = ok && isfinite(y[i]);
+    *okp = ok;
+}
+__device__ __forceinline__ void lm_next_step_fast(LMState* st, aloam_lm_summary* out, int max_iter) {
+    double A[21], g[6], sc[6], x[7];
+#pragma unroll
+    for (int i = 0; i < 21; i++) A[i] = st->A[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) { g[i] = st->g[i]; sc[i] = st->scale[i]; }
+#pragma unroll
+    for (int i = 0; i < 7; i++) x[i] = st->x[i];
+    double radius = st->radius, decrease = st->decrease_factor;
+    int reuse = st->reuse_diag, iteration = st->iteration;
+    while (true) {
+        if (iteration >= max_iter) {
+            st->radius = radius; st->decrease_factor = decrease; st->reuse_diag = reuse; st->iteration = iteration;
+            lm_finish(st, out, 0);
+            return;
+        }
+        iteration++;
+        double M[21], gs[6];
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+            gs[a] = sc[a] * g[a];
+#pragma unroll
+            for (int b = 0; b <= a; b++) M[a * (a + 1) / 2 + b] = sc[b] * Aget(A, b, a) * sc[a];
+        }
+        if (!reuse)
+#pragma unroll
+            for (int a = 0; a < 6; a++) st->diag[a] = fmin(fmax(M[a * (a + 1) / 2 + a], 1e-6), 1e32);
+        const double inv_radius = 1.0 / radius;
+#pragma unroll
+        for (int a = 0; a < 6; a++) M[a * (a + 1) / 2 + a] += st->diag[a] * inv_radius;   // D^2 = diag / radius
+        double y[6];
+        bool ok;
+        chol_solve6_packed(M, gs, y, &ok);
+        reuse = 1;
+        if (!ok) {                         // invalid step: StepIsInvalid() == StepRejected(0)
+            radius = radius / decrease;
+            decrease *= 2.0;
+            continue;
+        }
+        double delta[6];
+#pragma unroll
+        for (int a = 0; a < 6; a++) delta[a] = -y[a] * sc[a];
+        double cand[7];
+        plus7(x, delta, cand);
+#pragma unroll
+        for (int i = 0; i < 7; i++) st->cand[i] = cand[i];
+#pragma unroll
+        for (int a = 0; a < 6; a++) st->delta[a] = delta[a];
+        st->radius = radius; st->decrease_factor = decrease; st->reuse_diag = reuse; st->iteration = iteration;
+        st->pending = 1;
+        return;
+    }
+}
+// off the critical path (another wave, during the next pass's exchange): model cost change of the last
+// step from the unscaled normal equations (mcc = -(g.d + d'Ad/2), d = the tangent step), its norm in the
+// ambient space, and the norm of x
+__device__ __forceinline__ void lm_post(LMState* st) {
+    if (!st->pending || st->done) return;
+    double d[6], x[7], c[7];
+#pragma unroll
+    for (int a = 0; a < 6; a++) d[a] = st->delta[a];
+#pragma unroll
+    for (int i = 0; i < 7; i++) { x[i] = st->x[i]; c[i] = st->cand[i]; }
+    double sg = 0, sAs = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+        sg = fma(d[a], st->g[a], sg);
+        double t = 0;
+#pragma unroll
+        for (int b = 0; b < 6; b++) t = fma(Aget(st->A, a, b), d[b], t);
+        sAs = fma(d[a], t, sAs);
+    }
+    const double mcc = -(sg + 0.5 * sAs);
+    double dx[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) dx[i] = x[i] - c[i];
+    st->mcc = mcc;
+    st->invalid = mcc < 0.0;
+    st->step_norm = norm7(dx);
+    st->x_norm = norm7(x);
+    st->pending = 0;
+}
+__device__ __forceinline__ void lm_tail_fast(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+    if (pass == 0) {
+        #pragma unroll
+        for (int i = 0; i < 7; i++) st->x[i] = xp[i];
+        st->nres = (int)tot[28];
+        st->iteration = 0; st->successful = 0; st->done = 0; st->pending = 0; st->invalid = 0;
+        st->cost = tot[27]; st->initial_cost = tot[27];
+        if (st->nres == 0) { st->cost = 0; lm_finish(st, out, 4); return; }
+        #pragma unroll
+        for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        #pragma unroll
+        for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        #pragma unroll
+        for (int a = 0; a < 6; a++) st->scale[a] = 1.0 / (1.0 + sqrt(Aget(tot, a, a)));
+        st->radius = 1e4; st->decrease_factor = 2.0; st->reuse_diag = 0;
+        if (grad_max_norm(st->x, st->g) <= 1e-10) { lm_finish(st, out, 3); return; }
+        lm_next_step_fast(st, out, max_iter);
+        return;
+    }
+    if (st->invalid) {                     // the step evaluated in this pass was invalid: not a candidate
+        st->invalid = 0;
+        st->radius = st->radius / st->decrease_factor;
+        st->decrease_factor *= 2.0;
+        st->reuse_diag = 1;
+        lm_next_step_fast(st, out, max_iter);
+        return;
+    }
+    const double new_cost = tot[27];
+    if (st->step_norm <= 1e-8 * (st->x_norm + 1e-8)) { lm_finish(st, out, 2); return; }
+    const double cost_change = st->cost - new_cost;
+    if (fabs(cost_change) <= 1e-6 * st->cost) { lm_finish(st, out, 1); return; }
+    const double rel = cost_change / st->mcc;
+    if (rel > 1e-3) {
+        #pragma unroll
+        for (int i = 0; i < 7; i++) { st->x[i] = st->cand[i]; xp[i] = st->cand[i]; }
+        #pragma unroll
+        for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        #pragma unroll
+        for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        st->cost = new_cost;
+        st->successful++;
+        const double t = 2.0 * rel - 1.0;
+        st->radius = fmin(1e16, st->radius / fmax(1.0 / 3.0, 1.0 - t * t * t));
+        st->decrease_factor = 2.0;
+        st->reuse_diag = 0;
+        if (grad_max_norm(st->x, st->g) <= 1e-10) { lm_finish(st, out, 3); return; }
+    } else {
+        st->radius = st->radius / st->decrease_factor;
+        st->decrease_factor *= 2.0;
+        st->reuse_diag = 1;
+    }
+    lm_next_step_fast(st, out, max_iter);
+}
+
 // The same tail on a register copy of the state (one LDS read/write burst instead of dependent LDS
 // round trips inside the step computation).
 __device__ __forceinline__ void lm_tail_reg(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
@@ -545,12 +732,13 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
         LM_TS(pass, 4);
         block_reduce_acc<CB>(acc, rows, part8, tot);
         LM_TS(pass, 0);
+        if (pass > 0 && threadIdx.x == WAVE) lm_post(&ls);   // wave 1, while wave 0 exchanges the partials
         if (!gather_partials(recs + (size_t)(pass & 1) * LM_COOP_MAX * LM_REC, epoch0 + pass, tot, rows, G, err)) return;
         LM_TS(pass, 1);
         reduce_rows(rows, G, part8, tot);
         LM_TS(pass, 2);
         if (threadIdx.x == 0) {
-            lm_tail(&ls, tot, pass, xl, blockIdx.x == 0 ? out : nullptr, max_iter);
+            lm_tail_fast(&ls, tot, pass, xl, blockIdx.x == 0 ? out : nullptr, max_iter);
             done = ls.done;
         }
         __syncthreads();

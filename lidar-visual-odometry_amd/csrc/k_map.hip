@@ -763,7 +763,7 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
 static const int g_exp = getenv("ALOAM_EXP") ? atoi(getenv("ALOAM_EXP")) : 0;   // profiling experiments only
 static const int g_assoc_blocks = getenv("ALOAM_ASSOC_BLOCKS") ? atoi(getenv("ALOAM_ASSOC_BLOCKS")) : ASSOC_BLOCKS;   // tuning knob
 static const int g_fit_split = getenv("ALOAM_FIT_SPLIT") ? atoi(getenv("ALOAM_FIT_SPLIT")) : 0;   // tuning knob
-static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 16;   // tuning knob: lanes per query (8 / 16 / 32: 25.5 / 19.9 / 29.0 us at C3)
+static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 8;   // tuning knob: lanes per query (C3, serial on 256 CUs: 8 / 16 / 32 = 25.5 / 19.9 / 29.0 us; pipeline on 128 CUs: 8 / 16 = 22.2 / 24.6 us)
 static const int g_map_u = getenv("ALOAM_MAP_U") ? atoi(getenv("ALOAM_MAP_U")) : 4;     // tuning knob: loads in flight
 static int g_map_exp() { return g_exp; }
 void map_frame_launch(Ctx& C, int X) {

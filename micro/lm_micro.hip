@@ -62,6 +62,8 @@ int main(int argc, char** argv) {
     }
     Ctx C;
     C.P.max_solver_iterations = 4;
+    C.n_cus = 256;
+    lm_init(C);
     hipStreamCreate(&C.stream);
     aloam_factor* df; hipMalloc(&df, sizeof(aloam_factor) * n); hipMemcpy(df, f.data(), sizeof(aloam_factor) * n, hipMemcpyHostToDevice);
     hipMalloc(&C.d_lm_sum, sizeof(aloam_lm_summary) * 32); hipMalloc(&C.d_lm, sizeof(LMState));
@@ -80,7 +82,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 3; rep++) {
         hipMemcpy(dx, x0, 56, hipMemcpyHostToDevice);
         hipEventRecord(e0, C.stream);
-        for (int k = 0; k < 20; k++) lm_run(C, df, n, dx, 0, nullptr);
+        for (int k = 0; k < 20; k++) lm_run(C, df, n, dx, 0, nullptr, nullptr, n);
         hipEventRecord(e1, C.stream);
         hipEventSynchronize(e1);
         float ms; hipEventElapsedTime(&ms, e0, e1);
