@@ -51,7 +51,7 @@ __global__ void k_forward_map_input(ForwardJob j) {
     const int n = j.ndev[c] ? min(j.n[c], *j.ndev[c]) : j.n[c];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
     if (blockIdx.x == 0 && c == 0) {
-        if (threadIdx.x < 2) j.counts[threadIdx.x] = j.n[threadIdx.x];
+        if (threadIdx.x < 2) j.counts[threadIdx.x] = j.ndev[threadIdx.x] ? min(j.n[threadIdx.x], *j.ndev[threadIdx.x]) : j.n[threadIdx.x];
         if (threadIdx.x < 2 && j.stack_counts) j.stack_counts[threadIdx.x] = min(j.n[3 + threadIdx.x], *j.ndev[3 + threadIdx.x]);
         if (threadIdx.x < 7) j.pose_dst[threadIdx.x] = j.pose_src ? j.pose_src[threadIdx.x] : j.pose[threadIdx.x];
     }
@@ -221,11 +221,11 @@ static void allocate(Ctx& C) {
     for (auto& m : C.mset) {
         HIPCHK(hipEventCreateWithFlags(&m.ready, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&m.released, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&m.fwd, hipEventDisableTiming));
     }
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&C.ev_fwd, hipEventDisableTiming));
     HIPCHK(hipHostMalloc((void**)&C.h_meta_pin, sizeof(ScanMeta), hipHostMallocDefault));
     std::memset(C.h_meta_pin, 0, sizeof(ScanMeta));
     for (auto& e : C.ev_mdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -421,6 +421,55 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     if (!r.optimized) set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);   // else set by k_odom_compose
     build_last_grids(C, r.optimized != 0);
     prof_mark(C, 3);
+    const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
+    r.publish_to_mapping = (C.odom_frame_count % skip == 0);
+    if (r.publish_to_mapping) C.odom_frame_count = 0;
+    C.odom_frame_count++;
+    // the publish (/laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3, pose) is issued
+    // ahead of the sync below, sized on the device: the copy reads the clouds' device counts, the stack
+    // VoxelGrids run on launch-size hints (the previous publish's sizes + margin) and are redone with the
+    // exact sizes after the sync in the rare case a count outgrew its hint
+    const int t = C.in_cur ^ 1;
+    Ctx::MapInSet& m = C.mset[t];
+    int hint_c = 0, hint_s = 0;
+    if (r.publish_to_mapping) {
+        // publish into the other input set: a hand-off taken by value (MapSnapshot) stays valid until the
+        // publish after next, and a mapping frame of this context keeps reading its own set
+        const int capLS = MAXL * LINE_LSHARP_CAP;
+        const int cap_c = pend ? capLS : C.n_corner_last, cap_s = pend ? C.cap_in : C.n_surf_last;
+        const int cap_f = C.features_from_host ? 0 : (pend ? C.cap_in : C.n_full);
+        m.stacks = false;
+        ForwardJob j;
+        j.src[0] = C.d_corner_last; j.src[1] = C.d_surf_last; j.src[2] = C.d_cloud;
+        j.dst[0] = m.corner; j.dst[1] = m.surf; j.dst[2] = m.full;
+        j.n[0] = cap_c; j.n[1] = cap_s; j.n[2] = cap_f;
+        j.ndev[0] = C.d_last_n + 0; j.ndev[1] = C.d_last_n + 1; j.ndev[2] = (pend && cap_f) ? C.d_meta->counts : nullptr;
+        j.counts = m.n;
+        j.pose_dst = m.pose;
+        j.pose_src = C.d_odom->q_w;                    // q_w[4], t_w[3] adjacent (OdomState)
+        const int live = std::max(std::max(C.stack_hint[0], C.stack_hint[1]), 1);   // grid-stride copy: any size is correct
+        k_forward_map_input<<<dim3(std::max(1, std::min(1024, (std::min(live, std::max(cap_s, cap_c)) + 255) / 256)), 3), 256, 0, st>>>(j);
+        HIPCHK(hipGetLastError());
+        // the call returns before this copy ends: a hand-off of this set waits on its event
+        HIPCHK(hipEventRecord(m.fwd, st));
+        m.fwd_rec = true;
+        if (C.publish_stacks) {
+            // the mapping stacks (laserMapping.cpp:542-550) depend on this publish only: voxelised here on
+            // the otherwise idle stream2 (overlapping this context's next scan) and handed over with the
+            // clouds, which takes them off the mapping stage's critical path
+            hint_c = pend ? std::min(cap_c, C.stack_hint[0] > 0 ? C.stack_hint[0] : cap_c) : cap_c;   // (exact when known)
+            hint_s = pend ? std::min(cap_s, C.stack_hint[1] > 0 ? C.stack_hint[1] : cap_s) : cap_s;
+            fork_lane1(C);
+            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, hint_c, C.P.mapping_line_resolution, m.cstack,
+                                 C.d_out->stack_n + 2 * t + 0, false);
+            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.surf, m.n + 1, hint_s, C.P.mapping_plane_resolution, m.sstack,
+                                 C.d_out->stack_n + 2 * t + 1, false);
+            HIPCHK(hipEventRecord(m.ready, C.stream2));
+            m.stacks_pub = true;
+        } else {
+            m.stacks_pub = false;
+        }
+    }
     // results: odom state, round counts and LM summaries in one copy into the pinned mirror (+ the
     // scan's counts, queued behind scanRegistration): the scan's one sync
     HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, offsetof(DevOut, map_n), hipMemcpyDeviceToHost, st));
@@ -438,48 +487,23 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     for (int i = 0; i < r.rounds; i++) { r.corner_correspondence[i] = cnt[2 * i]; r.plane_correspondence[i] = cnt[2 * i + 1]; }
     for (int k = 0; k < 4; k++) { r.q_w_curr[k] = C.h_odom.q_w[k]; r.q_last_curr[k] = C.h_odom.para[k]; }
     for (int k = 0; k < 3; k++) { r.t_w_curr[k] = C.h_odom.t_w[k]; r.t_last_curr[k] = C.h_odom.para[4 + k]; }
-    const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
-    r.publish_to_mapping = (C.odom_frame_count % skip == 0);
-    if (r.publish_to_mapping) C.odom_frame_count = 0;
-    C.odom_frame_count++;
-    if (r.publish_to_mapping) {   // /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3, pose
+    if (r.publish_to_mapping) {
         for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = r.q_w_curr[k];
         for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = r.t_w_curr[k];
-        // publish into the other input set: a hand-off taken by value (MapSnapshot) stays valid until the
-        // publish after next, and a mapping frame of this context keeps reading its own set
-        const int t = C.in_cur ^ 1;
-        Ctx::MapInSet& m = C.mset[t];
         m.nc = C.n_corner_last;
         m.ns = C.n_surf_last;
         m.nf = C.features_from_host ? 0 : C.n_full;
-        m.stacks = false;
-        // clouds, counts and the composed pose (laserOdometry.cpp:588-598) into the mapping input: one launch
-        ForwardJob j;
-        j.src[0] = C.d_corner_last; j.src[1] = C.d_surf_last; j.src[2] = C.d_cloud;
-        j.dst[0] = m.corner; j.dst[1] = m.surf; j.dst[2] = m.full;
-        j.n[0] = m.nc; j.n[1] = m.ns; j.n[2] = m.nf;
-        j.counts = m.n;
-        j.pose_dst = m.pose;
-        j.pose_src = C.d_odom->q_w;                    // q_w[4], t_w[3] adjacent (OdomState)
-        const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
-        k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 3), 256, 0, st>>>(j);
-        HIPCHK(hipGetLastError());
-        // the call returns before this copy ends: a hand-off of this set waits on ev_fwd
-        HIPCHK(hipEventRecord(C.ev_fwd, st));
-        if (C.publish_stacks) {
-            // the mapping stacks (laserMapping.cpp:542-550) depend on this publish only: voxelised here on
-            // the otherwise idle stream2 (overlapping this context's next scan) and handed over with the
-            // clouds, which takes them off the mapping stage's critical path
-            fork_lane1(C);
+        if (C.publish_stacks && (m.nc > hint_c || m.ns > hint_s)) {
+            // a count outgrew its hint: redo both stacks with the exact sizes (stream order overwrites)
             voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
                                  C.d_out->stack_n + 2 * t + 0, false);
             voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
                                  C.d_out->stack_n + 2 * t + 1, false);
             HIPCHK(hipEventRecord(m.ready, C.stream2));
-            m.stacks_pub = true;
-        } else {
-            m.stacks_pub = false;
         }
+        // next publish's hints: these sizes + 25% + 1024 (capped by the buffers)
+        C.stack_hint[0] = std::min(m.nc + m.nc / 4 + 1024, std::min(MAXL * LINE_LSHARP_CAP, C.cap_voxel));
+        C.stack_hint[1] = std::min(m.ns + m.ns / 4 + 1024, std::min(C.cap_in, C.cap_voxel));
         use_input_set(C, t);
         C.have_map_input = true;
     }
@@ -606,7 +630,7 @@ void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
     o->stk[0] = m.cstack; o->stk[1] = m.sstack;
     o->stk_n = S.d_out->stack_n + 2 * S.in_cur;
     o->stk_ready = m.ready;
-    o->fwd_done = S.ev_fwd;
+    o->fwd_done = m.fwd_rec ? m.fwd : nullptr;
     o->n[0] = S.n_map_corner_in; o->n[1] = S.n_map_surf_in; o->n[2] = S.n_map_full_in;
     for (int k = 0; k < 4; k++) o->pose[k] = S.h_map.q_wodom[k];
     for (int k = 0; k < 3; k++) o->pose[4 + k] = S.h_map.t_wodom[k];
@@ -792,12 +816,12 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
-    if (C->ev_fwd) (void)hipEventDestroy(C->ev_fwd);
     if (C->h_meta_pin) (void)hipHostFree(C->h_meta_pin);
     for (auto e : C->ev_mdone) if (e) (void)hipEventDestroy(e);
     for (auto& m : C->mset) {
         if (m.ready) (void)hipEventDestroy(m.ready);
         if (m.released) (void)hipEventDestroy(m.released);
+        if (m.fwd) (void)hipEventDestroy(m.fwd);
     }
     s2m_release(*C);
     for (auto& b : C->bufs) (void)hipFree(b.p);
@@ -955,7 +979,7 @@ int aloam_set_mapping_input(aloam_ctx* ctx, const float* corner, int nc, const f
     Ctx::MapInSet& m = C.mset[ti];
     if (nc > 0) HIPCHK(hipMemcpyAsync(m.corner, corner, sizeof(float4) * nc, hipMemcpyHostToDevice, C.stream));
     if (ns > 0) HIPCHK(hipMemcpyAsync(m.surf, surf, sizeof(float4) * ns, hipMemcpyHostToDevice, C.stream));
-    m.nc = nc; m.ns = ns; m.nf = 0; m.stacks = false; m.stacks_pub = false;
+    m.nc = nc; m.ns = ns; m.nf = 0; m.stacks = false; m.stacks_pub = false; m.fwd_rec = false;
     set_counts2(C, m.n, nc, ns);
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = q[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = t[k];
@@ -1003,6 +1027,21 @@ int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out) {
         for (int i = os[c]; i < os[c + 1]; i++) { if (dst && n < out->cap) dst[n] = ps[i]; n++; }
     }
     out->n = n;
+    API_END
+}
+
+// profiling aid (not in include/aloam_hip.h): per-cube point counts of one map kind, and whether the
+// cube is in the current surrounding set; counts[CUBE_N], valid[CUBE_N]
+extern "C" int aloam_dbg_cube_counts(aloam_ctx* ctx, int which, int* counts, int* valid) {
+    API_BEGIN(ctx)
+    if (C.m_issued != C.m_done) throw ApiError{ALOAM_E_STATE, "a pipelined mapping frame is in flight"};
+    const int n = which == 0 ? C.n_mc : C.n_ms;
+    std::vector<int> cube(n);
+    if (n) HIPCHK(hipMemcpyAsync(cube.data(), which == 0 ? C.d_mc_cube : C.d_ms_cube, sizeof(int) * n, hipMemcpyDeviceToHost, C.stream));
+    sync(C);
+    for (int c = 0; c < CUBE_N; c++) { counts[c] = 0; valid[c] = 0; }
+    for (int c : cube) if (c >= 0 && c < CUBE_N) counts[c]++;
+    for (int i = 0; i < C.h_map.valid_num; i++) valid[C.h_map.valid_ind[i]] = 1;
     API_END
 }
 

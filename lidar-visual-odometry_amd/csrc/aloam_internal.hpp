@@ -118,7 +118,6 @@ struct Ctx {
     hipStream_t stream2 = nullptr;   // mapping: the surf half of the per-kind work runs here (fork/join)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_handoff = nullptr; // device-to-device hand-offs: the source stream waits on it
-    hipEvent_t ev_fwd = nullptr;     // after the publish copy of aloam_odometry (it returns before that copy ends)
     bool profiling = false;
     aloam_timing timing{};
     std::vector<DevBuf> bufs;
@@ -148,6 +147,7 @@ struct Ctx {
     ScanMeta* h_meta_pin = nullptr;  // pinned landing slot of the async meta copy
     bool meta_pending = false;       // scanRegistration's counts are in flight to h_meta_pin (no sync yet)
     int last_nslots = 0;             // the previous scan's odometry factor count (LM grid hint)
+    int stack_hint[2] = {0, 0};      // launch / sort sizes of the next publish's stack VoxelGrids (0: caps)
     // scanRegistration outputs (the "current" features)
     float4 *d_sharp = nullptr, *d_lsharp = nullptr, *d_flat = nullptr, *d_lflat = nullptr;
     int *d_sharp_idx = nullptr, *d_lsharp_idx = nullptr, *d_flat_idx = nullptr;
@@ -212,6 +212,9 @@ struct Ctx {
                                            // copied in with a hand-off); counts in DevOut::stack_n[2 set]
         hipEvent_t ready = nullptr;        // stream3: stacks of this set done
         hipEvent_t released = nullptr;     // stream: the last frame reading this set done
+        hipEvent_t fwd = nullptr;          // stream: the publish copy into this set done (aloam_odometry
+                                           // returns before it ends)
+        bool fwd_rec = false;              // `fwd` has been recorded for the set's current contents
     };
     MapInSet mset[2];
     int in_cur = 0;

@@ -47,6 +47,33 @@ __global__ void __launch_bounds__(64) k_tail_bench(const LMState* snap, long lon
     cyc[0] = sum / reps;
     cyc[1] = ls.iteration;
 }
+// pieces of the fast tail in isolation (one lane, dependent repetitions)
+template <int V>
+__global__ void __launch_bounds__(64) k_piece_bench(const LMState* snap, long long* cyc, int reps) {
+    __shared__ LMState ls;
+    if (threadIdx.x != 0) return;
+    ls = *snap;
+    double M[21], rhs[6], y[6], x[7], d[6], c[7];
+    for (int a = 0; a < 6; a++) for (int b = 0; b <= a; b++) M[a * (a + 1) / 2 + b] = ls.A[b * 6 - b * (b - 1) / 2 + (a - b)] + (a == b ? 1.0 : 0.0);
+    for (int a = 0; a < 6; a++) { rhs[a] = ls.g[a]; d[a] = 1e-3 * (a + 1); }
+    for (int i = 0; i < 7; i++) x[i] = ls.x[i];
+    bool ok = true;
+    long long sum = 0;
+    for (int r = 0; r < reps; r++) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const long long c0 = clock64();
+        if (V == 0) { chol_solve6_packed(M, rhs, y, &ok); rhs[0] += y[0] * 1e-30; }
+        if (V == 1) { plus7(x, d, c); x[0] += c[0] * 1e-30; }
+        if (V == 2) { ls.done = 0; ls.iteration = 0; lm_next_step_fast(&ls, nullptr, 4); x[0] += ls.cand[0] * 1e-30; }
+        if (V == 3) { ls.pending = 1; ls.done = 0; lm_post(&ls); x[0] += ls.mcc * 1e-30; }
+        if (V == 4) { y[0] = rsqrt_nr(x[1] + 2.0); x[1] += y[0] * 1e-30; }
+        __builtin_amdgcn_s_waitcnt(0);
+        const long long c1 = clock64();
+        sum += c1 - c0;
+    }
+    cyc[0] = sum / reps;
+    cyc[1] = (long long)(x[0] + y[0] + rhs[0]);
+}
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 20000;
     const int mode = argc > 2 ? atoi(argv[2]) : -1;
@@ -99,6 +126,16 @@ int main(int argc, char** argv) {
         printf("tail (LDS state): %lld cycles, it %lld\n", hc[0], hc[1]);
         k_tail_bench<1><<<1, 64>>>(C.d_lm, cy, 50); hipMemcpy(hc, cy, 16, hipMemcpyDeviceToHost);
         printf("tail (register state): %lld cycles, it %lld\n", hc[0], hc[1]);
+        const char* nm[] = {"chol_solve6_packed", "plus7", "lm_next_step_fast", "lm_post", "rsqrt_nr"};
+        for (int v = 0; v < 5; v++) {
+            if (v == 0) k_piece_bench<0><<<1, 64>>>(C.d_lm, cy, 50);
+            if (v == 1) k_piece_bench<1><<<1, 64>>>(C.d_lm, cy, 50);
+            if (v == 2) k_piece_bench<2><<<1, 64>>>(C.d_lm, cy, 50);
+            if (v == 3) k_piece_bench<3><<<1, 64>>>(C.d_lm, cy, 50);
+            if (v == 4) k_piece_bench<4><<<1, 64>>>(C.d_lm, cy, 50);
+            hipMemcpy(hc, cy, 16, hipMemcpyDeviceToHost);
+            printf("%-20s %lld cycles\n", nm[v], hc[0]);
+        }
     }
     aloam_lm_summary s; hipMemcpy(&s, C.d_lm_sum, sizeof(s), hipMemcpyDeviceToHost);
     printf("iters %d succ %d term %d cost %g -> %g\n", s.iterations, s.successful_steps, s.termination, s.initial_cost, s.final_cost);
