@@ -168,6 +168,7 @@ static void allocate(Ctx& C) {
     C.d_map_n = C.d_out->map_n;
     C.d_cube_cnt = (int*)dalloc(C, sizeof(int) * 2 * 7 * (CUBE_N + 1));
     C.d_cube_valid = (unsigned char*)dalloc(C, CUBE_N);
+    rebuild_init(C);                                              // map rebuild's run tables: reset
     grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f, 1, true);     // 5-NN within 1 m, 3x3x3 cells
     grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f, 1, true);
     for (auto& m : C.mset) {

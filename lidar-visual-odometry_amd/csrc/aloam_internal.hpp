@@ -305,6 +305,7 @@ void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float ra
                        unsigned long long* cand);
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
+void rebuild_init(Ctx& C);
 void set_counts2(Ctx& C, int* dst, int a, int b);
 // also sets d_last_n (from dcnt[2], dcnt[4] when dcnt = the device ScanMeta counts, else the host values)
 // and re-arms d_last_sorted

@@ -549,17 +549,6 @@ __global__ void k_cube_scatter(const float4* __restrict__ old_pts, const int* __
         Bcube[pos] = (int)c;
     }
 }
-__global__ void k_cube_final(const float4* __restrict__ B, const int* __restrict__ Bcube, const float4* __restrict__ Cf,
-                             const unsigned char* __restrict__ valid, CubeArrays a, float4* __restrict__ A, int* __restrict__ Acube) {
-    const int total = a.off[CUBE_N];
-    for (int p = blockIdx.x * MB + threadIdx.x; p < total; p += gridDim.x * MB) {
-        const int c = Bcube[p];
-        const int local = p - a.off[c];
-        if (!valid[c]) { A[a.final_off[c] + local] = B[p]; Acube[a.final_off[c] + local] = c; }
-        else if (local < a.seg_nout[c]) { A[a.final_off[c] + local] = Cf[p]; Acube[a.final_off[c] + local] = c; }
-    }
-}
-
 __global__ void k_map_register(const float4* __restrict__ full, int n, const MapState* __restrict__ m, float4* __restrict__ out) {
     const int i = blockIdx.x * MB + threadIdx.x;
     if (i < n) out[i] = associate_to_map(m->parameters, full[i]);
@@ -690,6 +679,186 @@ __global__ void k_cubevox_centroids(const float4* __restrict__ B, const unsigned
     if (last_of_cube) a.seg_nout[c] = local + 1;
 }
 
+// ------------------------------------------------------------------------------------------
+// Per-cube VoxelGrid of the surrounding cubes in ONE launch (replaces cubevox init / bbox / keys /
+// 39-bit radix sort / flags / scan / heads / centroids): one 1024-thread workgroup per surrounding cube
+// c, over its points in B[off[c], off[c+1]) = the cube's old points, then its appended stack points.
+// The old points are last frame's VoxelGrid output of the cube, i.e. in ascending PCL leaf order, and
+// leaf order is (k, j, i) order whatever the bbox, so they stay sorted: only the appended points are
+// sorted (by (leaf, position), chunk_rank_sort) and merged in by rank (old before new on equal leaves)
+// — the same sequence a stable sort by leaf of the whole cube gives, hence the same centroids (summed in
+// that order) as the device-wide sort. A cube whose old points are not sorted (it was outside the
+// surrounding set when they were appended) or with too many appended points takes a bitonic sort.
+constexpr int RBV_T = 1024;
+constexpr int RBV_CAP = 12288;       // cube points whose keys / order live in LDS (more: global scratch)
+constexpr int RBV_NCAP = 4096;       // appended points sorted in LDS (more: the bitonic fallback)
+constexpr size_t RBV_LDS = 256 + 2 * (size_t)RBV_NCAP * 8 + (size_t)RBV_CAP * 4 + (size_t)RBV_CAP * 2;
+struct RbvShared { unsigned bb[6]; int unsorted; int nrun; };
+
+__device__ __forceinline__ void rbv_bitonic_u64(unsigned long long* k, int n2) {   // global or LDS, whole block
+    for (int size = 2; size <= n2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {
+                const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+                const bool asc = (i & size) == 0;
+                const unsigned long long x = k[i], y = k[j];
+                if ((x > y) == asc) { k[i] = y; k[j] = x; }
+            }
+            __syncthreads();
+        }
+}
+
+__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__ B, CubeArrays a, const MapState* __restrict__ m,
+                                                      float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    RbvShared& SH = *(RbvShared*)smem;
+    unsigned long long* nk = (unsigned long long*)(smem + 256);
+    unsigned long long* nks = nk + RBV_NCAP;
+    unsigned* lkeys = (unsigned*)(nks + RBV_NCAP);
+    unsigned short* lorder = (unsigned short*)(lkeys + RBV_CAP);
+    const int r = blockIdx.x;
+    if (r >= m->valid_num) return;
+    const int c = m->valid_ind[r];
+    const int p0 = a.off[c], n = a.off[c + 1] - p0;
+    if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
+    const int n_o = old_count(a, c), n_n = n - n_o;
+    if (threadIdx.x < 6) SH.bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    if (threadIdx.x == 0) { SH.unsorted = 0; SH.nrun = 0; }
+    __syncthreads();
+    {   // bbox of the cube's points (ordered-int encoding)
+        unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+        for (int t = threadIdx.x; t < n; t += RBV_T) {
+            const float4 p = B[p0 + t];
+            const unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
+#pragma unroll
+            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+        }
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
+            if (lane_id() == 0) { atomicMin(&SH.bb[d], (unsigned)lo); atomicMax(&SH.bb[3 + d], (unsigned)hi); }
+        }
+    }
+    __syncthreads();
+    bool ovf;
+    int minb[3], mul1, mul2;
+    voxel_params(SH.bb, leaf, &ovf, minb, &mul1, &mul2);    // same bbox -> leaf grid as k_voxel.hip
+    if (ovf) {                            // PCL's int overflow: pass-through (every point its own leaf)
+        for (int t = threadIdx.x; t < n; t += RBV_T) Cf[p0 + t] = B[p0 + t];
+        if (threadIdx.x == 0) a.seg_nout[c] = n;
+        return;
+    }
+    const float inv = 1.0f / leaf;
+    const bool fits = n <= RBV_CAP;
+    unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, order, bitonic (2n)
+    unsigned* keys = fits ? lkeys : (unsigned*)gseg;
+    int* gorder = (int*)(gseg + (n + 1) / 2);
+    for (int t = threadIdx.x; t < n; t += RBV_T) keys[t] = voxel_index(B[p0 + t], inv, minb, mul1, mul2);
+    __syncthreads();
+    for (int t = threadIdx.x; t + 1 < n_o; t += RBV_T)
+        if (keys[t] > keys[t + 1]) SH.unsorted = 1;
+    __syncthreads();
+    auto put_order = [&](int pos, int idx) { if (fits) lorder[pos] = (unsigned short)idx; else gorder[pos] = idx; };
+    if (!SH.unsorted && n_n <= RBV_NCAP) {
+        // appended points: sort (leaf, position) keys, then merge by rank with the sorted old points
+        const int n2n = (n_n + WAVE - 1) / WAVE * WAVE;
+        for (int j = threadIdx.x; j < n2n; j += RBV_T)
+            nk[j] = j < n_n ? (((unsigned long long)keys[n_o + j] << 32) | (unsigned)j) : ~0ull;
+        __syncthreads();
+        if (n2n > 0) chunk_rank_sort(nk, nks, n2n);        // ends with a barrier
+        for (int t = threadIdx.x; t < n_o; t += RBV_T) {   // old point t: + appended points of smaller leaf
+            const unsigned long long k = (unsigned long long)keys[t] << 32;
+            int lo = 0, hi = n_n;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (nks[mid] < k) lo = mid + 1; else hi = mid; }
+            put_order(t + lo, t);
+        }
+        for (int j = threadIdx.x; j < n_n; j += RBV_T) {   // j-th appended point: + old points of leaf <= its leaf
+            const unsigned long long e = nks[j];
+            const unsigned lf = (unsigned)(e >> 32);
+            int lo = 0, hi = n_o;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (keys[mid] <= lf) lo = mid + 1; else hi = mid; }
+            put_order(j + lo, n_o + (int)(e & 0xffffffffu));
+        }
+    } else {
+        // bitonic sort of (leaf, position) over the cube (global scratch; rare: see above)
+        int n2 = 1;
+        while (n2 < n) n2 <<= 1;
+        unsigned long long* bk = gseg + (size_t)2 * n;      // n2 < 2n slots
+        for (int t = threadIdx.x; t < n2; t += RBV_T)
+            bk[t] = t < n ? (((unsigned long long)keys[t] << 32) | (unsigned)t) : ~0ull;
+        __syncthreads();
+        rbv_bitonic_u64(bk, n2);
+        for (int t = threadIdx.x; t < n; t += RBV_T) put_order(t, (int)(bk[t] & 0xffffffffu));
+    }
+    __syncthreads();
+    // runs of equal leaves in sorted order -> centroids in order (fp32, the sorted order of the points)
+    auto ord = [&](int pos) { return fits ? (int)lorder[pos] : gorder[pos]; };
+    for (int base = 0; base < n; base += RBV_T) {
+        const int t = base + threadIdx.x;
+        int oi = 0;
+        bool head = false;
+        if (t < n) {
+            oi = ord(t);
+            head = t == 0 || keys[ord(t - 1)] != keys[oi];
+        }
+        int tot;
+        const int run = SH.nrun + block_exscan<RBV_T>(head ? 1 : 0, &tot);
+        if (head) {
+            const unsigned lf = keys[oi];
+            float4 cc = B[p0 + oi];
+            int t2 = t + 1;
+            for (; t2 < n; t2++) {
+                const int o2 = ord(t2);
+                if (keys[o2] != lf) break;
+                const float4 q = B[p0 + o2];
+                cc.x += q.x; cc.y += q.y; cc.z += q.z; cc.w += q.w;
+            }
+            const float cnt = (float)(t2 - t);
+            Cf[p0 + run] = make_float4(cc.x / cnt, cc.y / cnt, cc.z / cnt, cc.w / cnt);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) SH.nrun += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.seg_nout[c] = SH.nrun;
+}
+
+// old and appended runs per cube in one launch; the run tables are reset by the previous rebuild's
+// final copy (k_cube_final_reset), so no reset launch
+__global__ void k_rb_count(const int* __restrict__ cube, const int* d_n, const unsigned* __restrict__ skey, int ub, CubeArrays a) {
+    const int n = *d_n;
+    const int stride = gridDim.x * MB;
+    for (int i = blockIdx.x * MB + threadIdx.x; i < max(n, ub); i += stride) {
+        if (i < n) {
+            const int c = cube[i];
+            if (c >= 0) {
+                if (i == 0 || cube[i - 1] != c) a.first_old[c] = i;
+                if (i == n - 1 || cube[i + 1] != c) a.last_old[c] = i;
+            }
+        }
+        if (i < ub) {
+            const unsigned c = skey[i];
+            if (c < (unsigned)CUBE_N) {
+                if (i == 0 || skey[i - 1] != c) a.first_new[c] = i;
+                if (i == ub - 1 || skey[i + 1] != c) a.last_new[c] = i;
+            }
+        }
+    }
+}
+__global__ void k_cube_final_reset(const float4* __restrict__ B, const int* __restrict__ Bcube, const float4* __restrict__ Cf,
+                                   const unsigned char* __restrict__ valid, CubeArrays a, float4* __restrict__ A, int* __restrict__ Acube) {
+    const int total = a.off[CUBE_N];
+    for (int p = blockIdx.x * MB + threadIdx.x; p < total; p += gridDim.x * MB) {
+        const int c = Bcube[p];
+        const int local = p - a.off[c];
+        if (!valid[c]) { A[a.final_off[c] + local] = B[p]; Acube[a.final_off[c] + local] = c; }
+        else if (local < a.seg_nout[c]) { A[a.final_off[c] + local] = Cf[p]; Acube[a.final_off[c] + local] = c; }
+    }
+    for (int c = blockIdx.x * MB + threadIdx.x; c <= CUBE_N; c += gridDim.x * MB) {   // next rebuild's run tables
+        a.last_old[c] = -1; a.last_new[c] = -1; a.first_old[c] = 0x7fffffff; a.first_new[c] = 0x7fffffff;
+    }
+}
+
 size_t cube_sort_tmp_bytes(int cap) {
     size_t bytes = 0;
     HIPCHK(rocprim::radix_sort_pairs((void*)nullptr, bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int*)nullptr, (int*)nullptr,
@@ -703,6 +872,8 @@ __global__ void k_scan_small_m(int* a, int nb, int* total) {
 
 // ------------------------------------------------------------------------------------------
 static int nblk(int n) { return std::max(1, std::min(2048, (n + MB - 1) / MB)); }
+// 0: the per-cube VoxelGrid as one device-wide radix sort + 12 launches (round-1 path, kept for A/B)
+static const int g_rebuild_fused = getenv("ALOAM_REBUILD_FUSED") ? atoi(getenv("ALOAM_REBUILD_FUSED")) : 1;
 
 static int g_map_exp();
 static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, const int* d_stack_n, float leaf) {
@@ -727,6 +898,19 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     if (ub_new > 0) {
         size_t bytes = C.sort_tmp_bytes;
         HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, k1, k2, K.ins_val, K.ins_val2, (unsigned)ub_new, 0, 13, st));
+    }
+    if (g_rebuild_fused) {
+        // counts (tables reset by the last rebuild) -> offsets -> old + appended points by cube into B ->
+        // per-cube VoxelGrid of the surrounding cubes into Cf -> final offsets -> copy (+ table reset)
+        float4* Cf = K.map_tmp;
+        k_rb_count<<<nblk(std::max(n_old_ub, ub_new)), MB, 0, st>>>(Acube, d_n_old, k2, ub_new, a);
+        k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 0, nullptr);
+        k_cube_scatter<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(A, Acube, d_n_old, K.ins_pts, k2, K.ins_val2, ub_new, a, B, Bcube);
+        k_rb_cubevox<<<125, RBV_T, RBV_LDS, st>>>(B, a, C.d_map, leaf, Cf, K.seg_keys + 32768);
+        k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 1, d_n_old);
+        k_cube_final_reset<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(B, Bcube, Cf, C.d_cube_valid, a, A, Acube);
+        HIPCHK(hipGetLastError());
+        return;
     }
     k_cube_reset<<<(CUBE_N + 1 + 255) / 256, 256, 0, st>>>(a);
     k_cube_count_old<<<nblk(n_old_ub), MB, 0, st>>>(Acube, d_n_old, a);
@@ -755,7 +939,25 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
         k_cubevox_centroids<<<nbt, MB, 0, st>>>(B, vk2, vv2, heads, &cv->nrun, ub_tot, C.d_map, cv, a, Cf);
     }
     k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 1, d_n_old);
-    k_cube_final<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(B, Bcube, Cf, C.d_cube_valid, a, A, Acube);
+    k_cube_final_reset<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(B, Bcube, Cf, C.d_cube_valid, a, A, Acube);
+    HIPCHK(hipGetLastError());
+}
+
+// one-time state of the rebuild's run tables (afterwards every rebuild leaves them reset)
+void rebuild_init(Ctx& C) {
+    static bool attr = false;
+    if (!attr) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubevox, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBV_LDS));
+        attr = true;
+    }
+    for (int which = 0; which < 2; which++) {
+        CubeArrays a;
+        int* base = C.d_cube_cnt + which * 7 * (CUBE_N + 1);
+        a.first_old = base; a.last_old = base + (CUBE_N + 1); a.first_new = base + 2 * (CUBE_N + 1);
+        a.last_new = base + 3 * (CUBE_N + 1); a.off = base + 4 * (CUBE_N + 1); a.seg_nout = base + 5 * (CUBE_N + 1);
+        a.final_off = base + 6 * (CUBE_N + 1);
+        k_cube_reset<<<(CUBE_N + 1 + 255) / 256, 256, 0, C.stream>>>(a);
+    }
     HIPCHK(hipGetLastError());
 }
 

@@ -444,51 +444,6 @@ __device__ void bitonic_sort_reg4(unsigned long long* k, int n2) {
     __syncthreads();
 }
 
-// Ascending sort of n2 (a multiple of 64) u64 keys held in LDS into out[] (LDS): every 64-key chunk is
-// bitonic-sorted inside one wave (lane exchanges only), then each real key's rank is its position in
-// its chunk plus, per other chunk, the number of that chunk's keys below it (chunk bounds first, else
-// a 6-step binary search). No block-wide compare-exchange stages: the 2048-key bitonic network's ~60
-// dependent LDS/permute stages took ~27 us per line, this ~3-5 us. Keys other than the ~0 padding must
-// be distinct. Ends with a barrier.
-__device__ void chunk_rank_sort(unsigned long long* keys, unsigned long long* out, int n2) {
-    const int lane = lane_id(), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    const int nch = n2 / WAVE;
-    for (int c = wv; c < nch; c += nw) {
-        unsigned long long v = keys[c * WAVE + lane];
-#pragma unroll
-        for (int size = 2; size <= WAVE; size <<= 1) {
-#pragma unroll
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                const unsigned long long o = __shfl_xor(v, stride, WAVE);
-                const bool asc = (lane & size) == 0, lower = (lane & stride) == 0;
-                v = (lower == asc) ? (v < o ? v : o) : (v < o ? o : v);
-            }
-        }
-        keys[c * WAVE + lane] = v;
-        out[c * WAVE + lane] = ~0ull;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < n2; e += blockDim.x) {
-        const unsigned long long x = keys[e];
-        if (x == ~0ull) continue;
-        const int c = e / WAVE;
-        int rank = e % WAVE;
-        for (int c2 = 0; c2 < nch; c2++) {
-            if (c2 == c) continue;
-            const unsigned long long* k = keys + c2 * WAVE;
-            if (k[WAVE - 1] < x) { rank += WAVE; continue; }
-            if (!(k[0] < x)) continue;
-            int lo = 0;
-#pragma unroll
-            for (int st = WAVE / 2; st >= 1; st >>= 1)
-                if (k[lo + st - 1] < x) lo += st;
-            rank += lo;
-        }
-        out[rank] = x;
-    }
-    __syncthreads();
-}
-
 #ifdef ALOAM_LF_TIMING
 __device__ unsigned long long g_lf_ts[64][8];      // micro-benchmark only: per-line phase stamps
 #define LF_TS(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts[blockIdx.x][k] = wall_clock64(); } while (0)
