@@ -477,10 +477,41 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
     }
     return found;
 }
+// v / k for a point count k in [1, 2^24), correctly rounded like the IEEE division PCL's centroid
+// (Eigen "/= num_pts") does. For |x| in [2^-89, 2^90) or x == 0, v_div_scale / v_div_fmas /
+// v_div_fixup in the compiler's fp32 division sequence are identities, leaving rcp, one Newton step on
+// the reciprocal and two residual corrections of the quotient: that sequence is evaluated here with the
+// refined reciprocal shared by the 4 components (~2.5x fewer VALU cycles; the centroid passes are
+// VALU-bound on their divisions). Zero numerators are returned as is (sign of zero); anything else
+// falls back to the division operator.
+__device__ __noinline__ float4 div4_slow(float4 v, float d) { return make_float4(v.x / d, v.y / d, v.z / d, v.w / d); }
+__device__ __forceinline__ float4 div4_by_count(float4 v, int k) {
+    const float d = (float)k;
+    auto in_range = [](float x) {           // biased exponent in [38, 216] (2^-89 .. 2^90), or +-0
+        const unsigned b = __float_as_uint(x);
+        return (((b >> 23) & 0xffu) - 38u < 179u) | ((b << 1) == 0u);
+    };
+    if (!(in_range(v.x) & in_range(v.y) & in_range(v.z) & in_range(v.w))) return div4_slow(v, d);
+    float rc = __builtin_amdgcn_rcpf(d);
+    rc = fmaf(fmaf(-d, rc, 1.0f), rc, rc);
+    auto q1 = [&](float x) {
+        float q = x * rc;
+        q = fmaf(fmaf(-d, q, x), rc, q);
+        q = fmaf(fmaf(-d, q, x), rc, q);
+        return x == 0.f ? x : q;
+    };
+    return make_float4(q1(v.x), q1(v.y), q1(v.z), q1(v.w));
+}
+
+// Workgroup barrier that orders LDS only: __syncthreads() is also a release fence for global memory,
+// so it waits for every outstanding global store (and load) of the wave first; where only LDS is
+// shared across the barrier that wait is a full memory round trip for nothing.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Exclusive scan of one int per thread over a whole workgroup of NT threads (NT/64 waves):
 // wave shuffle scans + one LDS round for the wave totals. Returns the exclusive prefix; *total =
-// the workgroup sum (all threads). Two barriers.
-template <int NT>
+// the workgroup sum (all threads). Two barriers (LDS-only ones with LDS_ONLY).
+template <int NT, bool LDS_ONLY = false>
 __device__ __forceinline__ int block_exscan(int v, int* total) {
     __shared__ int wsum[NT / WAVE];
     __shared__ int wtot;
@@ -488,7 +519,7 @@ __device__ __forceinline__ int block_exscan(int v, int* total) {
     int incl = v;
     incl = wave_incl_scan(incl);
     if (lane == WAVE - 1) wsum[w] = incl;
-    __syncthreads();
+    if (LDS_ONLY) lds_barrier(); else __syncthreads();
     if (w == 0) {
         const int x = lane < NT / WAVE ? wsum[lane] : 0;
         int xi = x;
@@ -496,7 +527,7 @@ __device__ __forceinline__ int block_exscan(int v, int* total) {
         if (lane < NT / WAVE) wsum[lane] = xi - x;
         if (lane == NT / WAVE - 1) wtot = xi;
     }
-    __syncthreads();
+    if (LDS_ONLY) lds_barrier(); else __syncthreads();
     *total = wtot;
     return wsum[w] + incl - v;
 }
@@ -557,6 +588,118 @@ __device__ inline void chunk_rank_sort(unsigned long long* keys, unsigned long l
     __syncthreads();
 }
 
+// Block bitonic sort of n2 (power of two, 256 <= n2 <= 4 * blockDim.x, blockDim.x = 1024) u64 keys held in LDS, ascending.
+// Thread t keeps positions 4t..4t+3 in registers: strides 1-2 are in-thread, strides 4-128 are
+// lane exchanges inside the wave (__shfl_xor), only strides >= 256 go through LDS + barriers
+// (10 barrier steps for 4096 keys instead of 78).
+__device__ __forceinline__ void cmpx(unsigned long long& a, unsigned long long& b, bool asc) {
+    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+    a = asc ? lo : hi;
+    b = asc ? hi : lo;
+}
+__device__ inline void bitonic_sort_reg4(unsigned long long* k, int n2) {
+    const int t = threadIdx.x;
+    const bool act = 4 * t < n2;
+    unsigned long long v[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = act ? k[4 * t + r] : ~0ull;
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 256) {
+                __syncthreads();
+                if (act) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) k[4 * t + r] = v[r];
+                }
+                __syncthreads();
+                if (act) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int g = 4 * t + r;
+                        const unsigned long long o = k[g ^ stride];
+                        const bool asc = (g & size) == 0, lower = (g & stride) == 0;
+                        const unsigned long long mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
+                        v[r] = (lower == asc) ? mn : mx;
+                    }
+                }
+            } else if (stride >= 4) {
+                const int lo = stride >> 2;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int g = 4 * t + r;
+                    const unsigned long long o = __shfl_xor(v[r], lo, WAVE);
+                    const bool asc = (g & size) == 0, lower = (g & stride) == 0;
+                    const unsigned long long mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
+                    v[r] = (lower == asc) ? mn : mx;
+                }
+            } else if (stride == 2) {
+                const bool asc = ((4 * t) & size) == 0;
+                cmpx(v[0], v[2], asc);
+                cmpx(v[1], v[3], asc);
+            } else {
+                const bool asc0 = ((4 * t) & size) == 0, asc1 = ((4 * t + 2) & size) == 0;
+                cmpx(v[0], v[1], asc0);
+                cmpx(v[2], v[3], asc1);
+            }
+        }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) k[4 * t + r] = v[r];
+    }
+    __syncthreads();
+}
+
+// Ascending sort of n64 (a multiple of 64, <= 4 * blockDim.x, blockDim.x = 1024) distinct u64 keys in
+// LDS: every 64-key chunk is bitonic-sorted inside one wave (lane exchanges only), then log2(n64 / 64)
+// merge rounds ping-pong between a[] and b[], each thread producing 4 consecutive outputs of one pair
+// of runs after one binary search along the merge path. Returns the buffer holding the result; ends
+// with a barrier. O(n log n): ~4 us for 4096 keys where the rank sort's O(n^2 / 64) took ~26 us.
+__device__ inline unsigned long long* block_merge_sort_u64(unsigned long long* a, unsigned long long* b, int n64) {
+    const int lane = lane_id(), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    for (int c = wv; c < n64 / WAVE; c += nw) {
+        unsigned long long v = a[c * WAVE + lane];
+#pragma unroll
+        for (int size = 2; size <= WAVE; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const unsigned long long o = __shfl_xor(v, stride, WAVE);
+                const bool asc = (lane & size) == 0, lower = (lane & stride) == 0;
+                v = (lower == asc) ? (v < o ? v : o) : (v < o ? o : v);
+            }
+        }
+        a[c * WAVE + lane] = v;
+    }
+    lds_barrier();
+    unsigned long long* src = a;
+    unsigned long long* dst = b;
+    for (int L = WAVE; L < n64; L <<= 1) {
+        const int t0 = 4 * threadIdx.x;
+        if (t0 < n64) {
+            const int s = t0 / (2 * L) * (2 * L);
+            const int la = min(L, n64 - s), lb = max(0, min(L, n64 - s - L));
+            const unsigned long long* A = src + s;
+            const unsigned long long* Bv = src + s + L;
+            const int k0 = t0 - s;
+            int lo = max(0, k0 - lb), hi = min(k0, la);
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (A[mid] < Bv[k0 - 1 - mid]) lo = mid + 1; else hi = mid;
+            }
+            int i = lo, j = k0 - lo;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool ta = i < la && (j >= lb || A[i] < Bv[j]);
+                dst[t0 + u] = ta ? A[i] : Bv[j];
+                if (ta) i++; else j++;
+            }
+        }
+        lds_barrier();
+        unsigned long long* tmp = src; src = dst; dst = tmp;
+    }
+    return src;
+}
 // PCL 1.8 VoxelGrid leaf grid from an ordered-int bbox (voxel_grid.cpp applyFilter)
 __device__ inline void voxel_params(const unsigned* bb, float leaf, bool* overflow, int minb[3], int* mul1, int* mul2) {
     const float inv = 1.0f / leaf;

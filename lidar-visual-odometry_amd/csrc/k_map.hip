@@ -29,6 +29,12 @@ WSTAMP_DEFINE_TABLE
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
+#ifdef ALOAM_WSTAMP_RB       // k_rb_cubevox phases, one row per workgroup (profiling builds only)
+WSTAMP_DEFINE_TABLE
+#define RBSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 128) g_wstamp[(blockIdx.x + (leaf > 0.6f ? 128 : 0)) * WSTAMP_SLOTS + (k)] = wall_clock64(); } while (0)
+#else
+#define RBSTAMP(k) do { } while (0)
+#endif
 
 void prof_mark(Ctx& C, int idx);
 void segment_voxel_launch(Ctx& C, const float4* pts, const int* off, const int* seg_list, const int* nseg_p, int max_seg,
@@ -689,10 +695,20 @@ __global__ void k_cubevox_centroids(const float4* __restrict__ B, const unsigned
 // — the same sequence a stable sort by leaf of the whole cube gives, hence the same centroids (summed in
 // that order) as the device-wide sort. A cube whose old points are not sorted (it was outside the
 // surrounding set when they were appended) or with too many appended points takes a bitonic sort.
+#ifdef ALOAM_WSTAMP_RB
+__device__ int g_rb_info[256][4];
+extern "C" int aloam_dbg_rb_info(int* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rb_info), sizeof(g_rb_info)); }
+__device__ inline void g_dbg_n(int c, int n, int n_o, int uns, float leaf) { const int b = blockIdx.x + (leaf > 0.6f ? 128 : 0); if (blockIdx.x < 128) { g_rb_info[b][0] = c; g_rb_info[b][1] = n; g_rb_info[b][2] = n_o; g_rb_info[b][3] = uns; } }
+#else
+__device__ inline void g_dbg_n(int, int, int, int, float) {}
+#endif
 constexpr int RBV_T = 1024;
-constexpr int RBV_CAP = 12288;       // cube points whose keys / order live in LDS (more: global scratch)
+constexpr int RBV_CAP = 16320;       // cube points whose keys / order live in LDS (more: global scratch)
 constexpr int RBV_NCAP = 4096;       // appended points sorted in LDS (more: the bitonic fallback)
 constexpr size_t RBV_LDS = 256 + 2 * (size_t)RBV_NCAP * 8 + (size_t)RBV_CAP * 4 + (size_t)RBV_CAP * 2;
+constexpr int RBV_PER = 12;          // points per thread held in registers for the bbox and the keys
+constexpr int RBV_RUN = 8;           // sorted positions per thread per centroid pass (n > RBV_T x RBV_RUN: more passes)
+static_assert(RBV_LDS <= 160 * 1024, "LDS");
 struct RbvShared { unsigned bb[6]; int unsorted; int nrun; };
 
 __device__ __forceinline__ void rbv_bitonic_u64(unsigned long long* k, int n2) {   // global or LDS, whole block
@@ -708,26 +724,39 @@ __device__ __forceinline__ void rbv_bitonic_u64(unsigned long long* k, int n2) {
         }
 }
 
-__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__ B, CubeArrays a, const MapState* __restrict__ m,
-                                                      float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// barrier for data that lives in LDS when the cube fits, in global scratch otherwise
+template <bool FITS> __device__ __forceinline__ void rbv_bar() { if (FITS) lds_barrier(); else __syncthreads(); }
+
+template <bool FITS>
+__device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n, int n_o,
+                                         float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr) {
     RbvShared& SH = *(RbvShared*)smem;
     unsigned long long* nk = (unsigned long long*)(smem + 256);
-    unsigned long long* nks = nk + RBV_NCAP;
-    unsigned* lkeys = (unsigned*)(nks + RBV_NCAP);
+    unsigned long long* nk2 = nk + RBV_NCAP;               // merge sort ping-pong
+    unsigned* lkeys = (unsigned*)(nk2 + RBV_NCAP);
     unsigned short* lorder = (unsigned short*)(lkeys + RBV_CAP);
-    const int r = blockIdx.x;
-    if (r >= m->valid_num) return;
-    const int c = m->valid_ind[r];
-    const int p0 = a.off[c], n = a.off[c + 1] - p0;
-    if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
-    const int n_o = old_count(a, c), n_n = n - n_o;
+    const int n_n = n - n_o;
+    RBSTAMP(0);
     if (threadIdx.x < 6) SH.bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     if (threadIdx.x == 0) { SH.unsorted = 0; SH.nrun = 0; }
-    __syncthreads();
-    {   // bbox of the cube's points (ordered-int encoding)
+    lds_barrier();
+    // the cube's points: up to RBV_PER per thread in registers (bbox, then keys without a reload)
+    float4 pt[RBV_PER];
+#pragma unroll
+    for (int u = 0; u < RBV_PER; u++) {
+        const int t = threadIdx.x + u * RBV_T;
+        pt[u] = t < n ? B[p0 + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    {   // bbox (ordered-int encoding)
         unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-        for (int t = threadIdx.x; t < n; t += RBV_T) {
+#pragma unroll
+        for (int u = 0; u < RBV_PER; u++) {
+            if (threadIdx.x + u * RBV_T >= n) continue;
+            const unsigned v[3] = {f2ord(pt[u].x), f2ord(pt[u].y), f2ord(pt[u].z)};
+#pragma unroll
+            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+        }
+        for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) {   // beyond the register tile
             const float4 p = B[p0 + t];
             const unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
 #pragma unroll
@@ -739,7 +768,8 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__
             if (lane_id() == 0) { atomicMin(&SH.bb[d], (unsigned)lo); atomicMax(&SH.bb[3 + d], (unsigned)hi); }
         }
     }
-    __syncthreads();
+    lds_barrier();
+    RBSTAMP(1);
     bool ovf;
     int minb[3], mul1, mul2;
     voxel_params(SH.bb, leaf, &ovf, minb, &mul1, &mul2);    // same bbox -> leaf grid as k_voxel.hip
@@ -749,35 +779,44 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__
         return;
     }
     const float inv = 1.0f / leaf;
-    const bool fits = n <= RBV_CAP;
     unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, order, bitonic (2n)
-    unsigned* keys = fits ? lkeys : (unsigned*)gseg;
+    unsigned* keys = FITS ? lkeys : (unsigned*)gseg;      // compile-time choice: ds_* or global, never flat
     int* gorder = (int*)(gseg + (n + 1) / 2);
-    for (int t = threadIdx.x; t < n; t += RBV_T) keys[t] = voxel_index(B[p0 + t], inv, minb, mul1, mul2);
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RBV_PER; u++) {
+        const int t = threadIdx.x + u * RBV_T;
+        if (t < n) keys[t] = voxel_index(pt[u], inv, minb, mul1, mul2);
+    }
+    for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) keys[t] = voxel_index(B[p0 + t], inv, minb, mul1, mul2);
+    rbv_bar<FITS>();
     for (int t = threadIdx.x; t + 1 < n_o; t += RBV_T)
         if (keys[t] > keys[t + 1]) SH.unsorted = 1;
-    __syncthreads();
-    auto put_order = [&](int pos, int idx) { if (fits) lorder[pos] = (unsigned short)idx; else gorder[pos] = idx; };
+    rbv_bar<FITS>();
+    auto put_order = [&](int pos, int idx) { if (FITS) lorder[pos] = (unsigned short)idx; else gorder[pos] = idx; };
     if (!SH.unsorted && n_n <= RBV_NCAP) {
-        // appended points: sort (leaf, position) keys, then merge by rank with the sorted old points
-        const int n2n = (n_n + WAVE - 1) / WAVE * WAVE;
-        for (int j = threadIdx.x; j < n2n; j += RBV_T)
+        // appended points: sort (leaf, position) keys, then merge with the sorted old points along the
+        // merge path (each thread: one diagonal binary search, then its contiguous run of outputs)
+        const int n2 = (n_n + WAVE - 1) / WAVE * WAVE;
+        for (int j = threadIdx.x; j < n2; j += RBV_T)
             nk[j] = j < n_n ? (((unsigned long long)keys[n_o + j] << 32) | (unsigned)j) : ~0ull;
-        __syncthreads();
-        if (n2n > 0) chunk_rank_sort(nk, nks, n2n);        // ends with a barrier
-        for (int t = threadIdx.x; t < n_o; t += RBV_T) {   // old point t: + appended points of smaller leaf
-            const unsigned long long k = (unsigned long long)keys[t] << 32;
-            int lo = 0, hi = n_n;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (nks[mid] < k) lo = mid + 1; else hi = mid; }
-            put_order(t + lo, t);
-        }
-        for (int j = threadIdx.x; j < n_n; j += RBV_T) {   // j-th appended point: + old points of leaf <= its leaf
-            const unsigned long long e = nks[j];
-            const unsigned lf = (unsigned)(e >> 32);
-            int lo = 0, hi = n_o;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (keys[mid] <= lf) lo = mid + 1; else hi = mid; }
-            put_order(j + lo, n_o + (int)(e & 0xffffffffu));
+        rbv_bar<FITS>();
+        RBSTAMP(2);
+        const unsigned long long* nks = n2 > 0 ? block_merge_sort_u64(nk, nk2, n2) : nk;   // ends with a barrier
+        RBSTAMP(3);
+        const int per = (n + RBV_T - 1) / RBV_T;
+        const int d0 = min(n, (int)threadIdx.x * per), d1 = min(n, d0 + per);
+        if (d0 < d1) {
+            int lo = max(0, d0 - n_n), hi = min(d0, n_o);   // old points among the first d0 outputs
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (keys[mid] <= (unsigned)(nks[d0 - 1 - mid] >> 32)) lo = mid + 1; else hi = mid;   // old first on ties
+            }
+            int i = lo, j = d0 - lo;
+            for (int d = d0; d < d1; d++) {
+                const bool take_old = i < n_o && (j >= n_n || keys[i] <= (unsigned)(nks[j] >> 32));
+                if (take_old) { put_order(d, i); i++; }
+                else { put_order(d, n_o + (int)(nks[j] & 0xffffffffu)); j++; }
+            }
         }
     } else {
         // bitonic sort of (leaf, position) over the cube (global scratch; rare: see above)
@@ -790,37 +829,99 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__
         rbv_bitonic_u64(bk, n2);
         for (int t = threadIdx.x; t < n; t += RBV_T) put_order(t, (int)(bk[t] & 0xffffffffu));
     }
-    __syncthreads();
-    // runs of equal leaves in sorted order -> centroids in order (fp32, the sorted order of the points)
-    auto ord = [&](int pos) { return fits ? (int)lorder[pos] : gorder[pos]; };
-    for (int base = 0; base < n; base += RBV_T) {
-        const int t = base + threadIdx.x;
-        int oi = 0;
-        bool head = false;
-        if (t < n) {
-            oi = ord(t);
-            head = t == 0 || keys[ord(t - 1)] != keys[oi];
+    rbv_bar<FITS>();
+    RBSTAMP(4);
+    // runs of equal leaves in sorted order -> centroids, fp32 in sorted order. Thread k owns sorted
+    // positions [k per, (k+1) per): head flags, one block scan for the run numbers, all its points loaded
+    // at once, then each head sums its run (reading past the thread's range from global memory).
+    auto ord = [&](int pos) { return FITS ? (int)lorder[pos] : gorder[pos]; };
+    auto put_run = [&](int run, float4 v, int k) { Cf[p0 + run] = div4_by_count(v, k); };
+    for (int base = 0; base < n; base += RBV_T * RBV_RUN) {
+        const int per = min(RBV_RUN, (n - base + RBV_T - 1) / RBV_T);
+        const int t0 = base + threadIdx.x * per;
+        int oi[RBV_RUN];
+        unsigned kk[RBV_RUN];
+        int nh = 0;
+        unsigned kprev = 0;
+        if (t0 < n && t0 > 0) kprev = keys[ord(t0 - 1)];
+#pragma unroll
+        for (int u = 0; u < RBV_RUN; u++) {
+            const int t = t0 + u;
+            oi[u] = (u < per && t < n) ? ord(t) : 0;
+            kk[u] = (u < per && t < n) ? keys[oi[u]] : 0;
+        }
+        float4 pv[RBV_RUN];
+#pragma unroll
+        for (int u = 0; u < RBV_RUN; u++) pv[u] = (u < per && t0 + u < n) ? B[p0 + oi[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < RBV_RUN; u++) {
+            const int t = t0 + u;
+            if (u < per && t < n && (t == 0 || kk[u] != (u ? kk[u - 1] : kprev))) nh++;
         }
         int tot;
-        const int run = SH.nrun + block_exscan<RBV_T>(head ? 1 : 0, &tot);
-        if (head) {
-            const unsigned lf = keys[oi];
-            float4 cc = B[p0 + oi];
-            int t2 = t + 1;
-            for (; t2 < n; t2++) {
-                const int o2 = ord(t2);
-                if (keys[o2] != lf) break;
-                const float4 q = B[p0 + o2];
-                cc.x += q.x; cc.y += q.y; cc.z += q.z; cc.w += q.w;
+        int run = SH.nrun + block_exscan<RBV_T, true>(nh, &tot);
+        if (base == 0) RBSTAMP(7);
+        // each run: heads in the thread's range, summed in order (registers, then global past the range)
+        float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int cnt = 0;
+        bool open = false;
+#pragma unroll
+        for (int u = 0; u < RBV_RUN; u++) {
+            const int t = t0 + u;
+            if (!(u < per && t < n)) continue;
+            const bool head = t == 0 || kk[u] != (u ? kk[u - 1] : kprev);
+            if (head) {
+                if (open) { put_run(run, cc, cnt); run++; }
+                cc = pv[u]; cnt = 1; open = true;
+            } else if (open) {
+                cc.x += pv[u].x; cc.y += pv[u].y; cc.z += pv[u].z; cc.w += pv[u].w; cnt++;
             }
-            const float cnt = (float)(t2 - t);
-            Cf[p0 + run] = make_float4(cc.x / cnt, cc.y / cnt, cc.z / cnt, cc.w / cnt);
         }
-        __syncthreads();
+#ifdef ALOAM_WSTAMP_RB
+        lds_barrier();
+        if (base == 0) RBSTAMP(6);
+#endif
+        if (open) {   // the last run begun here may continue into the next threads' positions
+            const unsigned lf = kk[min(per, n - t0) - 1];
+            for (int t = t0 + per; t < n; t += 8) {        // 8 positions per step: one load latency per 8 points
+                int o8[8];
+                bool in8[8];
+                float4 q8[8];
+                bool go = true;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    o8[u] = t + u < n ? ord(t + u) : 0;
+                    go = go && t + u < n && keys[o8[u]] == lf;
+                    in8[u] = go;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) if (in8[u]) q8[u] = B[p0 + o8[u]];
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (in8[u]) { cc.x += q8[u].x; cc.y += q8[u].y; cc.z += q8[u].z; cc.w += q8[u].w; cnt++; }
+                if (!in8[7]) break;
+            }
+            put_run(run, cc, cnt);
+        }
+        lds_barrier();                    // (the centroid stores are left in flight)
         if (threadIdx.x == 0) SH.nrun += tot;
-        __syncthreads();
+        lds_barrier();
     }
-    if (threadIdx.x == 0) a.seg_nout[c] = SH.nrun;
+    RBSTAMP(5);
+    if (threadIdx.x == 0) { a.seg_nout[c] = SH.nrun; g_dbg_n(c, n, n_o, SH.unsorted, leaf); }
+}
+
+__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__ B, CubeArrays a, const MapState* __restrict__ m,
+                                                      float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int r = blockIdx.x;
+    if (r >= m->valid_num) return;
+    const int c = m->valid_ind[r];
+    const int p0 = a.off[c], n = a.off[c + 1] - p0;
+    if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
+    const int n_o = old_count(a, c);
+    if (n <= RBV_CAP) rbv_cube<true>(smem, B, a, c, p0, n, n_o, leaf, Cf, gscr);
+    else rbv_cube<false>(smem, B, a, c, p0, n, n_o, leaf, Cf, gscr);
 }
 
 // old and appended runs per cube in one launch; the run tables are reset by the previous rebuild's

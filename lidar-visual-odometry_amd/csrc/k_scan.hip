@@ -381,69 +381,6 @@ __device__ inline void bitonic_sort_u64(unsigned long long* k, int n2) {
     }
 }
 
-// Block bitonic sort of n2 (power of two, 256 <= n2 <= 4 * LT) u64 keys held in LDS, ascending.
-// Thread t keeps positions 4t..4t+3 in registers: strides 1-2 are in-thread, strides 4-128 are
-// lane exchanges inside the wave (__shfl_xor), only strides >= 256 go through LDS + barriers
-// (10 barrier steps for 4096 keys instead of 78).
-__device__ __forceinline__ void cmpx(unsigned long long& a, unsigned long long& b, bool asc) {
-    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
-    a = asc ? lo : hi;
-    b = asc ? hi : lo;
-}
-__device__ void bitonic_sort_reg4(unsigned long long* k, int n2) {
-    const int t = threadIdx.x;
-    const bool act = 4 * t < n2;
-    unsigned long long v[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) v[r] = act ? k[4 * t + r] : ~0ull;
-    for (int size = 2; size <= n2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            if (stride >= 256) {
-                __syncthreads();
-                if (act) {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) k[4 * t + r] = v[r];
-                }
-                __syncthreads();
-                if (act) {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const int g = 4 * t + r;
-                        const unsigned long long o = k[g ^ stride];
-                        const bool asc = (g & size) == 0, lower = (g & stride) == 0;
-                        const unsigned long long mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
-                        v[r] = (lower == asc) ? mn : mx;
-                    }
-                }
-            } else if (stride >= 4) {
-                const int lo = stride >> 2;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int g = 4 * t + r;
-                    const unsigned long long o = __shfl_xor(v[r], lo, WAVE);
-                    const bool asc = (g & size) == 0, lower = (g & stride) == 0;
-                    const unsigned long long mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
-                    v[r] = (lower == asc) ? mn : mx;
-                }
-            } else if (stride == 2) {
-                const bool asc = ((4 * t) & size) == 0;
-                cmpx(v[0], v[2], asc);
-                cmpx(v[1], v[3], asc);
-            } else {
-                const bool asc0 = ((4 * t) & size) == 0, asc1 = ((4 * t + 2) & size) == 0;
-                cmpx(v[0], v[1], asc0);
-                cmpx(v[2], v[3], asc1);
-            }
-        }
-    }
-    __syncthreads();
-    if (act) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) k[4 * t + r] = v[r];
-    }
-    __syncthreads();
-}
-
 #ifdef ALOAM_LF_TIMING
 __device__ unsigned long long g_lf_ts[64][8];      // micro-benchmark only: per-line phase stamps
 #define LF_TS(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_lf_ts[blockIdx.x][k] = wall_clock64(); } while (0)
