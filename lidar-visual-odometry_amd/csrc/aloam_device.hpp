@@ -651,36 +651,37 @@ __device__ inline void bitonic_sort_reg4(unsigned long long* k, int n2) {
     __syncthreads();
 }
 
-// Ascending sort of n64 (a multiple of 64, <= 4 * blockDim.x, blockDim.x = 1024) distinct u64 keys in
-// LDS: every 64-key chunk is bitonic-sorted inside one wave (lane exchanges only), then log2(n64 / 64)
-// merge rounds ping-pong between a[] and b[], each thread producing 4 consecutive outputs of one pair
-// of runs after one binary search along the merge path. Returns the buffer holding the result; ends
-// with a barrier. O(n log n): ~4 us for 4096 keys where the rank sort's O(n^2 / 64) took ~26 us.
-__device__ inline unsigned long long* block_merge_sort_u64(unsigned long long* a, unsigned long long* b, int n64) {
+// Ascending sort of n64 (a multiple of 64) distinct keys in LDS (GLOBAL: in global scratch, full
+// barriers): every 64-key chunk is bitonic-sorted inside one wave (lane exchanges only), then
+// log2(n64 / 64) merge rounds ping-pong between a[] and b[], each thread producing IPT consecutive
+// outputs of one pair of runs per step after one binary search along the merge path. Returns the
+// buffer holding the result; ends with a barrier. O(n log n): ~4 us for 4096 u64 keys where a rank sort's O(n^2 / 64) took ~26 us.
+template <typename T, int IPT, bool GLOBAL = false>
+__device__ inline T* block_merge_sort(T* a, T* b, int n64) {
+    static_assert(IPT <= 2 * WAVE && (IPT & (IPT - 1)) == 0, "outputs of a thread stay inside one pair of runs");
     const int lane = lane_id(), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
     for (int c = wv; c < n64 / WAVE; c += nw) {
-        unsigned long long v = a[c * WAVE + lane];
+        T v = a[c * WAVE + lane];
 #pragma unroll
         for (int size = 2; size <= WAVE; size <<= 1) {
 #pragma unroll
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                const unsigned long long o = __shfl_xor(v, stride, WAVE);
+                const T o = __shfl_xor(v, stride, WAVE);
                 const bool asc = (lane & size) == 0, lower = (lane & stride) == 0;
                 v = (lower == asc) ? (v < o ? v : o) : (v < o ? o : v);
             }
         }
         a[c * WAVE + lane] = v;
     }
-    lds_barrier();
-    unsigned long long* src = a;
-    unsigned long long* dst = b;
+    if (GLOBAL) __syncthreads(); else lds_barrier();
+    T* src = a;
+    T* dst = b;
     for (int L = WAVE; L < n64; L <<= 1) {
-        const int t0 = 4 * threadIdx.x;
-        if (t0 < n64) {
+        for (int t0 = IPT * threadIdx.x; t0 < n64; t0 += IPT * blockDim.x) {
             const int s = t0 / (2 * L) * (2 * L);
             const int la = min(L, n64 - s), lb = max(0, min(L, n64 - s - L));
-            const unsigned long long* A = src + s;
-            const unsigned long long* Bv = src + s + L;
+            const T* A = src + s;
+            const T* Bv = src + s + L;
             const int k0 = t0 - s;
             int lo = max(0, k0 - lb), hi = min(k0, la);
             while (lo < hi) {
@@ -689,14 +690,14 @@ __device__ inline unsigned long long* block_merge_sort_u64(unsigned long long* a
             }
             int i = lo, j = k0 - lo;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < IPT; u++) {
                 const bool ta = i < la && (j >= lb || A[i] < Bv[j]);
                 dst[t0 + u] = ta ? A[i] : Bv[j];
                 if (ta) i++; else j++;
             }
         }
-        lds_barrier();
-        unsigned long long* tmp = src; src = dst; dst = tmp;
+        if (GLOBAL) __syncthreads(); else lds_barrier();
+        T* tmp = src; src = dst; dst = tmp;
     }
     return src;
 }

@@ -511,7 +511,11 @@ __global__ void k_cube_count_new(const unsigned* __restrict__ skey, int ub, Cube
     }
 }
 // single block: exclusive scan over cubes of v(c); mode 0: cnt_old+cnt_new -> off ; mode 1: final counts -> final_off
+__device__ __forceinline__ void cube_scan_body(const CubeArrays& a, const unsigned char* __restrict__ valid, int mode, int* total);
 __global__ void __launch_bounds__(1024) k_cube_scan(CubeArrays a, const unsigned char* __restrict__ valid, int mode, int* total) {
+    cube_scan_body(a, valid, mode, total);
+}
+__device__ __forceinline__ void cube_scan_body(const CubeArrays& a, const unsigned char* __restrict__ valid, int mode, int* total) {
     constexpr int PER = (CUBE_N + 1023) / 1024;
     int* dst = mode == 0 ? a.off : a.final_off;
     const int c0 = threadIdx.x * PER;
@@ -801,7 +805,7 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
             nk[j] = j < n_n ? (((unsigned long long)keys[n_o + j] << 32) | (unsigned)j) : ~0ull;
         rbv_bar<FITS>();
         RBSTAMP(2);
-        const unsigned long long* nks = n2 > 0 ? block_merge_sort_u64(nk, nk2, n2) : nk;   // ends with a barrier
+        const unsigned long long* nks = n2 > 0 ? block_merge_sort<unsigned long long, 4>(nk, nk2, n2) : nk;   // ends with a barrier
         RBSTAMP(3);
         const int per = (n + RBV_T - 1) / RBV_T;
         const int d0 = min(n, (int)threadIdx.x * per), d1 = min(n, d0 + per);
@@ -911,41 +915,146 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     if (threadIdx.x == 0) { a.seg_nout[c] = SH.nrun; g_dbg_n(c, n, n_o, SH.unsorted, leaf); }
 }
 
-__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(const float4* __restrict__ B, CubeArrays a, const MapState* __restrict__ m,
-                                                      float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int r = blockIdx.x;
-    if (r >= m->valid_num) return;
-    const int c = m->valid_ind[r];
-    const int p0 = a.off[c], n = a.off[c + 1] - p0;
-    if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
-    const int n_o = old_count(a, c);
-    if (n <= RBV_CAP) rbv_cube<true>(smem, B, a, c, p0, n, n_o, leaf, Cf, gscr);
-    else rbv_cube<false>(smem, B, a, c, p0, n, n_o, leaf, Cf, gscr);
-}
+// ------------------------------------------------------------------------------------------
+// Both map kinds per launch (blockIdx.y / blockIdx.x = kind): insert -> sort + scan -> scatter ->
+// per-cube VoxelGrid -> final scan -> copy, 6 launches on one stream for the two kinds.
+struct RbKind {
+    const float4* stack; const int* d_stack_n; int ub_new; float leaf;
+    float4* A; int* Acube; int* d_n; int n_old_ub;        // the kind's map (old points in, rebuilt map out)
+    float4* B; int* Bcube;                                // old + appended points grouped by cube
+    float4* ins_pts; unsigned* k1; unsigned* k2; int* v2; // appended points in the map frame, cube keys
+    float4* Cf; unsigned long long* gscr;                 // per-cube VoxelGrid output / global scratch
+    CubeArrays a;
+};
+struct RbKinds { RbKind k[2]; };
 
-// old and appended runs per cube in one launch; the run tables are reset by the previous rebuild's
-// final copy (k_cube_final_reset), so no reset launch
-__global__ void k_rb_count(const int* __restrict__ cube, const int* d_n, const unsigned* __restrict__ skey, int ub, CubeArrays a) {
-    const int n = *d_n;
+// stack point -> map frame -> cube key (k_map_insert), and the old map's per-cube runs (the map is
+// ordered by cube); the run tables were reset by the previous rebuild's final copy
+__global__ void k_rb_insert(RbKinds P, const MapState* __restrict__ m) {
+    const RbKind& K = P.k[blockIdx.y];
+    const int n = *K.d_stack_n, n_old = *K.d_n;
     const int stride = gridDim.x * MB;
-    for (int i = blockIdx.x * MB + threadIdx.x; i < max(n, ub); i += stride) {
-        if (i < n) {
-            const int c = cube[i];
-            if (c >= 0) {
-                if (i == 0 || cube[i - 1] != c) a.first_old[c] = i;
-                if (i == n - 1 || cube[i + 1] != c) a.last_old[c] = i;
+    for (int i = blockIdx.x * MB + threadIdx.x; i < max(n_old, K.ub_new); i += stride) {
+        if (i < K.ub_new) {
+            unsigned k = PAD_CUBE;
+            if (i < n) {
+                const float4 s = associate_to_map(m->parameters, K.stack[i]);
+                K.ins_pts[i] = s;
+                const int ci = cube_coord(s.x, m->cenW), cj = cube_coord(s.y, m->cenH), ck = cube_coord(s.z, m->cenD);
+                if (ci >= 0 && ci < CUBE_W && cj >= 0 && cj < CUBE_H && ck >= 0 && ck < CUBE_D)
+                    k = (unsigned)(ci + CUBE_W * cj + CUBE_W * CUBE_H * ck);
             }
+            K.k1[i] = k;
         }
-        if (i < ub) {
-            const unsigned c = skey[i];
-            if (c < (unsigned)CUBE_N) {
-                if (i == 0 || skey[i - 1] != c) a.first_new[c] = i;
-                if (i == ub - 1 || skey[i + 1] != c) a.last_new[c] = i;
+        if (i < n_old) {
+            const int c = K.Acube[i];
+            if (c >= 0) {
+                if (i == 0 || K.Acube[i - 1] != c) K.a.first_old[c] = i;
+                if (i == n_old - 1 || K.Acube[i + 1] != c) K.a.last_old[c] = i;
             }
         }
     }
 }
+
+// one workgroup per kind: stable sort of the appended points by cube ((cube, index) keys, merge sort in
+// LDS; more than RBS_CAP points: the same sort on u64 keys in global scratch), their per-cube runs, then
+// the exclusive scan of old + appended counts over the cubes (k_cube_scan mode 0)
+constexpr int RBS_T = 1024, RBS_IPT = 16, RBS_CAP = RBS_T * RBS_IPT;   // 16384 keys < 2^16 positions
+constexpr size_t RBS_LDS = 2 * (size_t)RBS_CAP * 4;
+__global__ void __launch_bounds__(RBS_T) k_rb_sort_scan(RbKinds P, const unsigned char* __restrict__ valid) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RbKind& K = P.k[blockIdx.x];
+    const int n = min(*K.d_stack_n, K.ub_new);            // keys >= n are PAD_CUBE: sorted last, ignored
+    const int n64 = (n + WAVE - 1) / WAVE * WAVE;
+    if (n64 > 0 && n64 <= RBS_CAP) {
+        unsigned* ka = (unsigned*)smem;
+        for (int i = threadIdx.x; i < n64; i += RBS_T) ka[i] = i < n ? ((K.k1[i] << 16) | (unsigned)i) : 0xffffffffu;
+        lds_barrier();
+        const unsigned* sk = block_merge_sort<unsigned, RBS_IPT>(ka, ka + RBS_CAP, n64);
+        for (int p = threadIdx.x; p < n; p += RBS_T) {
+            const unsigned c = sk[p] >> 16;
+            K.k2[p] = c;
+            K.v2[p] = (int)(sk[p] & 0xffffu);
+            if (c < (unsigned)CUBE_N) {
+                if (p == 0 || (sk[p - 1] >> 16) != c) K.a.first_new[c] = p;
+                if (p == n - 1 || (sk[p + 1] >> 16) != c) K.a.last_new[c] = p;
+            }
+        }
+    } else if (n64 > 0) {
+        unsigned long long* ga = K.gscr;
+        for (int i = threadIdx.x; i < n64; i += RBS_T) ga[i] = i < n ? (((unsigned long long)K.k1[i] << 32) | (unsigned)i) : ~0ull;
+        __syncthreads();
+        const unsigned long long* sk = block_merge_sort<unsigned long long, RBS_IPT, true>(ga, ga + n64, n64);
+        for (int p = threadIdx.x; p < n; p += RBS_T) {
+            const unsigned c = (unsigned)(sk[p] >> 32);
+            K.k2[p] = c;
+            K.v2[p] = (int)(sk[p] & 0xffffffffu);
+            if (c < (unsigned)CUBE_N) {
+                if (p == 0 || (unsigned)(sk[p - 1] >> 32) != c) K.a.first_new[c] = p;
+                if (p == n - 1 || (unsigned)(sk[p + 1] >> 32) != c) K.a.last_new[c] = p;
+            }
+        }
+    }
+    __syncthreads();                                      // run tables (global) -> the scan below
+    cube_scan_body(K.a, valid, 0, nullptr);
+}
+
+__global__ void k_rb_scatter(RbKinds P) {
+    const RbKind& K = P.k[blockIdx.y];
+    const int n_old = *K.d_n, n_new = min(*K.d_stack_n, K.ub_new);
+    const int stride = gridDim.x * MB;
+    for (int i = blockIdx.x * MB + threadIdx.x; i < n_old; i += stride) {
+        const int c = K.Acube[i];
+        if (c < 0) continue;
+        const int pos = K.a.off[c] + (i - K.a.first_old[c]);
+        K.B[pos] = K.A[i];
+        K.Bcube[pos] = c;
+    }
+    for (int p = blockIdx.x * MB + threadIdx.x; p < n_new; p += stride) {
+        const unsigned c = K.k2[p];
+        if (c >= (unsigned)CUBE_N) continue;
+        const int pos = K.a.off[c] + old_count(K.a, c) + (p - K.a.first_new[c]);
+        K.B[pos] = K.ins_pts[K.v2[p]];
+        K.Bcube[pos] = (int)c;
+    }
+}
+
+__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState* __restrict__ m) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RbKind& K = P.k[blockIdx.y];
+    const int r = blockIdx.x;
+    if (r >= m->valid_num) return;
+    const int c = m->valid_ind[r];
+    const CubeArrays& a = K.a;
+    const int p0 = a.off[c], n = a.off[c + 1] - p0;
+    if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
+    const int n_o = old_count(a, c);
+    if (n <= RBV_CAP) rbv_cube<true>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr);
+    else rbv_cube<false>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr);
+}
+
+__global__ void __launch_bounds__(1024) k_rb_final_scan(RbKinds P, const unsigned char* __restrict__ valid) {
+    const RbKind& K = P.k[blockIdx.x];
+    cube_scan_body(K.a, valid, 1, K.d_n);
+}
+
+// rebuilt map into A (valid cubes: their VoxelGrid output; others: old + appended as grouped), then the
+// next rebuild's run tables
+__global__ void k_rb_final(RbKinds P, const unsigned char* __restrict__ valid) {
+    const RbKind& K = P.k[blockIdx.y];
+    const CubeArrays& a = K.a;
+    const int total = a.off[CUBE_N];
+    for (int p = blockIdx.x * MB + threadIdx.x; p < total; p += gridDim.x * MB) {
+        const int c = K.Bcube[p];
+        const int local = p - a.off[c];
+        if (!valid[c]) { K.A[a.final_off[c] + local] = K.B[p]; K.Acube[a.final_off[c] + local] = c; }
+        else if (local < a.seg_nout[c]) { K.A[a.final_off[c] + local] = K.Cf[p]; K.Acube[a.final_off[c] + local] = c; }
+    }
+    for (int c = blockIdx.x * MB + threadIdx.x; c <= CUBE_N; c += gridDim.x * MB) {
+        a.last_old[c] = -1; a.last_new[c] = -1; a.first_old[c] = 0x7fffffff; a.first_new[c] = 0x7fffffff;
+    }
+}
+
 __global__ void k_cube_final_reset(const float4* __restrict__ B, const int* __restrict__ Bcube, const float4* __restrict__ Cf,
                                    const unsigned char* __restrict__ valid, CubeArrays a, float4* __restrict__ A, int* __restrict__ Acube) {
     const int total = a.off[CUBE_N];
@@ -976,6 +1085,51 @@ static int nblk(int n) { return std::max(1, std::min(2048, (n + MB - 1) / MB)); 
 // 0: the per-cube VoxelGrid as one device-wide radix sort + 12 launches (round-1 path, kept for A/B)
 static const int g_rebuild_fused = getenv("ALOAM_REBUILD_FUSED") ? atoi(getenv("ALOAM_REBUILD_FUSED")) : 1;
 
+static CubeArrays cube_arrays(Ctx& C, int which) {
+    CubeArrays a;
+    int* base = C.d_cube_cnt + which * 7 * (CUBE_N + 1);
+    a.first_old = base; a.last_old = base + (CUBE_N + 1); a.first_new = base + 2 * (CUBE_N + 1);
+    a.last_new = base + 3 * (CUBE_N + 1); a.off = base + 4 * (CUBE_N + 1); a.seg_nout = base + 5 * (CUBE_N + 1);
+    a.final_off = base + 6 * (CUBE_N + 1);
+    return a;
+}
+
+// both kinds' map update (:739-797 + the per-cube VoxelGrid :799-820) in 6 launches on the frame's stream
+static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, const int* stack_n, int ub_c, int ub_s) {
+    hipStream_t st = C.stream;
+    if (C.n_mc + C.n_ms + 2 * std::max(ub_c, ub_s) > C.cap_map) throw ApiError{ALOAM_E_CAPACITY, "map capacity exceeded"};
+    RbKinds P;
+    for (int w = 0; w < 2; w++) {
+        RbKind& k = P.k[w];
+        KindScratch& K = C.ks[w];
+        k.stack = w == 0 ? cstack : sstack;
+        k.d_stack_n = stack_n + w;
+        k.ub_new = w == 0 ? ub_c : ub_s;
+        k.leaf = w == 0 ? C.P.mapping_line_resolution : C.P.mapping_plane_resolution;
+        k.A = w == 0 ? C.d_mc : C.d_ms;
+        k.Acube = w == 0 ? C.d_mc_cube : C.d_ms_cube;
+        k.d_n = C.d_map_n + w;
+        k.n_old_ub = w == 0 ? C.n_mc : C.n_ms;
+        k.B = w == 0 ? C.d_mc2 : C.d_ms2;
+        k.Bcube = w == 0 ? C.d_mc2_cube : C.d_ms2_cube;
+        k.ins_pts = K.ins_pts;
+        k.k1 = (unsigned*)K.vkeys;
+        k.k2 = (unsigned*)K.vkeys2;
+        k.v2 = K.ins_val2;
+        k.Cf = K.map_tmp;
+        k.gscr = K.seg_keys + 32768;
+        k.a = cube_arrays(C, w);
+    }
+    const int n_old = std::max(C.n_mc, C.n_ms), ub = std::max(ub_c, ub_s);
+    k_rb_insert<<<dim3(nblk(std::max(n_old, ub)), 2), MB, 0, st>>>(P, C.d_map);
+    k_rb_sort_scan<<<2, RBS_T, RBS_LDS, st>>>(P, C.d_cube_valid);
+    k_rb_scatter<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P);
+    k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
+    k_rb_final_scan<<<2, 1024, 0, st>>>(P, C.d_cube_valid);
+    k_rb_final<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P, C.d_cube_valid);
+    HIPCHK(hipGetLastError());
+}
+
 static int g_map_exp();
 static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, const int* d_stack_n, float leaf) {
     hipStream_t st = (which && !(g_map_exp() & 8)) ? C.stream2 : C.stream;   // the kinds rebuild concurrently
@@ -999,19 +1153,6 @@ static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, cons
     if (ub_new > 0) {
         size_t bytes = C.sort_tmp_bytes;
         HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, k1, k2, K.ins_val, K.ins_val2, (unsigned)ub_new, 0, 13, st));
-    }
-    if (g_rebuild_fused) {
-        // counts (tables reset by the last rebuild) -> offsets -> old + appended points by cube into B ->
-        // per-cube VoxelGrid of the surrounding cubes into Cf -> final offsets -> copy (+ table reset)
-        float4* Cf = K.map_tmp;
-        k_rb_count<<<nblk(std::max(n_old_ub, ub_new)), MB, 0, st>>>(Acube, d_n_old, k2, ub_new, a);
-        k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 0, nullptr);
-        k_cube_scatter<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(A, Acube, d_n_old, K.ins_pts, k2, K.ins_val2, ub_new, a, B, Bcube);
-        k_rb_cubevox<<<125, RBV_T, RBV_LDS, st>>>(B, a, C.d_map, leaf, Cf, K.seg_keys + 32768);
-        k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 1, d_n_old);
-        k_cube_final_reset<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(B, Bcube, Cf, C.d_cube_valid, a, A, Acube);
-        HIPCHK(hipGetLastError());
-        return;
     }
     k_cube_reset<<<(CUBE_N + 1 + 255) / 256, 256, 0, st>>>(a);
     k_cube_count_old<<<nblk(n_old_ub), MB, 0, st>>>(Acube, d_n_old, a);
@@ -1049,6 +1190,7 @@ void rebuild_init(Ctx& C) {
     static bool attr = false;
     if (!attr) {
         HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubevox, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBV_LDS));
+        HIPCHK(hipFuncSetAttribute((const void*)k_rb_sort_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBS_LDS));
         attr = true;
     }
     for (int which = 0; which < 2; which++) {
@@ -1069,6 +1211,27 @@ static const int g_fit_split = getenv("ALOAM_FIT_SPLIT") ? atoi(getenv("ALOAM_FI
 static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 8;   // tuning knob: lanes per query (C3, serial on 256 CUs: 8 / 16 / 32 = 25.5 / 19.9 / 29.0 us; pipeline on 128 CUs: 8 / 16 = 22.2 / 24.6 us)
 static const int g_map_u = getenv("ALOAM_MAP_U") ? atoi(getenv("ALOAM_MAP_U")) : 4;     // tuning knob: loads in flight
 static int g_map_exp() { return g_exp; }
+// ALOAM_MAP_PHASES (profiling aid): GPU time of the frame's phases from events on the frame's stream,
+// read back two frames later (that frame is complete by then), means printed every 200 frames
+static const bool g_map_phases = getenv("ALOAM_MAP_PHASES") != nullptr;
+static void map_phase(Ctx& C, int k) {
+    static hipEvent_t ev[2][5];
+    static bool made = false, used[2] = {false, false};
+    static double acc[4] = {0, 0, 0, 0};
+    static long frame = 0, nacc = 0;
+    if (!made) { for (auto& r : ev) for (auto& e : r) HIPCHK(hipEventCreate(&e)); made = true; }
+    const int s = (int)(frame & 1);
+    if (k == 0 && used[s]) {
+        HIPCHK(hipEventSynchronize(ev[s][4]));
+        for (int i = 0; i < 4; i++) { float ms = 0; HIPCHK(hipEventElapsedTime(&ms, ev[s][i], ev[s][i + 1])); acc[i] += ms * 1e3; }
+        if (++nacc % 200 == 0)
+            std::fprintf(stderr, "[aloam map phases] us per frame: prepare+grids %.1f, rounds %.1f, rebuild %.1f, register %.1f (mean of %ld)\n",
+                         acc[0] / nacc, acc[1] / nacc, acc[2] / nacc, acc[3] / nacc, nacc);
+    }
+    HIPCHK(hipEventRecord(ev[s][k], C.stream));
+    if (k == 4) { used[s] = true; frame++; }
+}
+
 void map_frame_launch(Ctx& C, int X) {
     hipStream_t st = C.stream;
     Ctx::MapInSet& in = C.mset[X];
@@ -1077,6 +1240,7 @@ void map_frame_launch(Ctx& C, int X) {
     // an input set written on another stream (stream3 hand-off, or this context's stream2 stacks): its
     // clouds, pose and stacks are complete at `ready` — wait before the first kernel that reads the pose
     if (in.stacks_pub || in.stacks) HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
+    if (g_map_phases) map_phase(C, 0);
     k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_map_spread, voxel_hdr(C, 0), voxel_hdr(C, 1),
                                      in.pose);
     k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
@@ -1100,6 +1264,7 @@ void map_frame_launch(Ctx& C, int X) {
     in.stacks = false;
     in.stacks_pub = false;
     const int nq = ub_c + ub_s;
+    if (g_map_phases) map_phase(C, 1);
     C.t_rounds_issued = std::chrono::steady_clock::now();
     if (nq > 0) {
         if (nq > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity exceeded"};
@@ -1129,16 +1294,22 @@ void map_frame_launch(Ctx& C, int X) {
         if (C.profiling || !C.use_graphs) issue(true, hint);
         else run_graph(C, 2 + X, in.cstack, in.sstack, rounds, [&] { issue(false, hint); });
     }
+    if (g_map_phases) map_phase(C, 2);
     k_map_update<<<1, 64, 0, st>>>(C.d_map, C.d_map_spread, std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS),
                                    C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS);
-    if (!(g_exp & 4)) {              // (profiling experiment 4: skip the map update — results invalid)
+    if (g_exp & 4) {                 // (profiling experiment 4: skip the map update — results invalid)
+    } else if (g_rebuild_fused) {
+        rebuild_maps(C, in.cstack, in.sstack, stack_n, ub_c, ub_s);
+    } else {
         fork_lane1(C);
         rebuild_map(C, 0, ub_c, in.cstack, stack_n + 0, C.P.mapping_line_resolution);
         rebuild_map(C, 1, ub_s, in.sstack, stack_n + 1, C.P.mapping_plane_resolution);
         join_lane1(C);
     }
+    if (g_map_phases) map_phase(C, 3);
     if (in.nf > 0)
         k_map_register<<<(in.nf + MB - 1) / MB, MB, 0, st>>>(in.full, in.nf, C.d_map, C.d_registered);
+    if (g_map_phases) map_phase(C, 4);
     HIPCHK(hipGetLastError());
 }
 
