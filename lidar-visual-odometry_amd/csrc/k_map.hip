@@ -922,7 +922,7 @@ struct RbKind {
     const float4* stack; const int* d_stack_n; int ub_new; float leaf;
     float4* A; int* Acube; int* d_n; int n_old_ub;        // the kind's map (old points in, rebuilt map out)
     float4* B; int* Bcube;                                // old + appended points grouped by cube
-    float4* ins_pts; unsigned* k1; unsigned* k2; int* v2; // appended points in the map frame, cube keys
+    float4* ins_pts; unsigned* k1; int* v2;               // appended points in the map frame, cube keys, ranks
     float4* Cf; unsigned long long* gscr;                 // per-cube VoxelGrid output / global scratch
     CubeArrays a;
 };
@@ -956,43 +956,92 @@ __global__ void k_rb_insert(RbKinds P, const MapState* __restrict__ m) {
     }
 }
 
-// one workgroup per kind: stable sort of the appended points by cube ((cube, index) keys, merge sort in
-// LDS; more than RBS_CAP points: the same sort on u64 keys in global scratch), their per-cube runs, then
-// the exclusive scan of old + appended counts over the cubes (k_cube_scan mode 0)
-constexpr int RBS_T = 1024, RBS_IPT = 16, RBS_CAP = RBS_T * RBS_IPT;   // 16384 keys < 2^16 positions
-constexpr size_t RBS_LDS = 2 * (size_t)RBS_CAP * 4;
+// one workgroup per kind: stable rank of every appended point among the kind's appended points of its
+// cube (its slot after the cube's old points), the per-cube appended counts, then the exclusive scan of
+// old + appended counts over the cubes (k_cube_scan mode 0). Counting, not sorting: wave w owns a
+// contiguous chunk of the points and a u16 count row per cube in LDS; pass 1 counts (per 64-point batch,
+// one ballot per distinct cube — the stacks come in leaf order, so a batch holds few cubes), the rows
+// are turned into per-wave bases by a scan over the waves, pass 2 re-walks the chunk handing out ranks
+// in order. Same ranks as a stable sort by cube. Over 65535 points: a merge sort in global scratch.
+constexpr int RBS_T = 1024, RBS_W = RBS_T / WAVE;
+constexpr size_t RBS_LDS = (size_t)RBS_W * CUBE_N * 2;
+static_assert(RBS_LDS <= 160 * 1024 - 1024, "LDS");
+// the 64 lanes' keys (ok = lane holds a real point): each lane gets its rank among the lanes with the
+// same key below it plus cnt[key]; cnt[key] += the key's lanes (one distinct key per step)
+__device__ __forceinline__ int wave_rank_by_key(unsigned key, bool ok, unsigned short* cnt) {
+    const int lane = lane_id();
+    unsigned long long todo = __ballot(ok);
+    int rank = 0;
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const unsigned kl = (unsigned)__builtin_amdgcn_readlane((int)key, leader);
+        const unsigned long long m = __ballot(ok && key == kl) & todo;
+        const int base = cnt[kl];                      // uniform address: one LDS read for the wave
+        if (ok && key == kl) rank = base + __popcll(m & lanemask_lt64());
+        if (lane == leader) cnt[kl] = (unsigned short)(base + __popcll(m));
+        todo &= ~m;
+    }
+    return rank;
+}
 __global__ void __launch_bounds__(RBS_T) k_rb_sort_scan(RbKinds P, const unsigned char* __restrict__ valid) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RbKind& K = P.k[blockIdx.x];
-    const int n = min(*K.d_stack_n, K.ub_new);            // keys >= n are PAD_CUBE: sorted last, ignored
-    const int n64 = (n + WAVE - 1) / WAVE * WAVE;
-    if (n64 > 0 && n64 <= RBS_CAP) {
-        unsigned* ka = (unsigned*)smem;
-        for (int i = threadIdx.x; i < n64; i += RBS_T) ka[i] = i < n ? ((K.k1[i] << 16) | (unsigned)i) : 0xffffffffu;
+    const int n = min(*K.d_stack_n, K.ub_new);
+    const int lane = lane_id(), w = threadIdx.x / WAVE;
+    if (n < 65536) {
+        unsigned short* cnt = (unsigned short*)smem;   // [RBS_W][CUBE_N]
+        for (int i = threadIdx.x; i < RBS_W * CUBE_N / 2; i += RBS_T) ((unsigned*)cnt)[i] = 0;
+        if (threadIdx.x == 0 && (RBS_W * CUBE_N) % 2) cnt[RBS_W * CUBE_N - 1] = 0;
         lds_barrier();
-        const unsigned* sk = block_merge_sort<unsigned, RBS_IPT>(ka, ka + RBS_CAP, n64);
-        for (int p = threadIdx.x; p < n; p += RBS_T) {
-            const unsigned c = sk[p] >> 16;
-            K.k2[p] = c;
-            K.v2[p] = (int)(sk[p] & 0xffffu);
-            if (c < (unsigned)CUBE_N) {
-                if (p == 0 || (sk[p - 1] >> 16) != c) K.a.first_new[c] = p;
-                if (p == n - 1 || (sk[p + 1] >> 16) != c) K.a.last_new[c] = p;
+        const int per = ((n + RBS_W - 1) / RBS_W + WAVE - 1) / WAVE * WAVE;
+        const int i0 = w * per, i1 = min(n, i0 + per);
+        unsigned short* row = cnt + w * CUBE_N;
+        constexpr int U = 8;                            // batches whose keys are loaded together
+        for (int pass = 0; pass < 2; pass++) {
+            for (int b0 = i0; b0 < i1; b0 += U * WAVE) {
+                unsigned kk[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int i = b0 + u * WAVE + lane;
+                    kk[u] = i < i1 ? K.k1[i] : PAD_CUBE;
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    if (b0 + u * WAVE >= i1) break;
+                    const int i = b0 + u * WAVE + lane;
+                    const bool ok = kk[u] < (unsigned)CUBE_N;
+                    const int r = wave_rank_by_key(kk[u], ok, row);
+                    if (pass == 1 && ok) K.v2[i] = r;
+                }
+            }
+            if (pass == 0) {
+                __syncthreads();
+                for (int c = threadIdx.x; c < CUBE_N; c += RBS_T) {   // counts -> per-wave bases, cube totals
+                    int run = 0;
+#pragma unroll
+                    for (int v = 0; v < RBS_W; v++) { const int t = cnt[v * CUBE_N + c]; cnt[v * CUBE_N + c] = (unsigned short)run; run += t; }
+                    if (run > 0) { K.a.first_new[c] = 0; K.a.last_new[c] = run - 1; }
+                }
+                __syncthreads();
             }
         }
-    } else if (n64 > 0) {
+    } else {
+        const int n64 = (n + WAVE - 1) / WAVE * WAVE;
         unsigned long long* ga = K.gscr;
         for (int i = threadIdx.x; i < n64; i += RBS_T) ga[i] = i < n ? (((unsigned long long)K.k1[i] << 32) | (unsigned)i) : ~0ull;
         __syncthreads();
-        const unsigned long long* sk = block_merge_sort<unsigned long long, RBS_IPT, true>(ga, ga + n64, n64);
+        const unsigned long long* sk = block_merge_sort<unsigned long long, 16, true>(ga, ga + n64, n64);
         for (int p = threadIdx.x; p < n; p += RBS_T) {
             const unsigned c = (unsigned)(sk[p] >> 32);
-            K.k2[p] = c;
-            K.v2[p] = (int)(sk[p] & 0xffffffffu);
             if (c < (unsigned)CUBE_N) {
                 if (p == 0 || (unsigned)(sk[p - 1] >> 32) != c) K.a.first_new[c] = p;
                 if (p == n - 1 || (unsigned)(sk[p + 1] >> 32) != c) K.a.last_new[c] = p;
             }
+        }
+        __syncthreads();
+        for (int p = threadIdx.x; p < n; p += RBS_T) {
+            const unsigned c = (unsigned)(sk[p] >> 32);
+            if (c < (unsigned)CUBE_N) K.v2[(int)(sk[p] & 0xffffffffu)] = p - K.a.first_new[c];
         }
     }
     __syncthreads();                                      // run tables (global) -> the scan below
@@ -1010,11 +1059,11 @@ __global__ void k_rb_scatter(RbKinds P) {
         K.B[pos] = K.A[i];
         K.Bcube[pos] = c;
     }
-    for (int p = blockIdx.x * MB + threadIdx.x; p < n_new; p += stride) {
-        const unsigned c = K.k2[p];
+    for (int i = blockIdx.x * MB + threadIdx.x; i < n_new; i += stride) {   // appended: rank within the cube
+        const unsigned c = K.k1[i];
         if (c >= (unsigned)CUBE_N) continue;
-        const int pos = K.a.off[c] + old_count(K.a, c) + (p - K.a.first_new[c]);
-        K.B[pos] = K.ins_pts[K.v2[p]];
+        const int pos = K.a.off[c] + old_count(K.a, c) + K.v2[i];
+        K.B[pos] = K.ins_pts[i];
         K.Bcube[pos] = (int)c;
     }
 }
@@ -1114,7 +1163,6 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
         k.Bcube = w == 0 ? C.d_mc2_cube : C.d_ms2_cube;
         k.ins_pts = K.ins_pts;
         k.k1 = (unsigned*)K.vkeys;
-        k.k2 = (unsigned*)K.vkeys2;
         k.v2 = K.ins_val2;
         k.Cf = K.map_tmp;
         k.gscr = K.seg_keys + 32768;
