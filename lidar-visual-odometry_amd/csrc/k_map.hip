@@ -1259,6 +1259,7 @@ static const int g_fit_split = getenv("ALOAM_FIT_SPLIT") ? atoi(getenv("ALOAM_FI
 static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 8;   // tuning knob: lanes per query (C3, serial on 256 CUs: 8 / 16 / 32 = 25.5 / 19.9 / 29.0 us; pipeline on 128 CUs: 8 / 16 = 22.2 / 24.6 us)
 static const int g_map_u = getenv("ALOAM_MAP_U") ? atoi(getenv("ALOAM_MAP_U")) : 4;     // tuning knob: loads in flight
 static int g_map_exp() { return g_exp; }
+__global__ void k_noop() {}
 // ALOAM_MAP_PHASES (profiling aid): GPU time of the frame's phases from events on the frame's stream,
 // read back two frames later (that frame is complete by then), means printed every 200 frames
 static const bool g_map_phases = getenv("ALOAM_MAP_PHASES") != nullptr;
@@ -1334,6 +1335,7 @@ void map_frame_launch(Ctx& C, int X) {
                     k_map_fit<<<FIT_BLOCKS, 256, 0, st>>>(in.cstack, in.sstack, stack_n, C.g_map_corner.pts, C.g_map_surf.pts, C.d_map,
                                                          C.d_nbr, C.d_factors, cnt);
                 if (marks) prof_mark(C, 7 + 2 * (ALOAM_MAX_ROUNDS + it));
+                if (g_exp & 16) k_noop<<<1, 64, 0, st>>>();   // (profiling experiment 16: cost of a kernel boundary)
                 lm_run(C, C.d_factors, C.cap_factors, C.d_map->parameters, ALOAM_MAX_ROUNDS + it, &C.d_map->optimize,
                        stack_n, live_hint);
             }

@@ -493,8 +493,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     if (!big) {
 #endif
         const int M = e - s;                                             // positions s .. e-1
-        int n2 = 256;
-        while (n2 < M) n2 <<= 1;
+        const int n2 = (M + WAVE - 1) / WAVE * WAVE;
         for (int i = threadIdx.x; i < n2; i += LT) {
             unsigned long long key = ~0ull;
             if (i < M) {
@@ -508,12 +507,12 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         }
         __syncthreads();
         LF_TS3(1);
-        chunk_rank_sort(keys, sorted, n2);
+        const unsigned long long* sorted_k = block_merge_sort<unsigned long long, LINE_LDS_CAP / LT>(keys, sorted, n2);
         LF_TS3(2);
         for (int i = threadIdx.x; i < M; i += LT) {
-            const unsigned long long key = sorted[i];
+            const unsigned long long key = sorted_k[i];
             S[s - off0 + i] = s + (int)(key & 0xfffu);
-            if (i > 0 && (sorted[i - 1] >> 12) == (key >> 12)) {        // exact tie: sorted slots s+i-1, s+i
+            if (i > 0 && (sorted_k[i - 1] >> 12) == (key >> 12)) {      // exact tie: sorted slots s+i-1, s+i
                 atomicMin(&s_tlo[(int)(key >> 44)], s + i - 1);
                 atomicMax(&s_thi[(int)(key >> 44)], s + i);
             }
@@ -749,8 +748,9 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         divb[d] = maxb - minb[d] + 1;
     }
     const int mul1 = divb[0], mul2 = divb[0] * divb[1];
-    int n2 = 1;
-    while (n2 < nc) n2 <<= 1;
+    int n2 = 1;                            // big lines: power-of-two bitonic; LDS lines: multiple of 64
+    if (big) while (n2 < nc) n2 <<= 1;
+    else n2 = (nc + WAVE - 1) / WAVE * WAVE;
     for (int t = threadIdx.x; t < n2; t += LT) {
         unsigned long long key = ~0ull;
         if (t < nc) {
@@ -769,10 +769,11 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     }
     __syncthreads();
     LF_TS(4);
-    if (!big && n2 >= WAVE) {
-        chunk_rank_sort(keys, sorted, n2);
-        for (int t = threadIdx.x; t < n2; t += LT) keys[t] = sorted[t];
-        __syncthreads();
+    if (!big) {
+        if (n2 > 0 && block_merge_sort<unsigned long long, LINE_LDS_CAP / LT>(keys, sorted, n2) != keys) {
+            for (int t = threadIdx.x; t < n2; t += LT) keys[t] = sorted[t];
+            __syncthreads();
+        }
     } else {
         bitonic_sort_u64(keys, n2);
     }
