@@ -315,6 +315,26 @@ __global__ void k_pc2_gather(const unsigned char* __restrict__ blob, int n, int 
     out[i] = make_float4(r[0], r[1], r[2], 0.f);
 }
 
+// ALOAM_FRONT_PHASES (profiling aid): GPU time of the front's phases (scanRegistration, odometry
+// rounds, compose + grid builds) from events on the stream, read back at the next scan's start
+static const bool g_front_phases = getenv("ALOAM_FRONT_PHASES") != nullptr;
+static void front_phase(Ctx& C, int k) {
+    static hipEvent_t ev[5];
+    static bool made = false, used = false;
+    static double acc[4] = {0, 0, 0, 0};
+    static long nacc = 0;
+    if (!made) { for (auto& e : ev) HIPCHK(hipEventCreate(&e)); made = true; }
+    if (k == 0 && used) {
+        HIPCHK(hipEventSynchronize(ev[4]));
+        for (int i = 0; i < 4; i++) { float ms = 0; HIPCHK(hipEventElapsedTime(&ms, ev[i], ev[i + 1])); acc[i] += ms * 1e3; }
+        if (++nacc % 200 == 0)
+            std::fprintf(stderr, "[aloam front phases] us per scan: scanRegistration %.1f, gap %.1f, odometry rounds %.1f, compose+grids %.1f (mean of %ld)\n",
+                         acc[0] / nacc, acc[1] / nacc, acc[2] / nacc, acc[3] / nacc, nacc);
+    }
+    HIPCHK(hipEventRecord(ev[k], C.stream));
+    if (k == 4) used = true;
+}
+
 static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     if (n < 0 || (n > 0 && !xyzr)) throw ApiError{ALOAM_E_ARG, "bad input"};
     if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "scan larger than max_scan_points"};
@@ -328,7 +348,9 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
         in = C.d_in;
     }
     prof_mark(C, 0);
+    if (g_front_phases) front_phase(C, 0);
     scan_registration_launch(C, in, n);
+    if (g_front_phases) front_phase(C, 1);
     prof_mark(C, 1);
     queue_meta(C);
     if (C.profiling) {
@@ -401,6 +423,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
             }
         };
         C.odom_spread_dirty = true;
+        if (g_front_phases) front_phase(C, 2);
         if (C.profiling || !C.use_graphs) {
             issue(true, hint);
         } else {   // two cached graphs: the last-cloud buffers alternate between scans
@@ -409,6 +432,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
                      : (C.graphs[0].exec ? 1 : 0);
             run_graph(C, slot, C.d_corner_last, C.d_surf_last, rounds, [&] { issue(false, hint); });
         }
+        if (g_front_phases) front_phase(C, 3);
         // pairs with build_last_grids(C, true) below; the new last-cloud counts from the device meta
         odom_compose(C, C.n_lsharp, C.n_lflat, pend ? C.d_meta->counts : nullptr);
         C.odom_spread_dirty = false;
@@ -421,6 +445,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     C.n_surf_last = C.n_lflat;
     if (!r.optimized) set_counts2(C, C.d_last_n, C.n_corner_last, C.n_surf_last);   // else set by k_odom_compose
     build_last_grids(C, r.optimized != 0);
+    if (g_front_phases && r.optimized) front_phase(C, 4);
     prof_mark(C, 3);
     const int skip = C.P.mapping_skip_frame > 0 ? C.P.mapping_skip_frame : 1;
     r.publish_to_mapping = (C.odom_frame_count % skip == 0);

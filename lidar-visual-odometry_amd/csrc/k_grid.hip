@@ -69,71 +69,64 @@ __device__ inline bool grid_include(int i, const int* cube_of, const unsigned ch
 
 
 
-// three-phase exclusive scan of cell_count[0, ncells) into cell_start
-constexpr int SCAN_CHUNK = 4096;
+// two-launch exclusive scan of cell_count[0, ncells) into cell_start: chunk sums, then per chunk the
+// sum of the preceding chunk sums + a local scan. 1024 threads x 16 consecutive cells per chunk (int4
+// loads), so an 8M-cell grid is 512 chunks and the chunk-sum prefix is one value per thread.
+constexpr int SCAN_T = 1024, SCAN_PER = 16, SCAN_CHUNK = SCAN_T * SCAN_PER;
+static_assert(GRID_MAX_CELLS / SCAN_CHUNK <= SCAN_T, "chunk sums: one per thread");
+__device__ __forceinline__ void load16(const int* __restrict__ cnt, int i0, int nc, int v[SCAN_PER]) {
+    if (i0 + SCAN_PER <= nc) {
+        const int4* q = (const int4*)(cnt + i0);
+#pragma unroll
+        for (int k = 0; k < SCAN_PER / 4; k++) { const int4 t = q[k]; v[4 * k] = t.x; v[4 * k + 1] = t.y; v[4 * k + 2] = t.z; v[4 * k + 3] = t.w; }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; k++) v[k] = i0 + k < nc ? cnt[i0 + k] : 0;
+    }
+}
 __device__ __forceinline__ void k_grid_scan1_body(const int* __restrict__ cnt, const GridDesc* d, int* blk) {
-    __shared__ int sh[GB / WAVE];
     const int nc = d->ncells;
     const int base = blockIdx.x * SCAN_CHUNK;
+    int v[SCAN_PER];
+    load16(cnt, base + threadIdx.x * SCAN_PER, nc, v);
     int s = 0;
-    if (base < nc)
-        for (int i = base + threadIdx.x; i < min(base + SCAN_CHUNK, nc); i += GB) s += cnt[i];
-    s = wave_sum_i(s);
-    if (lane_id() == 0) sh[threadIdx.x / WAVE] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < GB / WAVE; w++) t += sh[w]; blk[blockIdx.x] = t; }
-}
-__device__ __forceinline__ void k_grid_scan2_body(int* blk, const GridDesc* d) {
-    __shared__ int sh[1024];
-    const int nb = (d->ncells + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    // nb <= GRID_MAX_CELLS / SCAN_CHUNK = 2048: two entries per thread
-    const int i0 = 2 * threadIdx.x, i1 = i0 + 1;
-    const int v0 = i0 < nb ? blk[i0] : 0, v1 = i1 < nb ? blk[i1] : 0;
-    const int v = v0 + v1;
-    sh[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-        __syncthreads();
-        sh[threadIdx.x] += t;
-        __syncthreads();
-    }
-    const int ex = sh[threadIdx.x] - v;
-    if (i0 < nb) blk[i0] = ex;
-    if (i1 < nb) blk[i1] = ex + v0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) s += v[k];
+    int tot;
+    (void)block_exscan<SCAN_T, true>(s, &tot);
+    if (threadIdx.x == 0) blk[blockIdx.x] = tot;
 }
 __device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, const GridDesc* d, const int* blk, int* start) {
-    __shared__ int sh[SCAN_CHUNK];
     const int nc = d->ncells;
     const int base = blockIdx.x * SCAN_CHUNK;
-    if (base >= nc) return;
-    const int len = min(SCAN_CHUNK, nc - base);
-    // each thread scans 16 consecutive entries serially, then a block scan of the thread sums
-    const int per = SCAN_CHUNK / GB;
-    int loc[SCAN_CHUNK / GB];
+    const int i0 = base + threadIdx.x * SCAN_PER;
+    int v[SCAN_PER];
+    load16(cnt, i0, nc, v);
+    const int pre = threadIdx.x < (int)blockIdx.x ? blk[threadIdx.x] : 0;   // chunks before this one
     int s = 0;
-    for (int k = 0; k < per; k++) {
-        int i = threadIdx.x * per + k;
-        int v = i < len ? cnt[base + i] : 0;
-        loc[k] = s;
-        s += v;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) s += v[k];
+    int tot, ptot;
+    const int ex = block_exscan<SCAN_T, true>(s, &tot);
+    (void)block_exscan<SCAN_T, true>(pre, &ptot);
+    int run = ptot + ex;
+    if (i0 + SCAN_PER <= nc) {
+        int4* q = (int4*)(start + i0);
+#pragma unroll
+        for (int k = 0; k < SCAN_PER / 4; k++) {
+            int4 t;
+            t.x = run; run += v[4 * k];
+            t.y = run; run += v[4 * k + 1];
+            t.z = run; run += v[4 * k + 2];
+            t.w = run; run += v[4 * k + 3];
+            q[k] = t;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; k++) { if (i0 + k < nc) start[i0 + k] = run; run += v[k]; }
     }
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 1; o < GB; o <<= 1) {
-        int t = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-        __syncthreads();
-        sh[threadIdx.x] += t;
-        __syncthreads();
-    }
-    const int off = blk[blockIdx.x] + sh[threadIdx.x] - s;
-    for (int k = 0; k < per; k++) {
-        int i = threadIdx.x * per + k;
-        if (i < len) start[base + i] = off + loc[k];
-    }
-    if (base + len == nc && threadIdx.x == GB - 1) start[nc] = off + s;
+    if (base + SCAN_CHUNK >= nc && threadIdx.x == 0) start[nc] = ptot + tot;
 }
-
 
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_index, bool flat) {
     g.cap = cap;
@@ -229,16 +222,12 @@ __global__ void k_gm_count(GridJobs J) {
         if (c >= 0 && h == lane_id()) atomicAdd(&g.cell_count[c], len);
     }
 }
-__global__ void k_gm_scan1(GridJobs J) {
+__global__ void __launch_bounds__(SCAN_T) k_gm_scan1(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
     if (blockIdx.x * SCAN_CHUNK >= g.desc->ncells) return;
     k_grid_scan1_body(g.cell_count, g.desc, g.blk);
 }
-__global__ void k_gm_scan2(GridJobs J) {
-    const GridJob& g = J.j[blockIdx.y];
-    k_grid_scan2_body(g.blk, g.desc);
-}
-__global__ void k_gm_scan3(GridJobs J) {
+__global__ void __launch_bounds__(SCAN_T) k_gm_scan3(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
     if (blockIdx.x * SCAN_CHUNK >= g.desc->ncells) return;
     k_grid_scan3_body(g.cell_count, g.desc, g.blk, g.cell_start);
@@ -287,9 +276,8 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     const int nsb = GRID_MAX_CELLS / SCAN_CHUNK;
     k_gm_bbox<<<dim3(nb, nj), GB, 0, st>>>(J);
     k_gm_count<<<dim3(nb, nj), GB, 0, st>>>(J);
-    k_gm_scan1<<<dim3(nsb, nj), GB, 0, st>>>(J);
-    k_gm_scan2<<<dim3(1, nj), 1024, 0, st>>>(J);
-    k_gm_scan3<<<dim3(nsb, nj), GB, 0, st>>>(J);
+    k_gm_scan1<<<dim3(nsb, nj), SCAN_T, 0, st>>>(J);
+    k_gm_scan3<<<dim3(nsb, nj), SCAN_T, 0, st>>>(J);
     k_gm_scatter<<<dim3(nb, nj), GB, 0, st>>>(J);
     HIPCHK(hipGetLastError());
 }
