@@ -702,7 +702,7 @@ static void prepare_stacks(Ctx& C, int t) {
 
 // A hand-off into the other input set, on stream3 (after the frame that last read that set): one copy
 // launch for the clouds, counts and pose, `copied` recorded behind it, then the set's stacks.
-void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
+void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied, bool defer_stacks) {
     HIPCHK(hipSetDevice(C.device));
     if (s.n[0] > MAXL * LINE_LSHARP_CAP || s.n[1] > C.cap_in || s.n[2] > C.cap_in)
         throw ApiError{ALOAM_E_CAPACITY, "mapping input too large"};
@@ -728,7 +728,15 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
     j.pose_dst = m.pose;
     std::memcpy(j.pose, s.pose, sizeof(j.pose));
     int ncl = 3;
-    if (s.has_stacks) {               // stacks voxelised by the source (its stream2): copied with the clouds
+    m.pstk = false;
+    if (s.has_stacks && !side && defer_stacks) {   // stacks voxelised by the source (its stream2): copied
+        m.pstk = true;                // right before the rounds (forward_stacks_pending), the clouds and the
+                                      // pose now; `copied` is recorded then (mapping_issue of this set)
+        for (int k = 0; k < 2; k++) { m.pstk_src[k] = s.stk[k]; m.pstk_n[k] = s.n[k]; }
+        m.pstk_ndev = s.stk_n;
+        m.pstk_ready = s.stk_ready;
+        m.pstk_copied = copied;
+    } else if (s.has_stacks) {        // (copied with the clouds)
         HIPCHK(hipStreamWaitEvent(fs, s.stk_ready, 0));
         for (int k = 0; k < 2; k++) {
             j.src[3 + k] = s.stk[k];
@@ -742,13 +750,42 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied) {
     const int nmax = std::max(std::max(j.n[0], j.n[1]), j.n[2]);
     k_forward_map_input<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), ncl), 256, 0, fs>>>(j);
     HIPCHK(hipGetLastError());
-    if (copied) HIPCHK(hipEventRecord(copied, fs));
+    if (copied && !m.pstk) HIPCHK(hipEventRecord(copied, fs));
     m.stacks_pub = s.has_stacks;      // present in this set once `ready` (recorded behind the copy) fires
-    if (s.has_stacks) HIPCHK(hipEventRecord(m.ready, fs));
+    if (s.has_stacks && !m.pstk) HIPCHK(hipEventRecord(m.ready, fs));
     if (side && !s.has_stacks) prepare_stacks(C, t);
     else m.stacks = false;
     use_input_set(C, t);
     C.have_map_input = true;
+}
+
+__global__ void k_forward_stacks(ForwardJob j) {
+    const int c = 3 + blockIdx.y;
+    const int n = min(j.n[c], *j.ndev[c]);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) j.dst[c][i] = j.src[c][i];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) j.stack_counts[threadIdx.x] = min(j.n[3 + threadIdx.x], *j.ndev[3 + threadIdx.x]);
+}
+// the deferred stacks copy of input set t on the context's stream (then `copied`: the source may reuse
+// its set, and `ready`)
+void forward_stacks_pending(Ctx& C, int t) {
+    Ctx::MapInSet& m = C.mset[t];
+    if (!m.pstk) return;
+    hipStream_t st = C.stream;
+    HIPCHK(hipStreamWaitEvent(st, m.pstk_ready, 0));
+    ForwardJob j;
+    for (int k = 0; k < 2; k++) {
+        j.src[3 + k] = m.pstk_src[k];
+        j.dst[3 + k] = k ? m.sstack : m.cstack;
+        j.n[3 + k] = m.pstk_n[k];
+        j.ndev[3 + k] = m.pstk_ndev + k;
+    }
+    j.stack_counts = C.d_out->stack_n + 2 * t;
+    const int nmax = std::max(m.pstk_n[0], m.pstk_n[1]);
+    k_forward_stacks<<<dim3(std::max(1, std::min(1024, (nmax + 255) / 256)), 2), 256, 0, st>>>(j);
+    HIPCHK(hipGetLastError());
+    if (m.pstk_copied) HIPCHK(hipEventRecord(m.pstk_copied, st));
+    HIPCHK(hipEventRecord(m.ready, st));
+    m.pstk = false;
 }
 
 }  // namespace aloam

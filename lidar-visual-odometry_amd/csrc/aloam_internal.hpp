@@ -215,6 +215,13 @@ struct Ctx {
         hipEvent_t fwd = nullptr;          // stream: the publish copy into this set done (aloam_odometry
                                            // returns before it ends)
         bool fwd_rec = false;              // `fwd` has been recorded for the set's current contents
+        // a hand-off's stacks copy deferred to just before the frame's rounds (forward_snapshot): the
+        // prepare and grid builds need only the clouds and the pose, so they overlap the source's stacks
+        bool pstk = false;
+        const float4* pstk_src[2] = {nullptr, nullptr};
+        int pstk_n[2] = {0, 0};
+        const int* pstk_ndev = nullptr;
+        hipEvent_t pstk_ready = nullptr, pstk_copied = nullptr;
     };
     MapInSet mset[2];
     int in_cur = 0;
@@ -306,6 +313,7 @@ void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float ra
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
 void rebuild_init(Ctx& C);
+void forward_stacks_pending(Ctx& C, int t);
 void set_counts2(Ctx& C, int* dst, int a, int b);
 // also sets d_last_n (from dcnt[2], dcnt[4] when dcnt = the device ScanMeta counts, else the host values)
 // and re-arms d_last_sorted
@@ -343,7 +351,7 @@ struct MapSnapshot {
     hipEvent_t fwd_done = nullptr;     // source stream: the publish copy into src[] done
 };
 void snapshot_mapping_input(Ctx& S, MapSnapshot* out);
-void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied);
+void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied, bool defer_stacks = false);
 // laserMapping split in two so the host can issue frame k while the GPU still runs frame k-1 (at most
 // two frames in flight; every launch size of frame k is an upper bound known before k-1 completes)
 void mapping_issue(Ctx& C);

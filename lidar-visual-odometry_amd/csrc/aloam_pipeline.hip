@@ -190,12 +190,14 @@ void map_server(aloam_pipeline* P) {
         std::string e;
         double t1 = 0, t2 = 0;
         if (g_pipe_timing) { t1 = now_us(); S.t_idle += t1 - ti; }
-        int rc = guarded([&] { aloam::forward_snapshot(B, S.snap[i], S.copied[i]); }, e);
-        S.issued.store(j + 1, std::memory_order_release);
+        // the hand-off's stacks are copied inside mapping_issue, right before the rounds (after the
+        // prepare and grid builds), and `copied` is recorded there: `issued` follows the issue
+        int rc = guarded([&] { aloam::forward_snapshot(B, S.snap[i], S.copied[i], true); }, e);
         if (g_pipe_timing) { t2 = now_us(); S.t_fwd += t2 - t1; }
         // a frame that has already finished is handed back before the ~0.5 ms of launch issue below
         if (inflight >= 0 && aloam::mapping_ready(B)) { complete(inflight); inflight = -1; }
         if (!rc) rc = guarded([&] { aloam::mapping_issue(B); }, e);
+        S.issued.store(j + 1, std::memory_order_release);
         if (g_pipe_timing) { S.t_issue += now_us() - t2; S.n_srv++; }
         if (inflight >= 0) { complete(inflight); inflight = -1; }
         if (rc) {

@@ -1288,7 +1288,8 @@ void map_frame_launch(Ctx& C, int X) {
     const int ub_c = in.nc, ub_s = in.ns;
     // an input set written on another stream (stream3 hand-off, or this context's stream2 stacks): its
     // clouds, pose and stacks are complete at `ready` — wait before the first kernel that reads the pose
-    if (in.stacks_pub || in.stacks) HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
+    const bool deferred = in.pstk;   // stacks copied right before the rounds (forward_stacks_pending)
+    if (in.stacks || (in.stacks_pub && !deferred)) HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
     if (g_map_phases) map_phase(C, 0);
     k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_map_spread, voxel_hdr(C, 0), voxel_hdr(C, 1),
                                      in.pose);
@@ -1298,7 +1299,9 @@ void map_frame_launch(Ctx& C, int X) {
     grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
     // stacks (:542-550): voxelised on stream3 when the input came as a hand-off, else here in two lanes
-    if (in.stacks_pub) {
+    if (deferred) {
+        forward_stacks_pending(C, X);
+    } else if (in.stacks_pub) {
         // present already: voxelised at this context's own publish (stream2), or at the source's and
         // copied in (this stream or stream3); `ready` is recorded behind either
         HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
