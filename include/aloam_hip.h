@@ -266,11 +266,13 @@ const char*     aloam_pipeline_last_error(const aloam_pipeline* pl);
 aloam_ctx*      aloam_pipeline_context(aloam_pipeline* pl, int stage);
 /* Feeds one sweep (flags as aloam_scan_registration). Outputs the odometry result completed in this
  * step (*have_od: scan k for stages 2, k-1 for stages 3) and the mapping result completed in it
- * (*have_mp: scan k-1 / k-2). od / mp may be NULL. */
+ * (*have_mp: scan k-2 for stages 2 — k-1 with ALOAM_PIPE_LAG=1 or profiling on —, k-2 for stages 3).
+ * od / mp may be NULL. */
 int aloam_pipeline_push(aloam_pipeline* pl, const float* xyzr, int n, int flags,
                         aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp);
 /* Drains the pipeline: the odometry result still in flight (stages 3), the mapping job in flight
- * (mp) and the mapping of that last odometry result (mp2). */
+ * (mp) and the mapping of that last odometry result (mp2); stages 2: the (up to two) mapping results
+ * still in flight, oldest in mp. */
 int aloam_pipeline_flush(aloam_pipeline* pl, aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp,
                          aloam_map_result* mp2, int* have_mp2);
 /* HIP-event timing of each stage's last completed job (profiling on). */

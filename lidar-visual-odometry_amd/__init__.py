@@ -454,6 +454,8 @@ class Pipeline:
             out.append((None, abi.map_to_dict(mp)))
         if ho.value:
             out.append((abi.odom_to_dict(od), abi.map_to_dict(mp2) if hm2.value else None))
+        elif hm2.value:                  # 2 stages: the second mapping result still in flight
+            out.append((None, abi.map_to_dict(mp2)))
         return out
 
     def close(self):

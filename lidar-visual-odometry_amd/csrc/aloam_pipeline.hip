@@ -98,12 +98,18 @@ struct MapServer {
     std::mutex m;
     std::condition_variable cv;
     aloam::MapSnapshot snap[2];
-    aloam_map_result res[2];
-    aloam_timing tim[2];
-    int rc[2] = {0, 0};
-    std::string err[2];
+    static constexpr int NRES = 4;               // result slots (index j % NRES): up to lag + 2 outstanding
+    aloam_map_result res[NRES];
+    aloam_timing tim[NRES];
+    int rc[NRES] = {0, 0, 0, 0};
+    std::string err[NRES];
     hipEvent_t copied[2] = {nullptr, nullptr};   // after the copy of hand-off j (index j & 1)
     long returned = 0;                           // results handed to the caller
+    // result lag of aloam_pipeline_push: mapping result k-lag is returned at scan k. lag 1 makes the front
+    // wait for mapping k-1 before it starts scan k+1, so the two stages alternate their host latencies
+    // (hand-off, issue, completion) on one critical path; lag 2 lets the front run one scan further
+    // ahead. ALOAM_PIPE_LAG (1 or 2, default 2); profiling runs one frame at a time (lag 1).
+    int lag = 2;
     // ALOAM_PIPE_TIMING (profiling aid): host-side stage occupancy, printed at destroy
     double t_fwd = 0, t_issue = 0, t_complete = 0, t_idle = 0, t_front = 0, t_take = 0;
     long n_srv = 0, n_front = 0;
@@ -167,7 +173,7 @@ void map_server(aloam_pipeline* P) {
     aloam::Ctx& B = *(aloam::Ctx*)P->back;
     long inflight = -1;
     auto complete = [&](long j) {
-        const int i = (int)(j & 1);
+        const int i = (int)(j % MapServer::NRES);
         const double t0 = g_pipe_timing ? now_us() : 0;
         const int rc = guarded([&] { aloam::mapping_complete(B, &S.res[i]); }, S.err[i]);
         if (g_pipe_timing) S.t_complete += now_us() - t0;
@@ -186,13 +192,13 @@ void map_server(aloam_pipeline* P) {
             S.cv.wait(lk, [&] { return S.posted.load(std::memory_order_acquire) > j || S.quit.load(std::memory_order_acquire); });
             spins = 0;
         }
-        const int i = (int)(j & 1);
+        const int i = (int)(j % MapServer::NRES);
         std::string e;
         double t1 = 0, t2 = 0;
         if (g_pipe_timing) { t1 = now_us(); S.t_idle += t1 - ti; }
         // the hand-off's stacks are copied inside mapping_issue, right before the rounds (after the
         // prepare and grid builds), and `copied` is recorded there: `issued` follows the issue
-        int rc = guarded([&] { aloam::forward_snapshot(B, S.snap[i], S.copied[i], true); }, e);
+        int rc = guarded([&] { aloam::forward_snapshot(B, S.snap[j & 1], S.copied[j & 1], true); }, e);
         if (g_pipe_timing) { t2 = now_us(); S.t_fwd += t2 - t1; }
         // a frame that has already finished is handed back before the ~0.5 ms of launch issue below
         if (inflight >= 0 && aloam::mapping_ready(B)) { complete(inflight); inflight = -1; }
@@ -217,7 +223,7 @@ int take_result(aloam_pipeline* P, aloam_map_result* mp, int* have) {
     MapServer& S = P->ms;
     const long j = S.returned;
     while (S.done.load(std::memory_order_acquire) <= j) std::this_thread::yield();
-    const int i = (int)(j & 1);
+    const int i = (int)(j % MapServer::NRES);
     S.returned = j + 1;
     if (S.rc[i]) { P->err = S.err[i]; return S.rc[i]; }
     *have = 1;
@@ -296,6 +302,8 @@ aloam_pipeline* aloam_pipeline_create(const aloam_params* p, int device, int sta
         }
     }
     if (stages == 2) {
+        const char* lenv = std::getenv("ALOAM_PIPE_LAG");
+        P->ms.lag = lenv && std::atoi(lenv) == 1 ? 1 : 2;
         // the front voxelises the mapping stacks of each publish on its stream2 (ALOAM_PIPE_FRONT_STACKS=0: off)
         const char* fsenv = std::getenv("ALOAM_PIPE_FRONT_STACKS");
         ((aloam::Ctx*)P->front)->publish_stacks = !fsenv || std::atoi(fsenv) != 0;
@@ -380,7 +388,7 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
             }
             if (e != hipSuccess) {
                 P->err = std::string("hipStreamWaitEvent failed: ") + hipGetErrorName(e) + " (hand-off " +
-                         std::to_string(seq - 2) + ", server rc " + std::to_string(S.rc[seq & 1]) + " " + S.err[seq & 1] + ")";
+                         std::to_string(seq - 2) + ", server rc " + std::to_string(S.rc[(seq - 2) % MapServer::NRES]) + " " + S.err[(seq - 2) % MapServer::NRES] + ")";
                 return ALOAM_E_HIP;
             }
         }
@@ -407,8 +415,9 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
             S.cv.notify_one();
             posted = true;
         }
-        // the previous scan's mapping result (the job before the one just posted)
-        if (S.returned < S.posted.load(std::memory_order_relaxed) - (posted ? 1 : 0)) {
+        // mapping result k - lag (the lag-th job before the one just posted)
+        const int lag = P->profiling ? 1 : S.lag;
+        if (S.posted.load(std::memory_order_relaxed) - S.returned > (posted ? lag : lag - 1)) {
             const double tt0 = g_pipe_timing ? now_us() : 0;
             const int trc = take_result(P, mp, have_mp);
             if (g_pipe_timing) S.t_take += now_us() - tt0;
@@ -441,8 +450,9 @@ int aloam_pipeline_flush(aloam_pipeline* P, aloam_odom_result* od, int* have_od,
     if (!P || !have_od || !have_mp || !have_mp2) return ALOAM_E_ARG;
     *have_od = *have_mp = *have_mp2 = 0;
     int rc;
-    if (P->stages == 2) {
-        if (P->ms.returned < P->ms.posted.load(std::memory_order_relaxed)) return take_result(P, mp, have_mp);
+    if (P->stages == 2) {             // up to two results in flight (lag 2): the older into mp, the newer into mp2
+        if (P->ms.returned < P->ms.posted.load(std::memory_order_relaxed) && (rc = take_result(P, mp, have_mp))) return rc;
+        if (P->ms.returned < P->ms.posted.load(std::memory_order_relaxed)) return take_result(P, mp2, have_mp2);
         return ALOAM_OK;
     }
     const int orc = P->wo.join();

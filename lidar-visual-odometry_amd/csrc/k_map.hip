@@ -1266,16 +1266,20 @@ static const bool g_map_phases = getenv("ALOAM_MAP_PHASES") != nullptr;
 static void map_phase(Ctx& C, int k) {
     static hipEvent_t ev[2][5];
     static bool made = false, used[2] = {false, false};
-    static double acc[4] = {0, 0, 0, 0};
+    static double acc[5] = {0, 0, 0, 0, 0};
     static long frame = 0, nacc = 0;
     if (!made) { for (auto& r : ev) for (auto& e : r) HIPCHK(hipEventCreate(&e)); made = true; }
     const int s = (int)(frame & 1);
-    if (k == 0 && used[s]) {
+    if (k == 0 && used[s] && used[s ^ 1]) {
         HIPCHK(hipEventSynchronize(ev[s][4]));
         for (int i = 0; i < 4; i++) { float ms = 0; HIPCHK(hipEventElapsedTime(&ms, ev[s][i], ev[s][i + 1])); acc[i] += ms * 1e3; }
+        float gap = 0;                   // the next frame's start - this frame's end (stream idle)
+        HIPCHK(hipEventSynchronize(ev[s ^ 1][0]));
+        HIPCHK(hipEventElapsedTime(&gap, ev[s][4], ev[s ^ 1][0]));
+        acc[4] += gap * 1e3;
         if (++nacc % 200 == 0)
-            std::fprintf(stderr, "[aloam map phases] us per frame: prepare+grids %.1f, rounds %.1f, rebuild %.1f, register %.1f (mean of %ld)\n",
-                         acc[0] / nacc, acc[1] / nacc, acc[2] / nacc, acc[3] / nacc, nacc);
+            std::fprintf(stderr, "[aloam map phases] us per frame: prepare+grids %.1f, rounds %.1f, rebuild %.1f, register %.1f, idle before %.1f (mean of %ld)\n",
+                         acc[0] / nacc, acc[1] / nacc, acc[2] / nacc, acc[3] / nacc, acc[4] / nacc, nacc);
     }
     HIPCHK(hipEventRecord(ev[s][k], C.stream));
     if (k == 4) { used[s] = true; frame++; }
