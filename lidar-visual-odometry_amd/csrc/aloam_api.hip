@@ -36,6 +36,27 @@ void prof_mark(Ctx& C, int idx) {
 }
 
 __global__ void k_set2(int* dst, int a, int b) { dst[0] = a; dst[1] = b; }
+
+// Small results block device -> pinned host memory: one workgroup storing straight into the mapped
+// buffer (host-coherent, visible at the stream's completion) instead of hipMemcpyAsync, whose copy
+// engine / blit launch adds ~10-20 us to the stream for a few KB. ALOAM_D2H_COPY=1: hipMemcpyAsync.
+__global__ void k_to_host(const unsigned* __restrict__ src, unsigned* __restrict__ dst, int nwords) {
+    const bool al = (((size_t)src | (size_t)dst) & 15) == 0;
+    const int n4 = al ? nwords / 4 : 0;
+    const uint4* s4 = (const uint4*)src;
+    uint4* d4 = (uint4*)dst;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+    for (int i = 4 * n4 + threadIdx.x; i < nwords; i += blockDim.x) dst[i] = src[i];
+}
+static const bool g_d2h_copy = getenv("ALOAM_D2H_COPY") && atoi(getenv("ALOAM_D2H_COPY")) == 1;
+static void d2h_small(void* host_mapped, const void* dev, size_t bytes, hipStream_t st) {
+    static_assert(sizeof(DevOut) % 4 == 0 && sizeof(ScanMeta) % 4 == 0 && offsetof(DevOut, map_n) % 4 == 0, "word copies");
+    if (g_d2h_copy) { HIPCHK(hipMemcpyAsync(host_mapped, dev, bytes, hipMemcpyDeviceToHost, st)); return; }
+    void* dptr = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dptr, host_mapped, 0));
+    k_to_host<<<1, 256, 0, st>>>((const unsigned*)dev, (unsigned*)dptr, (int)(bytes / 4));
+    HIPCHK(hipGetLastError());
+}
 void set_counts2(Ctx& C, int* dst, int a, int b) { k_set2<<<1, 1, 0, C.stream>>>(dst, a, b); }
 struct Vec7 { double v[7]; };
 // clouds 0-2: corner, surf, full (host counts n); 3-4 (optional): the VoxelGrid'ed corner / surf stacks,
@@ -109,9 +130,9 @@ static void allocate(Ctx& C) {
     C.d_flat_idx = (int*)dalloc(C, sizeof(int) * capF);
     // odometry
     C.d_out = (DevOut*)dalloc(C, sizeof(DevOut));
-    HIPCHK(hipHostMalloc((void**)&C.h_out, sizeof(DevOut), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&C.h_out, sizeof(DevOut), hipHostMallocMapped));
     std::memset(C.h_out, 0, sizeof(DevOut));
-    HIPCHK(hipHostMalloc((void**)&C.h_mout[0], 2 * sizeof(DevOut), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&C.h_mout[0], 2 * sizeof(DevOut), hipHostMallocMapped));
     std::memset(C.h_mout[0], 0, 2 * sizeof(DevOut));
     C.h_mout[1] = C.h_mout[0] + 1;
     C.d_odom = &C.d_out->odom;
@@ -227,7 +248,7 @@ static void allocate(Ctx& C) {
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
-    HIPCHK(hipHostMalloc((void**)&C.h_meta_pin, sizeof(ScanMeta), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&C.h_meta_pin, sizeof(ScanMeta), hipHostMallocMapped));
     std::memset(C.h_meta_pin, 0, sizeof(ScanMeta));
     for (auto& e : C.ev_mdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
@@ -287,7 +308,7 @@ static float ev_ms(Ctx& C, int a, int b) {
 // scanRegistration's counts reach the host without a sync of their own: the copy is queued behind the
 // registration kernels and read at the next sync of the stream (ensure_meta, or the odometry's result sync)
 static void queue_meta(Ctx& C) {
-    HIPCHK(hipMemcpyAsync(C.h_meta_pin, C.d_meta, sizeof(ScanMeta), hipMemcpyDeviceToHost, C.stream));
+    d2h_small(C.h_meta_pin, C.d_meta, sizeof(ScanMeta), C.stream);
     C.meta_pending = true;
 }
 static void apply_meta(Ctx& C) {   // the stream has been synchronised since queue_meta
@@ -498,7 +519,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
     }
     // results: odom state, round counts and LM summaries in one copy into the pinned mirror (+ the
     // scan's counts, queued behind scanRegistration): the scan's one sync
-    HIPCHK(hipMemcpyAsync(C.h_out, C.d_out, offsetof(DevOut, map_n), hipMemcpyDeviceToHost, st));
+    d2h_small(C.h_out, C.d_out, offsetof(DevOut, map_n), st);
     sync(C);
     if (pend) {
         apply_meta(C);
@@ -559,7 +580,7 @@ void mapping_issue(Ctx& C) {
     C.t_pre_us = std::chrono::duration<double, std::micro>(C.t_rounds_issued - th0).count();
     prof_mark(C, 5);
     // map state, counts, summaries, sizes: one copy of the results block into this frame's pinned mirror
-    HIPCHK(hipMemcpyAsync(C.h_mout[slot], C.d_out, sizeof(DevOut), hipMemcpyDeviceToHost, st));
+    d2h_small(C.h_mout[slot], C.d_out, sizeof(DevOut), st);
     HIPCHK(hipEventRecord(C.ev_mdone[slot], st));
     HIPCHK(hipEventRecord(in.released, st));   // the input set may be written again (stream3 waits on this)
     C.m_set[slot] = X;
