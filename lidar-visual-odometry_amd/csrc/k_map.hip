@@ -733,7 +733,7 @@ template <bool FITS> __device__ __forceinline__ void rbv_bar() { if (FITS) lds_b
 
 template <bool FITS>
 __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n, int n_o,
-                                         float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr) {
+                                         float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr, const int* fb) {
     RbvShared& SH = *(RbvShared*)smem;
     unsigned long long* nk = (unsigned long long*)(smem + 256);
     unsigned long long* nk2 = nk + RBV_NCAP;               // merge sort ping-pong
@@ -751,6 +751,42 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
         const int t = threadIdx.x + u * RBV_T;
         pt[u] = t < n ? B[p0 + t] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    const float inv = 1.0f / leaf;
+    unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, order, bitonic (2n)
+    unsigned* keys = FITS ? lkeys : (unsigned*)gseg;      // compile-time choice: ds_* or global, never flat
+    int* gorder = (int*)(gseg + (n + 1) / 2);
+    int minb[3], mul1, mul2;
+    // Leaf keys without the bbox (fb != null): the cube's points lie in its 50 m box, so leaf indices
+    // taken from a fixed base below the box, 10 bits per axis, order exactly like PCL's (k, j, i)-linear
+    // index over the bbox grid and are equal exactly when PCL's are (PCL's int-overflow pass-through
+    // cannot occur with under 1024 leaves per axis). A key out of range falls back to the bbox path.
+    bool slow = fb == nullptr;
+    if (!slow) {
+        for (int d = 0; d < 3; d++) minb[d] = fb[d];
+        mul1 = 1024; mul2 = 1 << 20;
+        bool bad = false;
+        auto fast_key = [&](float4 p) {
+            const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+            const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+            const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+            bad |= (unsigned)i0 >= 1024u || (unsigned)i1 >= 1024u || (unsigned)i2 >= 1024u;
+            return (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+        };
+#pragma unroll
+        for (int u = 0; u < RBV_PER; u++) {
+            const int t = threadIdx.x + u * RBV_T;
+            if (t < n) keys[t] = fast_key(pt[u]);
+        }
+        for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) keys[t] = fast_key(B[p0 + t]);
+        if (__ballot(bad) && lane_id() == 0) SH.unsorted = 2;
+        rbv_bar<FITS>();
+        slow = SH.unsorted == 2;
+        if (slow) {
+            lds_barrier();
+            if (threadIdx.x == 0) SH.unsorted = 0;
+        }
+    }
+    if (slow) {
     {   // bbox (ordered-int encoding)
         unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
 #pragma unroll
@@ -773,19 +809,13 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
         }
     }
     lds_barrier();
-    RBSTAMP(1);
     bool ovf;
-    int minb[3], mul1, mul2;
     voxel_params(SH.bb, leaf, &ovf, minb, &mul1, &mul2);    // same bbox -> leaf grid as k_voxel.hip
     if (ovf) {                            // PCL's int overflow: pass-through (every point its own leaf)
         for (int t = threadIdx.x; t < n; t += RBV_T) Cf[p0 + t] = B[p0 + t];
         if (threadIdx.x == 0) a.seg_nout[c] = n;
         return;
     }
-    const float inv = 1.0f / leaf;
-    unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, order, bitonic (2n)
-    unsigned* keys = FITS ? lkeys : (unsigned*)gseg;      // compile-time choice: ds_* or global, never flat
-    int* gorder = (int*)(gseg + (n + 1) / 2);
 #pragma unroll
     for (int u = 0; u < RBV_PER; u++) {
         const int t = threadIdx.x + u * RBV_T;
@@ -793,6 +823,8 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     }
     for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) keys[t] = voxel_index(B[p0 + t], inv, minb, mul1, mul2);
     rbv_bar<FITS>();
+    }
+    RBSTAMP(1);
     for (int t = threadIdx.x; t + 1 < n_o; t += RBV_T)
         if (keys[t] > keys[t + 1]) SH.unsorted = 1;
     rbv_bar<FITS>();
@@ -925,6 +957,7 @@ struct RbKind {
     float4* ins_pts; unsigned* k1; int* v2;               // appended points in the map frame, cube keys, ranks
     float4* Cf; unsigned long long* gscr;                 // per-cube VoxelGrid output / global scratch
     CubeArrays a;
+    int fast_keys;                                        // leaf keys from the cube box (< 1024 leaves per axis)
 };
 struct RbKinds { RbKind k[2]; };
 
@@ -1078,8 +1111,16 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
     const int p0 = a.off[c], n = a.off[c + 1] - p0;
     if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
     const int n_o = old_count(a, c);
-    if (n <= RBV_CAP) rbv_cube<true>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr);
-    else rbv_cube<false>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr);
+    int fbv[3];
+    const int* fb = nullptr;
+    if (K.fast_keys) {                    // leaf base below the cube's box (cube_coord: x in [50 (ci - cen) - 25, +50])
+        const int cc[3] = {c % CUBE_W, (c / CUBE_W) % CUBE_H, c / (CUBE_W * CUBE_H)}, cen[3] = {m->cenW, m->cenH, m->cenD};
+        const float inv = 1.0f / K.leaf;
+        for (int d = 0; d < 3; d++) fbv[d] = (int)floorf((float)(50.0 * (cc[d] - cen[d]) - 26.0) * inv);
+        fb = fbv;
+    }
+    if (n <= RBV_CAP) rbv_cube<true>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr, fb);
+    else rbv_cube<false>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr, fb);
 }
 
 __global__ void __launch_bounds__(1024) k_rb_final_scan(RbKinds P, const unsigned char* __restrict__ valid) {
@@ -1167,6 +1208,8 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
         k.Cf = K.map_tmp;
         k.gscr = K.seg_keys + 32768;
         k.a = cube_arrays(C, w);
+        static const bool bbox_keys = getenv("ALOAM_RB_BBOX") && atoi(getenv("ALOAM_RB_BBOX")) == 1;   // A/B knob
+        k.fast_keys = !bbox_keys && k.leaf > 0.f && 53.0 / k.leaf + 2.0 < 1024.0;
     }
     const int n_old = std::max(C.n_mc, C.n_ms), ub = std::max(ub_c, ub_s);
     k_rb_insert<<<dim3(nblk(std::max(n_old, ub)), 2), MB, 0, st>>>(P, C.d_map);
