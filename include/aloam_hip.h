@@ -225,7 +225,9 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
               float radius, int* idx, float* d2);
 /* The same search on device-resident data (~240k queries against a ~2M-point
  * local map): d_pts / d_queries are device float4 (x, y, z, w) arrays, d_idx / d_d2 device arrays
- * of nq * k; the index is built in context memory grown on demand. Synchronous. */
+ * of nq * k; the index is built in context memory grown on demand. Synchronous. Two-phase: a fine
+ * grid's 3x3x3 block first (exact when the k-th neighbour is closer than 0.99 fine cells), the
+ * radius-edge block for the rest; ALOAM_KNN_FINE = fine cell / radius (default 0.3; 0 = one phase). */
 int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k,
                      float radius, int* d_idx, float* d_d2);
 
@@ -243,6 +245,7 @@ typedef struct aloam_timing {
     float knn_ms;             /* aloam_knn_device: search kernel time (HIP events)              */
     int   knn_launches;
     double knn_bytes;         /* its algorithmic bytes: sum_q (16 + 16 |C27(q)|) + 8 k Q         */
+    double knn_streamed_bytes;/* bytes it actually streamed (both phases of the two-phase search)   */
 } aloam_timing;
 int aloam_set_profiling(aloam_ctx* ctx, int enable);
 int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);

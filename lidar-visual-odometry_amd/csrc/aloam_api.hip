@@ -1255,24 +1255,49 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
         C.g_knn = g;
     }
     C.g_knn.min_cell = radius * 1.025f;           // cells >= radius: the 27-cell block holds the ball
-    set_counts2(C, C.d_knn_n, n, 0);
-    grid_build(C, C.g_knn, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr);
-    if (C.profiling) {
-        HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long), C.stream));
-        HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 2], C.stream));
+    const char* fe = getenv("ALOAM_KNN_FINE");    // read per call (tests compare both paths in one process)
+    const float fine_frac = fe ? (float)atof(fe) : 0.3f;
+    const bool two_phase = fine_frac > 0.f && fine_frac < 1.f;
+    if (two_phase && C.g_knn_fine.cap < std::max(n, 1)) {
+        Grid g{};
+        grid_alloc(C, g, std::max(std::max(n, 1), C.g_knn_fine.cap * 2), radius * fine_frac, 1, true);
+        C.g_knn_fine = g;
     }
-    knn_device_launch(C, C.g_knn, (const float4*)d_queries, nq, k, radius, d_idx, d_d2, C.profiling ? C.d_cand : nullptr);
-    unsigned long long cand = 0;
+    set_counts2(C, C.d_knn_n, n, 0);
+    if (two_phase) {
+        C.g_knn_fine.min_cell = radius * fine_frac;
+        const GridBuild b[2] = {{&C.g_knn, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr},
+                                {&C.g_knn_fine, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr}};
+        grid_build_multi(C, b, 2);
+    } else {
+        grid_build(C, C.g_knn, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr);
+    }
+    // profiling: the timed launch runs without candidate counters (one same-address atomic per wave
+    // would be on the measured path); an untimed second launch (identical results) counts them
+    auto launch = [&](unsigned long long* cnt) {
+        if (two_phase)
+            knn_device_2phase_launch(C, C.g_knn_fine, C.g_knn, (const float4*)d_queries, nq, k, radius, d_idx, d_d2, cnt);
+        else
+            knn_device_launch(C, C.g_knn, (const float4*)d_queries, nq, k, radius, d_idx, d_d2, cnt);
+    };
+    if (C.profiling) HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 2], C.stream));
+    launch(nullptr);
     if (C.profiling) {
         HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 1], C.stream));
-        HIPCHK(hipMemcpyAsync(&cand, C.d_cand, sizeof(cand), hipMemcpyDeviceToHost, C.stream));
+        HIPCHK(hipMemsetAsync(C.d_cand, 0, sizeof(unsigned long long) * 2, C.stream));
+        launch(C.d_cand);
+    }
+    unsigned long long cand[2] = {0, 0};
+    if (C.profiling) {
+        HIPCHK(hipMemcpyAsync(cand, C.d_cand, sizeof(cand), hipMemcpyDeviceToHost, C.stream));
     }
     sync(C);
     if (C.profiling) {
         C.timing.knn_ms = ev_ms(C, Ctx::NEV - 2, Ctx::NEV - 1);
         C.timing.knn_launches = 1;
         // B = sum_q [16 + 16 |C27(q)|] + 8 k Q
-        C.timing.knn_bytes = 16.0 * nq + 16.0 * (double)cand + 8.0 * k * (double)nq;
+        C.timing.knn_bytes = 16.0 * nq + 16.0 * (double)cand[0] + 8.0 * k * (double)nq;
+        C.timing.knn_streamed_bytes = 16.0 * nq + 16.0 * (double)cand[1] + 8.0 * k * (double)nq;
     }
     API_END
 }

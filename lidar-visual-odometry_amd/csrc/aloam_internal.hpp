@@ -167,7 +167,8 @@ struct Ctx {
     Grid g_corner_last, g_surf_last;
     Grid g_corner_win, g_surf_win;  // scan-line-layered grids of the last clouds (window search)
     Grid g_corner_fine, g_surf_fine;  // fine grids of the last clouds (first 1-NN phase, k_odom.hip)
-    Grid g_knn;                     // aloam_knn_device (grown on demand)
+    Grid g_knn;                     // aloam_knn_device (grown on demand): radius-edge cells
+    Grid g_knn_fine;                // its fine grid (first search phase, k_knn_2phase)
     int* d_knn_n = nullptr;
     aloam_factor* d_factors = nullptr;
     int cap_factors = 0;
@@ -310,6 +311,8 @@ constexpr int GRID_MULTI_MAX = 6;
 void grid_build_multi(Ctx& C, const GridBuild* b, int n);   // up to GRID_MULTI_MAX grids in one set of launches
 void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2,
                        unsigned long long* cand);
+void knn_device_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int nq, int k, float radius, int* idx, float* d2,
+                              unsigned long long* cand);
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
 void rebuild_init(Ctx& C);

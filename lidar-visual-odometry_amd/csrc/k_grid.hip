@@ -304,7 +304,7 @@ __global__ void k_knn(const GridDesc* __restrict__ gdp, const int* __restrict__ 
 
 // Large searches (aloam_knn_device, C4): a GS-lane group per query (group_knn27 in
 // aloam_device.hpp) over the radius-edge grid; candidates counted per wave when profiling.
-template <int K, int GS>
+template <int K, int GS, bool CNT>
 __global__ void __launch_bounds__(256) k_knn_group(const GridDesc* __restrict__ gdp, const int* __restrict__ start,
                                                    const float4* __restrict__ spts, const int* __restrict__ sidx,
                                                    const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
@@ -330,18 +330,120 @@ __global__ void __launch_bounds__(256) k_knn_group(const GridDesc* __restrict__ 
                 d2[(size_t)qi * k + j] = j < f ? od[j] : INFINITY;
             }
     }
-    if (cand) {
+    if (CNT) {
         const int t = wave_sum_i(live && gl == 0 ? nc : 0);
-        if (lane_id() == 0 && t) atomicAdd(cand, (unsigned long long)t);
+        if (lane_id() == 0 && t) { atomicAdd(&cand[0], (unsigned long long)t); atomicAdd(&cand[1], (unsigned long long)t); }
     }
+}
+
+// Points of the 3x3x3 cell block around q (the 9 row ranges' lengths; nothing streamed): C27(q) of the
+// roofline's algorithmic bytes when the search itself does not visit that block.
+__device__ __forceinline__ int block27_total(const GridDesc& gd, const int* __restrict__ start, float qx, float qy, float qz) {
+    const int cx = (int)floorf((qx - gd.ox) * gd.inv_cell), cy = (int)floorf((qy - gd.oy) * gd.inv_cell),
+              cz = (int)floorf((qz - gd.oz) * gd.inv_cell);
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gd.dx - 1);
+    int t = 0;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
+        const bool ok = x0 <= x1 && y >= 0 && y < gd.dy && z >= 0 && z < gd.dz;
+        const int c = (z * gd.dy + y) * gd.dx;
+        t += load_or(start, c + x1 + 1, ok, 0) - load_or(start, c + x0, ok, 0);
+    }
+    return t;
+}
+
+// Two-phase exact radius k-NN (aloam_knn_device's default). Phase 1: the 3x3x3 block of a fine grid
+// (cell f < r). The block holds every point within f of q (q lies inside its centre cell), so when the
+// k-th neighbour found there is closer than 0.99 f, no point outside the block can precede it — the
+// result is the exact radius-r k-NN in the same (d2, index) order, ties included. Phase 2 (only groups
+// phase 1 did not settle): the radius-edge grid's 27-cell block, which holds the whole r-ball. On a
+// dense map (C4: the 5 neighbours within ~0.15 m, ~1000 points in the coarse block) phase 1 streams
+// ~10x fewer candidates. cand (profiling): [0] += C27(q) of the coarse block (SURVEY §8(d)'s
+// algorithmic count), [1] += candidates actually streamed by both phases.
+template <int K, int GS, bool CNT>
+__global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
+                                                    const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
+                                                    const int* __restrict__ cstart, const float4* __restrict__ cpts,
+                                                    const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
+                                                    float* __restrict__ d2, unsigned long long* cand) {
+    __shared__ int tabs[256 / GS][20];
+    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+    const bool live = qi < nq;
+    if (!__ballot(live)) return;
+    const float4 qq = q[live ? qi : 0];
+    int pos[K], oi[K], nf = 0, nc = 0;
+    float od[K];
+    const GridDesc gf = *fgd;
+    int f = group_knn27<K, GS, true>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, nullptr,
+                                     qq.x, qq.y, qq.z, r2, live, pos, od, oi, &nf, tabs[threadIdx.x / GS], gf.n);
+    float dk = INFINITY;
+#pragma unroll
+    for (int j = 0; j < K; j++) if (j == k - 1) dk = od[j];
+    const float lim = 0.99f * gf.cell;
+    const bool need = live && !(f >= k && dk < lim * lim);
+    const GridDesc gc = *cgd;
+    if (__any(need)) {                         // wave-uniform: every lane takes part in the group search
+        int p2[K], i2[K];
+        float e2[K];
+        const int f2 = group_knn27<K, GS, true>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, nullptr,
+                                                qq.x, qq.y, qq.z, r2, need, p2, e2, i2, &nc, tabs[threadIdx.x / GS], gc.n);
+        if (need) {
+#pragma unroll
+            for (int j = 0; j < K; j++) { od[j] = e2[j]; oi[j] = i2[j]; }
+            f = f2;
+        }
+    }
+    const int gl = lane_id() & (GS - 1);
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if (j < k && j % GS == gl) {
+                idx[(size_t)qi * k + j] = j < f ? oi[j] : -1;
+                d2[(size_t)qi * k + j] = j < f ? od[j] : INFINITY;
+            }
+    }
+    if (CNT) {
+        const int c27 = live && gl == 0 ? (need ? nc : block27_total(gc, cstart, qq.x, qq.y, qq.z)) : 0;
+        const int a = wave_sum_i(c27), s = wave_sum_i(live && gl == 0 ? nf + (need ? nc : 0) : 0);
+        if (lane_id() == 0) {
+            if (a) atomicAdd(&cand[0], (unsigned long long)a);
+            if (s) atomicAdd(&cand[1], (unsigned long long)s);
+        }
+    }
+}
+
+template <int GS>
+static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int nq, int k, float r2, int* idx, float* d2,
+                              unsigned long long* cand) {
+    const int blocks = (int)(((long long)nq * GS + 255) / 256);
+    // CNT: the candidate-counting instance (profiling), a separate symbol so kernel traces tell it apart
+#define KNN2(KK, CN) k_knn_2phase<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+    if (k <= 5) { if (cand) KNN2(5, true); else KNN2(5, false); }
+    else { if (cand) KNN2(8, true); else KNN2(8, false); }
+#undef KNN2
+}
+
+void knn_device_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int nq, int k, float radius, int* idx, float* d2,
+                              unsigned long long* cand) {
+    if (nq <= 0) return;
+    const float r2 = radius * radius;
+    static const int gs = getenv("ALOAM_KNN_GS2") ? atoi(getenv("ALOAM_KNN_GS2")) : 8;   // tuning knob
+    if (gs == 16) knn_2phase_launch<16>(C, gf, gc, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 2) knn_2phase_launch<2>(C, gf, gc, q, nq, k, r2, idx, d2, cand);
+    else if (gs == 4) knn_2phase_launch<4>(C, gf, gc, q, nq, k, r2, idx, d2, cand);
+    else knn_2phase_launch<8>(C, gf, gc, q, nq, k, r2, idx, d2, cand);
+    HIPCHK(hipGetLastError());
 }
 
 template <int GS>
 static void knn_group_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float r2, int* idx, float* d2,
                              unsigned long long* cand) {
     const int blocks = (int)(((long long)nq * GS + 255) / 256);
-    if (k <= 5) k_knn_group<5, GS><<<blocks, 256, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2, cand);
-    else k_knn_group<8, GS><<<blocks, 256, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2, cand);
+#define KNNG(KK, CN) k_knn_group<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(g.desc, g.cell_start, g.pts, g.idx, q, nq, k, r2, idx, d2, cand)
+    if (k <= 5) { if (cand) KNNG(5, true); else KNNG(5, false); }
+    else { if (cand) KNNG(8, true); else KNNG(8, false); }
+#undef KNNG
 }
 
 void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2,

@@ -281,6 +281,36 @@ def test_knn_device_c4_scale(gpu_ctx_factory):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("step,k,radius,frac", [(0.107, 5, 1.0, "0.3"), (0.15, 8, 1.0, "0.2"), (0.5, 5, 1.0, "0.3"),
+                                                (0.107, 3, 0.5, "0.45")])
+def test_knn_device_two_phase_bit_identical(gpu_ctx_factory, monkeypatch, step, k, radius, frac):
+    """The two-phase search (fine 3x3x3 block first, settled when the k-th neighbour is closer than
+    0.99 fine cells) returns exactly the single-phase radius-block result for EVERY query: indices,
+    distance bits and order. Dense maps (most queries settle in phase 1), a sparse one (0.5 m lattice:
+    most fall through to phase 2), k = 3/5/8 and a smaller radius."""
+    import torch
+    m = synth.dense_map(4, 0.0, 0.0, step=step)
+    R, o = synth.pose("l128", 0)
+    s = synth.scan("l128", 0)
+    q = s.copy()
+    q[:, :3] = (s[:, :3].astype(np.float64) @ R.T + o).astype(np.float32)
+    dm, dq = torch.from_numpy(m).cuda(), torch.from_numpy(q).cuda()
+    ctx = gpu_ctx_factory(128)
+    out = {}
+    for mode in ("0", frac):
+        monkeypatch.setenv("ALOAM_KNN_FINE", mode)
+        idx = torch.full((len(q), k), -7, dtype=torch.int32, device="cuda")
+        d2 = torch.full((len(q), k), -7.0, dtype=torch.float32, device="cuda")
+        ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), k, radius, idx.data_ptr(), d2.data_ptr())
+        out[mode] = (idx.cpu().numpy(), d2.cpu().numpy())
+    (i1, e1), (i2, e2) = out["0"], out[frac]
+    assert (i1 >= -1).all() and (i2 >= -1).all()
+    assert np.array_equal(i1, i2)
+    assert np.array_equal(e1.view(np.uint32), e2.view(np.uint32))
+    assert (i1[:, k - 1] >= 0).mean() > 0.3          # the case exercises found neighbourhoods
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("stages", [2, 3])
 def test_pipeline_matches_single_context(lvo, stages):
     """The node-split pipelines (aloam_forward_features / aloam_forward_mapping_input between
