@@ -106,6 +106,7 @@ static void allocate(Ctx& C) {
     C.d_ori = (float*)dalloc(C, sizeof(float) * N);
     C.d_blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, std::max(P.max_map_points, 1024) / 256 + 1) + 4096));
     C.d_hist = (int*)dalloc(C, sizeof(int) * (size_t)MAXL * nb);
+    C.d_hoff = (int*)dalloc(C, sizeof(int) * (size_t)MAXL * nb);
     C.d_cloud = (float4*)dalloc(C, sizeof(float4) * N);
     C.d_curv = (float*)dalloc(C, sizeof(float) * N);
     C.d_scratch_xyz = (float4*)dalloc(C, sizeof(float4) * N);

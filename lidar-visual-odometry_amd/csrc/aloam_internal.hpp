@@ -132,6 +132,7 @@ struct Ctx {
     float* d_ori = nullptr;        // raw -atan2f per filtered point
     int* d_blk = nullptr;          // block scratch
     int* d_hist = nullptr;         // line x block histogram
+    int* d_hoff = nullptr;         // its exclusive scan: each (line, block)'s first slot in laserCloud
     float4* d_cloud = nullptr;     // laserCloud (line ordered, intensity)
     float* d_curv = nullptr;
     float4* d_scratch_xyz = nullptr;   // per-line scratch for lines above the LDS cap

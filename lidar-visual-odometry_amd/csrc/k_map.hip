@@ -426,11 +426,18 @@ void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0
     const KindGrids cc{gc.desc, gc.cell_start, gc.pts, gc.idx}, cs{gs.desc, gs.cell_start, gs.pts, gs.idx};
     const KindGrids fc = fine ? KindGrids{gcf->desc, gcf->cell_start, gcf->pts, gcf->idx} : cc;
     const KindGrids fs = fine ? KindGrids{gsf->desc, gsf->cell_start, gsf->pts, gsf->idx} : cs;
-    if (s1 - s0 >= batch_min) {      // throughput regime: 16 points per wave pass, fits on 16 lanes
-        constexpr int NB = 2;
-        const int waves = (s1 - s0 + 8 * NB - 1) / (8 * NB);
-        const int blocks = std::max(1, std::min(16384, (waves + 3) / 4));
-        k_s2m_assoc<NB><<<blocks, 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, fc, fs, cc, cs, fine, out);
+    if (s1 - s0 >= batch_min) {      // throughput regime: 8 NB points per wave pass, fits on 8 NB lanes
+        const char* nbe = getenv("ALOAM_S2M_NB");                    // tuning knob: 2, 4, 8
+        const int nb = nbe ? atoi(nbe) : 2;
+        auto go = [&](auto nbc) {
+            constexpr int NB = decltype(nbc)::value;
+            const int waves = (s1 - s0 + 8 * NB - 1) / (8 * NB);
+            const int blocks = std::max(1, std::min(16384, (waves + 3) / 4));
+            k_s2m_assoc<NB><<<blocks, 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, fc, fs, cc, cs, fine, out);
+        };
+        if (nb == 8) go(std::integral_constant<int, 8>{});
+        else if (nb == 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 2>{});
     } else {                         // latency regime: 8 points per wave pass
         const int waves = (s1 - s0 + 7) / 8;
         const int blocks = std::max(1, std::min(4096, (waves + 3) / 4));

@@ -118,9 +118,10 @@ __global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta*
                                   int* __restrict__ sid, float* __restrict__ ori_out, int* hist, int nb, ScanMeta* meta_w) {
     __shared__ int h[MAXL];
     __shared__ int jmin;
+    __shared__ Oris sh_o;
     const int n = meta->n_cl;
     for (int i = threadIdx.x; i < N_SCANS; i += SB) h[i] = 0;
-    if (threadIdx.x == 0) jmin = 0x7fffffff;
+    if (threadIdx.x == 0) { jmin = 0x7fffffff; if (n > 0) sh_o = start_end_ori(cl, n); }   // once per block
     __syncthreads();
     int j = blockIdx.x * SB + threadIdx.x;
     if (j < n) {
@@ -130,9 +131,8 @@ __global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta*
         if (s >= 0) {
             float ori = -lm_atan2f(p.y, p.x);
             ori_out[j] = ori;
-            Oris o = start_end_ori(cl, n);
             bool passed;
-            ori_branch1(ori, o.start, &passed);
+            ori_branch1(ori, sh_o.start, &passed);
             if (passed) atomicMin(&jmin, j);
             atomicAdd(&h[s], 1);
         }
@@ -145,59 +145,37 @@ __global__ void k_bucket_classify(const float4* __restrict__ cl, const ScanMeta*
         for (int i = threadIdx.x; i < N_SCANS; i += SB) hist[i * nb + blockIdx.x] = h[i];
 }
 
-// single block: exclusive scan of hist (line-major [line][block]) and the line offsets. Chunks of
-// BS_E * 1024 counts are staged in LDS (padded against bank conflicts), each thread sums BS_E
-// consecutive counts, a wave-shuffle block scan combines the 1024 sums, and the chunk is rewritten
-// in place — ~33k counts (HDL-64) in one pass instead of a 20-step Hillis-Steele per 1024.
-constexpr int BS_T = 1024, BS_E = 32, BS_CHUNK = BS_T * BS_E;
-__host__ __device__ __forceinline__ int bs_pad(int i) { return i + (i >> 5); }
-__global__ void __launch_bounds__(BS_T) k_bucket_scan(int* hist, int nb, int N_SCANS, ScanMeta* meta) {
-    extern __shared__ int buf[];                                   // bs_pad(BS_CHUNK) ints
-    __shared__ int wsum[BS_T / WAVE];
-    __shared__ int carry_sh;
-    const int total_n = nb * N_SCANS;
-    const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
-    int carry = 0;
-    for (int base = 0; base < total_n; base += BS_CHUNK) {
-        const int cn = min(BS_CHUNK, total_n - base);
-        for (int i = t; i < BS_CHUNK; i += BS_T) buf[bs_pad(i)] = i < cn ? hist[base + i] : 0;
-        __syncthreads();
-        int s = 0;
-#pragma unroll
-        for (int k = 0; k < BS_E; k++) s += buf[bs_pad(t * BS_E + k)];
-        // block exclusive scan of s
-        int incl = s;
-        incl = wave_incl_scan(incl);
-        if (lane == WAVE - 1) wsum[w] = incl;
-        __syncthreads();
-        if (w == 0) {
-            int x = lane < BS_T / WAVE ? wsum[lane] : 0;
-            int xi = x;
-            xi = wave_incl_scan(xi);
-            if (lane < BS_T / WAVE) wsum[lane] = xi - x;               // exclusive wave offsets
-            if (lane == BS_T / WAVE - 1) carry_sh = xi;                // chunk total
-        }
-        __syncthreads();
-        int run = carry + wsum[w] + incl - s;
-#pragma unroll
-        for (int k = 0; k < BS_E; k++) {
-            const int j = bs_pad(t * BS_E + k);
-            const int v = buf[j];
-            buf[j] = run;
-            run += v;
-        }
-        __syncthreads();
-        for (int i = t; i < cn; i += BS_T) {
-            const int v = buf[bs_pad(i)];
-            hist[base + i] = v;
-            if ((base + i) % nb == 0) meta->line_off[(base + i) / nb] = v;
-        }
-        carry += carry_sh;
-        __syncthreads();
+// Line bucket offsets: one workgroup per line L. Its base is the sum of every count of the lines
+// before it (hist is line-major [line][block], so that is the prefix hist[0, L nb): read in int4
+// pieces, counts only, never rewritten), then the exclusive scan of its own nb block counts. The
+// offsets go to hoff (the scatter's table), line_off[L] = base. N_SCANS workgroups instead of one
+// serial workgroup over all N_SCANS x nb counts (22 us -> a few us at HDL-64 sizes).
+constexpr int BK_T = 512;
+__global__ void __launch_bounds__(BK_T) k_bucket_scan(const int* __restrict__ hist, int nb, int N_SCANS, ScanMeta* meta,
+                                                      int* __restrict__ hoff) {
+    const int L = blockIdx.x, t = threadIdx.x;
+    const int pre = L * nb;
+    int s = 0;
+    const int4* h4 = (const int4*)hist;
+    for (int i = t; i < pre / 4; i += BK_T) { const int4 v = h4[i]; s += (v.x + v.y) + (v.z + v.w); }
+    for (int i = (pre & ~3) + t; i < pre; i += BK_T) s += hist[i];
+    int base;
+    (void)block_exscan<BK_T>(s, &base);
+    int run = base;
+    const int* row = hist + pre;
+    for (int c0 = 0; c0 < nb; c0 += BK_T) {
+        const int v = c0 + t < nb ? row[c0 + t] : 0;
+        int tot;
+        const int ex = block_exscan<BK_T>(v, &tot);
+        if (c0 + t < nb) hoff[pre + c0 + t] = run + ex;
+        run += tot;
     }
     if (t == 0) {
-        meta->line_off[N_SCANS] = carry;
-        meta->cloud_size = carry;
+        meta->line_off[L] = base;
+        if (L == N_SCANS - 1) {
+            meta->line_off[N_SCANS] = run;
+            meta->cloud_size = run;
+        }
     }
 }
 
@@ -205,9 +183,11 @@ __global__ void k_bucket_scatter(const float4* __restrict__ cl, const ScanMeta* 
                                  const float* __restrict__ ori_in, const int* __restrict__ hist, int nb, int N_SCANS,
                                  float4* __restrict__ cloud) {
     __shared__ int wcnt[SB / WAVE][MAXL];
+    __shared__ Oris sh_o;
     const int n = meta->n_cl;
     const int w = threadIdx.x / WAVE, lane = lane_id();
     for (int i = threadIdx.x; i < (SB / WAVE) * MAXL; i += SB) (&wcnt[0][0])[i] = 0;
+    if (threadIdx.x == 0 && n > 0) sh_o = start_end_ori(cl, n);   // once per block
     __syncthreads();
     int j = blockIdx.x * SB + threadIdx.x;
     int s = j < n ? sid[j] : -1;
@@ -227,7 +207,7 @@ __global__ void k_bucket_scatter(const float4* __restrict__ cl, const ScanMeta* 
         int before = 0;
         for (int ww = 0; ww < w; ww++) before += wcnt[ww][s];
         float4 p = cl[j];
-        Oris o = start_end_ori(cl, n);
+        const Oris o = sh_o;
         float ori = ori_in[j];
         if (j <= meta->jstar) { bool passed; ori = ori_branch1(ori, o.start, &passed); }
         else ori = ori_branch2(ori, o.end);
@@ -831,14 +811,26 @@ __global__ void k_concat(const float4* __restrict__ cloud, const int* line_sharp
                          float4* sharp, int* sharp_idx, float4* lsharp, int* lsharp_idx, float4* flat, int* flat_idx,
                          float4* lflat, int* odom_nq) {
     const int line = blockIdx.x;
-    int o[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
-    for (int l = 0; l < N_SCANS; l++) {
-        for (int c = 0; c < 4; c++) {
-            int v = line_cnt[l * 4 + c];
-            if (l < line) o[c] += v;
-            tot[c] += v;
+    // per kind: the counts of the lines before this one (o) and of all lines (tot), one line per thread
+    __shared__ int sh_o[4], sh_tot[4];
+    if (threadIdx.x < 4) { sh_o[threadIdx.x] = 0; sh_tot[threadIdx.x] = 0; }
+    __syncthreads();
+    {
+        int v[4] = {0, 0, 0, 0};
+        const int l = threadIdx.x;
+        if (l < N_SCANS) { const int4 c = ((const int4*)line_cnt)[l]; v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w; }
+        if (threadIdx.x < WAVE * ((N_SCANS + WAVE - 1) / WAVE)) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int a = wave_sum_i(l < line ? v[c] : 0), b = wave_sum_i(v[c]);
+                if (lane_id() == 0) { if (a) atomicAdd(&sh_o[c], a); if (b) atomicAdd(&sh_tot[c], b); }
+            }
         }
     }
+    __syncthreads();
+    int o[4], tot[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) { o[c] = sh_o[c]; tot[c] = sh_tot[c]; }
     const int* lc = line_cnt + line * 4;
     for (int t = threadIdx.x; t < lc[0]; t += blockDim.x) {
         int i = line_sharp[line * LINE_SHARP_CAP + t];
@@ -883,14 +875,8 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
         k_filter_scatter<<<nb, SB, 0, st>>>(in, n, P.input_is_dense, thres, C.d_blk, C.d_cl);
         k_bucket_classify<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, N_SCANS, P.generic_min_elev_deg, P.generic_max_elev_deg,
                                              C.d_sid, C.d_ori, C.d_hist, nb, C.d_meta);
-        static bool scan_attr = false;
-        const size_t scan_lds = sizeof(int) * (size_t)bs_pad(BS_CHUNK);
-        if (!scan_attr) {
-            HIPCHK(hipFuncSetAttribute((const void*)k_bucket_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds));
-            scan_attr = true;
-        }
-        k_bucket_scan<<<1, BS_T, scan_lds, st>>>(C.d_hist, nb, N_SCANS, C.d_meta);
-        k_bucket_scatter<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, C.d_sid, C.d_ori, C.d_hist, nb, N_SCANS, C.d_cloud);
+        k_bucket_scan<<<N_SCANS, BK_T, 0, st>>>(C.d_hist, nb, N_SCANS, C.d_meta, C.d_hoff);
+        k_bucket_scatter<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, C.d_sid, C.d_ori, C.d_hoff, nb, N_SCANS, C.d_cloud);
         k_curvature<<<nb, SB, 0, st>>>(C.d_cloud, C.d_meta, C.d_curv);
         const size_t lds = line_lds_bytes();
         k_line_features<<<N_SCANS, LT, lds, st>>>(C.d_cloud, C.d_curv, C.d_meta, N_SCANS, C.d_scratch_xyz,
