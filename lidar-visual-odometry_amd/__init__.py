@@ -439,7 +439,8 @@ class Pipeline:
             self.last_front_timing = self._timing(0)
             self.last_odom_timing = self._timing(1)
             self.last_back_timing = self._timing(2)
-        return (abi.odom_to_dict(od) if ho.value else None), (abi.map_to_dict(mp) if hm.value else None)
+        return ((abi.LazyResult(od, abi.odom_to_dict) if ho.value else None),
+                (abi.LazyResult(mp, abi.map_to_dict) if hm.value else None))
 
     def flush(self):
         """Drain the pipeline: the (odometry, mapping) results that complete while draining."""

@@ -4,6 +4,7 @@ Kept in one place so the product binding (``__init__.py``) and the test-only ora
 (``tests/oracle_binding.py``) describe the same structs.
 """
 import ctypes as C
+from collections.abc import Mapping
 
 import numpy as np
 
@@ -148,6 +149,37 @@ def make_cloud(cap):
     buf = np.zeros((max(cap, 1), 4), np.float32)
     c = Cloud(fptr(buf), 0, cap)
     return c, buf
+
+
+class LazyResult(Mapping):
+    """Read-only mapping over a result struct, converted on first use: the pipeline returns one per
+    stage per scan, and building every list/array eagerly sat between one scan's completion and the
+    next scan's launches. The pose keys are read straight from the struct; any other access converts
+    the whole struct once (the dict odom_to_dict / map_to_dict would have built)."""
+    __slots__ = ("_raw", "_conv", "_d")
+    _POSE = ("q_w_curr", "t_w_curr")
+
+    def __init__(self, raw, conv):
+        self._raw, self._conv, self._d = raw, conv, None
+
+    def _full(self):
+        if self._d is None:
+            self._d = self._conv(self._raw)
+        return self._d
+
+    def __getitem__(self, k):
+        if self._d is None and k in self._POSE:
+            return np.array(getattr(self._raw, k)[:])
+        return self._full()[k]
+
+    def __iter__(self):
+        return iter(self._full())
+
+    def __len__(self):
+        return len(self._full())
+
+    def __repr__(self):
+        return repr(self._full())
 
 
 def odom_to_dict(r):
