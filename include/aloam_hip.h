@@ -268,14 +268,16 @@ const char*     aloam_pipeline_last_error(const aloam_pipeline* pl);
 /* stage 0 = scanRegistration context, 1 = laserOdometry (== 0 when stages == 2), 2 = laserMapping */
 aloam_ctx*      aloam_pipeline_context(aloam_pipeline* pl, int stage);
 /* Feeds one sweep (flags as aloam_scan_registration). Outputs the odometry result completed in this
- * step (*have_od: scan k for stages 2, k-1 for stages 3) and the mapping result completed in it
- * (*have_mp: scan k-2 for stages 2 — k-1 with ALOAM_PIPE_LAG=1 or profiling on —, k-2 for stages 3).
- * od / mp may be NULL. */
+ * step (*have_od: scan k-1 for both stages 2 and 3 — scan k for stages 2 with profiling on) and the
+ * mapping result completed in it (*have_mp: scan k-3 for stages 2 — k-2 with ALOAM_PIPE_LAG=1 —,
+ * k-1 with profiling on, k-2 for stages 3). od / mp may be NULL. Stages 2 returns once scan k is
+ * issued: its input (host or device) is read until the next push or flush returns. */
 int aloam_pipeline_push(aloam_pipeline* pl, const float* xyzr, int n, int flags,
                         aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp);
 /* Drains the pipeline: the odometry result still in flight (stages 3), the mapping job in flight
- * (mp) and the mapping of that last odometry result (mp2); stages 2: the (up to two) mapping results
- * still in flight, oldest in mp. */
+ * (mp) and the mapping of that last odometry result (mp2); stages 2: the issued scan's odometry
+ * result (od) and up to two of the mapping results still in flight, oldest first. Call again until it
+ * returns nothing (*have_od, *have_mp and *have_mp2 all 0). */
 int aloam_pipeline_flush(aloam_pipeline* pl, aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp,
                          aloam_map_result* mp2, int* have_mp2);
 /* HIP-event timing of each stage's last completed job (profiling on). */

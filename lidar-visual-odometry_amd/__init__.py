@@ -435,6 +435,8 @@ class Pipeline:
         od, mp = abi.OdomResult(), abi.MapResult()
         ho, hm = C.c_int(), C.c_int()
         self._check(lib().aloam_pipeline_push(self.h, ptr, cnt, flags, C.byref(od), C.byref(ho), C.byref(mp), C.byref(hm)))
+        # the scan is read until the next push / flush completes it (2 stages): keep a host array alive
+        self._held = pts if device_ptr is None else None
         if self._profiling:
             self.last_front_timing = self._timing(0)
             self.last_odom_timing = self._timing(1)
@@ -443,20 +445,25 @@ class Pipeline:
                 (abi.LazyResult(mp, abi.map_to_dict) if hm.value else None))
 
     def flush(self):
-        """Drain the pipeline: the (odometry, mapping) results that complete while draining."""
-        od, mp, mp2 = abi.OdomResult(), abi.MapResult(), abi.MapResult()
-        ho, hm, hm2 = C.c_int(), C.c_int(), C.c_int()
-        self._check(lib().aloam_pipeline_flush(self.h, C.byref(od), C.byref(ho), C.byref(mp), C.byref(hm),
-                                               C.byref(mp2), C.byref(hm2)))
-        if self._profiling:
-            self.last_back_timing = self._timing(2)
+        """Drain the pipeline: the (odometry, mapping) results that complete while draining (the C call
+        returns at most one odometry and two mapping results; it is repeated until nothing is left)."""
         out = []
-        if hm.value:
-            out.append((None, abi.map_to_dict(mp)))
-        if ho.value:
-            out.append((abi.odom_to_dict(od), abi.map_to_dict(mp2) if hm2.value else None))
-        elif hm2.value:                  # 2 stages: the second mapping result still in flight
-            out.append((None, abi.map_to_dict(mp2)))
+        while True:
+            od, mp, mp2 = abi.OdomResult(), abi.MapResult(), abi.MapResult()
+            ho, hm, hm2 = C.c_int(), C.c_int(), C.c_int()
+            self._check(lib().aloam_pipeline_flush(self.h, C.byref(od), C.byref(ho), C.byref(mp), C.byref(hm),
+                                                   C.byref(mp2), C.byref(hm2)))
+            if self._profiling:
+                self.last_back_timing = self._timing(2)
+            if hm.value:
+                out.append((None, abi.map_to_dict(mp)))
+            if ho.value:
+                out.append((abi.odom_to_dict(od), abi.map_to_dict(mp2) if hm2.value else None))
+            elif hm2.value:
+                out.append((None, abi.map_to_dict(mp2)))
+            if not (ho.value or hm.value or hm2.value):
+                break
+        self._held = None
         return out
 
     def close(self):

@@ -404,8 +404,13 @@ static void build_last_grids(Ctx& C, bool flags_preset = false, int cap_c = -1, 
     odom_last_sorted(C, flags_preset);
 }
 
-static void do_odometry(Ctx& C, aloam_odom_result* R) {
+// laserOdometry in two halves: the issue (every launch of the scan, up to the results copy) and the
+// completion (the scan's one sync, then the host-side bookkeeping). aloam_odometry runs both; the
+// 2-stage pipeline returns between them (front_issue / front_complete), so the caller's round trip
+// to the next scan overlaps this scan's GPU work.
+static void do_odometry_issue(Ctx& C) {
     if (!C.have_features) throw ApiError{ALOAM_E_STATE, "odometry before any features"};
+    if (C.fp_active) throw ApiError{ALOAM_E_STATE, "an issued odometry scan has not been completed"};
     aloam_odom_result r{};
     hipStream_t st = C.stream;
     prof_mark(C, 2);
@@ -495,6 +500,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         j.counts = m.n;
         j.pose_dst = m.pose;
         j.pose_src = C.d_odom->q_w;                    // q_w[4], t_w[3] adjacent (OdomState)
+        if (C.pre_publish) { auto f = std::move(C.pre_publish); C.pre_publish = nullptr; f(); }
         const int live = std::max(std::max(C.stack_hint[0], C.stack_hint[1]), 1);   // grid-stride copy: any size is correct
         k_forward_map_input<<<dim3(std::max(1, std::min(1024, (std::min(live, std::max(cap_s, cap_c)) + 255) / 256)), 3), 256, 0, st>>>(j);
         HIPCHK(hipGetLastError());
@@ -519,8 +525,20 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         }
     }
     // results: odom state, round counts and LM summaries in one copy into the pinned mirror (+ the
-    // scan's counts, queued behind scanRegistration): the scan's one sync
+    // scan's counts, queued behind scanRegistration): the scan's one sync, in do_odometry_complete
     d2h_small(C.h_out, C.d_out, offsetof(DevOut, map_n), st);
+    C.pre_publish = nullptr;                           // (a scan that does not publish drops it)
+    C.fp = Ctx::FrontPend{r, pend, t, hint_c, hint_s};
+    C.fp_active = true;
+}
+
+static void do_odometry_complete(Ctx& C, aloam_odom_result* R) {
+    if (!C.fp_active) throw ApiError{ALOAM_E_STATE, "no issued odometry scan"};
+    C.fp_active = false;
+    aloam_odom_result r = C.fp.r;
+    const bool pend = C.fp.pend;
+    const int t = C.fp.t, hint_c = C.fp.hint_c, hint_s = C.fp.hint_s;
+    Ctx::MapInSet& m = C.mset[t];
     sync(C);
     if (pend) {
         apply_meta(C);
@@ -563,6 +581,21 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
         C.timing.odom_search_launches = r.rounds;
     }
     if (R) *R = r;
+}
+
+static void do_odometry(Ctx& C, aloam_odom_result* R) {
+    do_odometry_issue(C);
+    do_odometry_complete(C, R);
+}
+
+void front_issue(Ctx& C, const float* xyzr, int n, int flags) {
+    HIPCHK(hipSetDevice(C.device));
+    do_scan_registration(C, xyzr, n, flags);
+    do_odometry_issue(C);
+}
+void front_complete(Ctx& C, aloam_odom_result* R) {
+    HIPCHK(hipSetDevice(C.device));
+    do_odometry_complete(C, R);
 }
 
 void mapping_issue(Ctx& C) {
@@ -679,6 +712,7 @@ void snapshot_mapping_input(Ctx& S, MapSnapshot* o) {
     o->stk_n = S.d_out->stack_n + 2 * S.in_cur;
     o->stk_ready = m.ready;
     o->fwd_done = m.fwd_rec ? m.fwd : nullptr;
+    o->src_capture_mu = &S.capture_mu;
     o->n[0] = S.n_map_corner_in; o->n[1] = S.n_map_surf_in; o->n[2] = S.n_map_full_in;
     for (int k = 0; k < 4; k++) o->pose[k] = S.h_map.q_wodom[k];
     for (int k = 0; k < 3; k++) o->pose[4 + k] = S.h_map.t_wodom[k];
@@ -739,7 +773,11 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied, bool defe
     if (side && !C.stream3) C.stream3 = make_stream(C, true);
     hipStream_t fs = side ? C.stream3 : C.stream;
     HIPCHK(hipStreamWaitEvent(fs, m.released, 0));
-    if (s.fwd_done) HIPCHK(hipStreamWaitEvent(fs, s.fwd_done, 0));   // the source's publish copy
+    if (s.fwd_done) {                                                  // the source's publish copy
+        std::unique_lock<std::mutex> lk;
+        if (s.src_capture_mu) lk = std::unique_lock<std::mutex>(*s.src_capture_mu);   // not while the source captures
+        HIPCHK(hipStreamWaitEvent(fs, s.fwd_done, 0));
+    }
     m.nc = s.n[0]; m.ns = s.n[1]; m.nf = s.n[2];
     for (int k = 0; k < 4; k++) C.h_map.q_wodom[k] = s.pose[k];
     for (int k = 0; k < 3; k++) C.h_map.t_wodom[k] = s.pose[4 + k];
@@ -757,8 +795,11 @@ void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied, bool defe
         for (int k = 0; k < 2; k++) { m.pstk_src[k] = s.stk[k]; m.pstk_n[k] = s.n[k]; }
         m.pstk_ndev = s.stk_n;
         m.pstk_ready = s.stk_ready;
+        m.pstk_mu = s.src_capture_mu;
         m.pstk_copied = copied;
     } else if (s.has_stacks) {        // (copied with the clouds)
+        std::unique_lock<std::mutex> lk;
+        if (s.src_capture_mu) lk = std::unique_lock<std::mutex>(*s.src_capture_mu);
         HIPCHK(hipStreamWaitEvent(fs, s.stk_ready, 0));
         for (int k = 0; k < 2; k++) {
             j.src[3 + k] = s.stk[k];
@@ -793,7 +834,11 @@ void forward_stacks_pending(Ctx& C, int t) {
     Ctx::MapInSet& m = C.mset[t];
     if (!m.pstk) return;
     hipStream_t st = C.stream;
-    HIPCHK(hipStreamWaitEvent(st, m.pstk_ready, 0));
+    {
+        std::unique_lock<std::mutex> lk;
+        if (m.pstk_mu) lk = std::unique_lock<std::mutex>(*m.pstk_mu);   // not while the source captures
+        HIPCHK(hipStreamWaitEvent(st, m.pstk_ready, 0));
+    }
     ForwardJob j;
     for (int k = 0; k < 2; k++) {
         j.src[3 + k] = m.pstk_src[k];

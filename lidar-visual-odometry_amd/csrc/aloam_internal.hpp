@@ -224,6 +224,7 @@ struct Ctx {
         int pstk_n[2] = {0, 0};
         const int* pstk_ndev = nullptr;
         hipEvent_t pstk_ready = nullptr, pstk_copied = nullptr;
+        std::mutex* pstk_mu = nullptr;     // the source's capture mutex (MapSnapshot::src_capture_mu)
     };
     MapInSet mset[2];
     int in_cur = 0;
@@ -275,6 +276,14 @@ struct Ctx {
     // context (the pipeline front on a hand-off's `copied`) must not do so mid-capture, or HIP fails the
     // wait with hipErrorStreamCaptureIsolation
     std::mutex capture_mu;
+    // an odometry scan issued but not yet completed (do_odometry_issue -> do_odometry_complete)
+    struct FrontPend { aloam_odom_result r; bool pend; int t, hint_c, hint_s; };
+    FrontPend fp{};
+    bool fp_active = false;
+    // run right before the next publish launch (2-stage pipeline: wait until the mapping stage has copied
+    // the hand-off that last used the target input set), then cleared; the scan's registration and
+    // odometry rounds are queued by then, so the wait holds back the publish only
+    std::function<void()> pre_publish;
     int* d_odom_nq = nullptr;        // [2]: sharp / flat counts of the current scan (device copy)
     bool ev_ready = false;
     std::chrono::steady_clock::time_point t_rounds_issued{};   // host-issue profiling (ALOAM_HOST_TIMING)
@@ -353,8 +362,14 @@ struct MapSnapshot {
     const int* stk_n = nullptr;        // device [2]
     hipEvent_t stk_ready = nullptr;    // source stream2: stacks done
     hipEvent_t fwd_done = nullptr;     // source stream: the publish copy into src[] done
+    // the source context's capture mutex: HIP fails a wait on an event whose stream is being captured
+    // (hipErrorStreamCaptureIsolation), so waits on the source's events are made under it
+    std::mutex* src_capture_mu = nullptr;
 };
 void snapshot_mapping_input(Ctx& S, MapSnapshot* out);
+// scanRegistration + laserOdometry of one scan split at its sync (2-stage pipeline front)
+void front_issue(Ctx& C, const float* xyzr, int n, int flags);
+void front_complete(Ctx& C, aloam_odom_result* R);
 void forward_snapshot(Ctx& C, const MapSnapshot& s, hipEvent_t copied, bool defer_stacks = false);
 // laserMapping split in two so the host can issue frame k while the GPU still runs frame k-1 (at most
 // two frames in flight; every launch size of frame k is an upper bound known before k-1 completes)

@@ -110,8 +110,11 @@ struct MapServer {
     // (hand-off, issue, completion) on one critical path; lag 2 lets the front run one scan further
     // ahead. ALOAM_PIPE_LAG (1 or 2, default 2); profiling runs one frame at a time (lag 1).
     int lag = 2;
+    // the front's scan k is issued by push k and completed by push k+1 (or flush): its odometry result
+    // is returned one push late, and the caller's round trip overlaps the scan's GPU work
+    bool front_pending = false;
     // ALOAM_PIPE_TIMING (profiling aid): host-side stage occupancy, printed at destroy
-    double t_fwd = 0, t_issue = 0, t_complete = 0, t_idle = 0, t_front = 0, t_take = 0;
+    double t_fwd = 0, t_issue = 0, t_complete = 0, t_idle = 0, t_front = 0, t_take = 0, t_wiss = 0;
     long n_srv = 0, n_front = 0;
 };
 static const bool g_pipe_timing = std::getenv("ALOAM_PIPE_TIMING") != nullptr;
@@ -246,6 +249,53 @@ int join_map(aloam_pipeline* P, aloam_map_result* mp, int* have) {
     return 0;
 }
 
+// completes the front's pending scan: its odometry result, its hand-off to the mapping server, and the
+// mapping result due at this point (lag)
+int finish_front(aloam_pipeline* P, aloam_odom_result* od, int* have_od, aloam_map_result* mp, int* have_mp) {
+    MapServer& S = P->ms;
+    aloam::Ctx& F = *(aloam::Ctx*)P->front;
+    S.front_pending = false;
+    aloam_odom_result o{};
+    const double tf0 = g_pipe_timing ? now_us() : 0;
+    int rc = guarded([&] { aloam::front_complete(F, &o); }, P->err);
+    if (g_pipe_timing) S.t_front += now_us() - tf0;
+    if (rc) return rc;
+    if (P->profiling) aloam_get_timing(P->front, &P->t_stage[0]), P->t_stage[1] = P->t_stage[0];
+    *have_od = 1;
+    if (od) *od = o;
+    const long seq = S.posted.load(std::memory_order_relaxed);
+    bool posted = false;
+    if (o.publish_to_mapping) {
+        try {
+            aloam::snapshot_mapping_input(F, &S.snap[seq & 1]);
+        } catch (const aloam::ApiError& e) {
+            P->err = e.msg;
+            return e.code;
+        }
+        {
+            std::lock_guard<std::mutex> lk(S.m);
+            S.posted.store(seq + 1, std::memory_order_release);
+        }
+        S.cv.notify_one();
+        posted = true;
+    }
+    // mapping result k - lag (the lag-th job before the one just posted); ALOAM_PIPE_POLL=1: returned
+    // only once done (no wait) unless NRES - 1 results are outstanding
+    const int lag = P->profiling ? 1 : S.lag;
+    static const bool poll = std::getenv("ALOAM_PIPE_POLL") && std::atoi(std::getenv("ALOAM_PIPE_POLL")) == 1;
+    const long outstanding = S.posted.load(std::memory_order_relaxed) - S.returned;
+    const bool due = poll && !P->profiling ? (outstanding >= MapServer::NRES - 1 ||
+                                              (outstanding > 0 && S.done.load(std::memory_order_acquire) > S.returned))
+                                           : outstanding > (posted ? lag : lag - 1);
+    if (due) {
+        const double tt0 = g_pipe_timing ? now_us() : 0;
+        const int trc = take_result(P, mp, have_mp);
+        if (g_pipe_timing) S.t_take += now_us() - tt0;
+        return trc;
+    }
+    return ALOAM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -328,9 +378,9 @@ void aloam_pipeline_destroy(aloam_pipeline* P) {
         if (P->ms.th.joinable()) P->ms.th.join();
         const MapServer& S = P->ms;
         if (g_pipe_timing && S.n_srv > 0 && S.n_front > 0)
-            std::fprintf(stderr, "[aloam pipe] per scan (us): front process %.1f, front wait-for-result %.1f | server: "
+            std::fprintf(stderr, "[aloam pipe] per scan (us): front process %.1f, front wait-for-result %.1f, front wait-for-issue %.1f | server: "
                          "idle %.1f, forward %.1f, issue %.1f, complete(wait+read) %.1f  (%ld / %ld)\n",
-                         S.t_front / S.n_front, S.t_take / S.n_front, S.t_idle / S.n_srv, S.t_fwd / S.n_srv,
+                         S.t_front / S.n_front, S.t_take / S.n_front, S.t_wiss / S.n_front, S.t_idle / S.n_srv, S.t_fwd / S.n_srv,
                          S.t_issue / S.n_srv, S.t_complete / S.n_srv, S.n_front, S.n_srv);
         for (auto& e : P->ms.copied) if (e) (void)hipEventDestroy(e);
     } else {
@@ -352,7 +402,7 @@ aloam_ctx* aloam_pipeline_context(aloam_pipeline* P, int stage) {
 
 int aloam_pipeline_set_profiling(aloam_pipeline* P, int enable) {
     if (!P || P->wm.busy() || (P->stages == 3 && P->wo.busy())) return ALOAM_E_STATE;
-    if (P->stages == 2 && P->ms.done.load() != P->ms.posted.load()) return ALOAM_E_STATE;
+    if (P->stages == 2 && (P->ms.front_pending || P->ms.done.load() != P->ms.posted.load())) return ALOAM_E_STATE;
     P->profiling = enable != 0;
     int rc = aloam_set_profiling(P->front, enable);
     if (!rc && P->stages == 3) rc = aloam_set_profiling(P->odom, enable);
@@ -376,53 +426,32 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
     if (P->stages == 2) {
         MapServer& S = P->ms;
         aloam::Ctx& F = *(aloam::Ctx*)P->front;
+        // scan k-1 first: its results, its hand-off (posted before scan k publishes into the other set)
+        if (S.front_pending && (rc = finish_front(P, od, have_od, mp, have_mp))) return rc;
         const long seq = S.posted.load(std::memory_order_relaxed);     // index of the next hand-off
         if (seq >= 2) {
             // this scan may publish into the buffer set hand-off seq-2 was taken from: its copy must be
-            // issued (host) and finished (GPU) first
-            while (S.issued.load(std::memory_order_acquire) < seq - 1) std::this_thread::yield();
-            hipError_t e = hipSetDevice(F.device);
-            if (e == hipSuccess) {
+            // issued (host) and finished (GPU) first. Done right before the publish launch (pre_publish),
+            // after the scan's registration and odometry rounds are queued: only the publish waits.
+            F.pre_publish = [P, &S, &F, seq]() {
+                const double tw0 = g_pipe_timing ? now_us() : 0;
+                while (S.issued.load(std::memory_order_acquire) < seq - 1) std::this_thread::yield();
+                if (g_pipe_timing) S.t_wiss += now_us() - tw0;
                 std::lock_guard<std::mutex> lk(((aloam::Ctx*)P->back)->capture_mu);   // not while mapping captures
-                e = hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0);
-            }
-            if (e != hipSuccess) {
-                P->err = std::string("hipStreamWaitEvent failed: ") + hipGetErrorName(e) + " (hand-off " +
-                         std::to_string(seq - 2) + ", server rc " + std::to_string(S.rc[(seq - 2) % MapServer::NRES]) + " " + S.err[(seq - 2) % MapServer::NRES] + ")";
-                return ALOAM_E_HIP;
-            }
+                const hipError_t e = hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0);
+                if (e != hipSuccess)
+                    throw aloam::HipError(std::string("hipStreamWaitEvent failed: ") + hipGetErrorName(e) + " (hand-off " +
+                                          std::to_string(seq - 2) + ", server rc " + std::to_string(S.rc[(seq - 2) % MapServer::NRES]) +
+                                          " " + S.err[(seq - 2) % MapServer::NRES] + ")");
+            };
         }
-        aloam_odom_result o{};
         const double tf0 = g_pipe_timing ? now_us() : 0;
-        rc = aloam_process_scan(P->front, xyzr, n, flags | ALOAM_NO_MAPPING, &o, nullptr);
+        rc = guarded([&] { aloam::front_issue(F, xyzr, n, flags); }, P->err);
         if (g_pipe_timing) { S.t_front += now_us() - tf0; S.n_front++; }
-        if (rc) return fail(P, P->front, rc);
-        if (P->profiling) aloam_get_timing(P->front, &P->t_stage[0]), P->t_stage[1] = P->t_stage[0];
-        *have_od = 1;
-        if (od) *od = o;
-        bool posted = false;
-        if (o.publish_to_mapping) {
-            try {
-                aloam::snapshot_mapping_input(F, &S.snap[seq & 1]);
-            } catch (const aloam::ApiError& e) {
-                P->err = e.msg;
-                return e.code;
-            }
-            {
-                std::lock_guard<std::mutex> lk(S.m);
-                S.posted.store(seq + 1, std::memory_order_release);
-            }
-            S.cv.notify_one();
-            posted = true;
-        }
-        // mapping result k - lag (the lag-th job before the one just posted)
-        const int lag = P->profiling ? 1 : S.lag;
-        if (S.posted.load(std::memory_order_relaxed) - S.returned > (posted ? lag : lag - 1)) {
-            const double tt0 = g_pipe_timing ? now_us() : 0;
-            const int trc = take_result(P, mp, have_mp);
-            if (g_pipe_timing) S.t_take += now_us() - tt0;
-            return trc;
-        }
+        if (rc) return rc;
+        S.front_pending = true;
+        // profiling events are per context and per call: one scan at a time (no lag on the front)
+        if (P->profiling) return finish_front(P, od, have_od, mp, have_mp);
         return ALOAM_OK;
     }
     // three stages: scanRegistration here, odometry and mapping of earlier scans in the workers
@@ -450,8 +479,9 @@ int aloam_pipeline_flush(aloam_pipeline* P, aloam_odom_result* od, int* have_od,
     if (!P || !have_od || !have_mp || !have_mp2) return ALOAM_E_ARG;
     *have_od = *have_mp = *have_mp2 = 0;
     int rc;
-    if (P->stages == 2) {             // up to two results in flight (lag 2): the older into mp, the newer into mp2
-        if (P->ms.returned < P->ms.posted.load(std::memory_order_relaxed) && (rc = take_result(P, mp, have_mp))) return rc;
+    if (P->stages == 2) {             // the pending front scan, then up to two mapping results per call
+        if (P->ms.front_pending && (rc = finish_front(P, od, have_od, mp, have_mp))) return rc;
+        if (!*have_mp && P->ms.returned < P->ms.posted.load(std::memory_order_relaxed) && (rc = take_result(P, mp, have_mp))) return rc;
         if (P->ms.returned < P->ms.posted.load(std::memory_order_relaxed)) return take_result(P, mp2, have_mp2);
         return ALOAM_OK;
     }

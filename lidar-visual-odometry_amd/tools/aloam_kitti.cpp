@@ -63,10 +63,11 @@ int main(int argc, char** argv) {
     }
     FILE* o = out_path ? std::fopen(out_path, "w") : stdout;
     if (!o) { std::perror(out_path); return 1; }
-    std::vector<float> pts;
-    size_t mapped = 0;
+    std::vector<float> bufs[2];     // a pushed sweep is read until the next push returns: alternate buffers
+    size_t mapped = 0, pushed = 0;
     double busy_s = 0;
     for (const char* path : files) {
+        std::vector<float>& pts = bufs[pushed++ & 1];
         if (!read_bin(path, pts)) {
             std::fprintf(stderr, "cannot read %s\n", path);
             return 1;
@@ -85,13 +86,16 @@ int main(int argc, char** argv) {
     }
     aloam_odom_result od;
     aloam_map_result mp, mp2;
-    int ho = 0, hm = 0, hm2 = 0;
-    if (aloam_pipeline_flush(pl, &od, &ho, &mp, &hm, &mp2, &hm2)) {
-        std::fprintf(stderr, "flush: %s\n", aloam_pipeline_last_error(pl));
-        return 1;
+    for (;;) {                      // until nothing is left in flight
+        int ho = 0, hm = 0, hm2 = 0;
+        if (aloam_pipeline_flush(pl, &od, &ho, &mp, &hm, &mp2, &hm2)) {
+            std::fprintf(stderr, "flush: %s\n", aloam_pipeline_last_error(pl));
+            return 1;
+        }
+        if (hm) { write_pose(o, mp.q_w_curr, mp.t_w_curr); mapped++; }
+        if (hm2) { write_pose(o, mp2.q_w_curr, mp2.t_w_curr); mapped++; }
+        if (!ho && !hm && !hm2) break;
     }
-    if (hm) { write_pose(o, mp.q_w_curr, mp.t_w_curr); mapped++; }
-    if (hm2) { write_pose(o, mp2.q_w_curr, mp2.t_w_curr); mapped++; }
     if (o != stdout) std::fclose(o);
     aloam_pipeline_destroy(pl);
     std::fprintf(stderr, "aloam_kitti: %zu scans, %zu mapped poses, %.3f ms/scan (incl. .bin upload)\n", files.size(),
