@@ -102,3 +102,26 @@ def test_cpp_host_tool_links_against_the_abi():
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 2 and "usage" in r.stderr
     assert "libaloam_hip.so" in subprocess.check_output(["ldd", exe], text=True)
+
+
+def test_lazy_result_matches_eager_conversion():
+    """Pipeline.push returns LazyResult mappings: the same keys and values as odom_to_dict /
+    map_to_dict, the pose keys readable before (and after) the full conversion."""
+    import numpy as np
+    od = abi.OdomResult()
+    od.rounds = 3
+    od.t_w_curr[0], od.q_w_curr[3] = 1.25, 1.0
+    for i in range(3):
+        od.corner_correspondence[i] = 10 + i
+        od.lm[i].iterations = 4
+    lz = abi.LazyResult(od, abi.odom_to_dict)
+    assert np.array_equal(lz["t_w_curr"], [1.25, 0.0, 0.0])     # pose key straight from the struct
+    eager = abi.odom_to_dict(od)
+    assert set(lz) == set(eager) and len(lz) == len(eager)
+    for k, v in eager.items():
+        assert np.array_equal(np.asarray(lz[k], dtype=object), np.asarray(v, dtype=object)), k
+    assert lz.get("missing") is None and "rounds" in lz
+    mp = abi.MapResult()
+    mp.map_total_points = 7
+    lm = abi.LazyResult(mp, abi.map_to_dict)
+    assert lm["map_total_points"] == 7 and np.array_equal(lm["q_w_curr"], abi.map_to_dict(mp)["q_w_curr"])
