@@ -156,7 +156,7 @@ static void allocate(Ctx& C) {
     C.d_nbr = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_factors);
     C.d_lm = (LMState*)dalloc(C, sizeof(LMState));
     C.d_partials = (double*)dalloc(C, sizeof(double) * 512 * 32);
-    C.d_lm_recs = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * 64 * 32);
+    C.d_lm_recs = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * 128 * 32);
     C.d_lm_seq = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2);
     HIPCHK(hipHostMalloc((void**)&C.h_bar_err, sizeof(int) * 4, hipHostMallocMapped));   // read at every sync, no copy
     std::memset(C.h_bar_err, 0, sizeof(int) * 4);
@@ -292,7 +292,7 @@ void join_lane1(Ctx& C) {
 static void sync(Ctx& C) {
     HIPCHK(hipStreamSynchronize(C.stream));
     if (*(volatile int*)C.h_bar_err) {   // a solver grid barrier timed out: reset it and report (results void)
-        HIPCHK(hipMemsetAsync(C.d_lm_recs, 0, sizeof(unsigned long long) * 2 * 64 * 32, C.stream));
+        HIPCHK(hipMemsetAsync(C.d_lm_recs, 0, sizeof(unsigned long long) * 2 * 128 * 32, C.stream));
         HIPCHK(hipMemsetAsync(C.d_lm_seq, 0, sizeof(unsigned long long) * 2, C.stream));
         HIPCHK(hipStreamSynchronize(C.stream));
         *(volatile int*)C.h_bar_err = 0;

@@ -175,7 +175,7 @@ struct Ctx {
     int cap_factors = 0;
     LMState* d_lm = nullptr;
     double* d_partials = nullptr;
-    unsigned long long* d_lm_recs = nullptr;  // 2 x 64 x 32 u64: LM pass partial records + tags (double-buffered)
+    unsigned long long* d_lm_recs = nullptr;  // 2 x 128 x 32 u64: LM pass partial records + tags (double-buffered)
     unsigned long long* d_lm_seq = nullptr;   // LM launch sequence number (record tags = seq*256 + pass + 1)
     int map_slots_hint = 0;          // last mapping frame's stack sizes (LM grid sizing only)
     int* d_last_sorted = nullptr;    // [2]: corner_last / surf_last ordered by scan line

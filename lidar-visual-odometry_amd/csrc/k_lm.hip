@@ -654,9 +654,12 @@ __device__ __forceinline__ bool gather_partials(unsigned long long* buf, unsigne
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) __hip_atomic_store(&mine[LM_REC - 1], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // lane l polls the tags of records l and l + 64 (G <= 128)
         const unsigned long long* tag = buf + (size_t)threadIdx.x * LM_REC + (LM_REC - 1);
+        const unsigned long long* tag2 = tag + (size_t)64 * LM_REC;
         int spins = 0, good = 1;
-        while (!__all(threadIdx.x >= G || __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch)) {
+        while (!__all((threadIdx.x >= G || __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) &&
+                      (threadIdx.x + 64 >= G || __hip_atomic_load(tag2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch))) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1 << 22)) { good = 0; break; }
         }
@@ -677,7 +680,7 @@ __device__ __forceinline__ bool gather_partials(unsigned long long* buf, unsigne
 // partials in the same fixed order and runs the identical LM tail on its own LDS copy of the state
 // (bitwise-identical on all workgroups, so no broadcast and one barrier per pass).
 constexpr int CB = 256;
-constexpr int LM_COOP_MAX = 64;
+constexpr int LM_COOP_MAX = 128;                   // records per pass buffer (gather_partials polls 2 per lane)
 constexpr int LM_CACHE = 1024;                      // factor slots per workgroup kept in LDS (80 KB)
 #ifdef ALOAM_LM_TIMING
 __device__ unsigned long long g_lm_ts[8][5];   // micro-benchmark only: block-0 phase stamps per pass
@@ -773,7 +776,10 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
     const int est = std::max(1, std::min(nslots, live_hint > 0 ? live_hint + live_hint / 4 : nslots));
     static const int spt = getenv("ALOAM_LM_SPT") ? std::max(1, atoi(getenv("ALOAM_LM_SPT"))) : 1;   // tuning knob
     int G = std::max((est + spt * CB - 1) / (spt * CB), (est + LM_CACHE - 1) / LM_CACHE);
-    G = std::max(1, std::min(std::min(LM_COOP_MAX, C.n_cus), G));   // every workgroup must be co-resident (<= 1 per CU)
+    // tuning knob: workgroup cap (C3 pipeline, mapping solves of ~100 workgroups' worth of slots: 64 ->
+    // 1393 scans/s, 128 -> 1366; fewer slots per workgroup cost more exchange than they save)
+    static const int gmax = getenv("ALOAM_LM_GMAX") ? std::max(1, std::min(LM_COOP_MAX, atoi(getenv("ALOAM_LM_GMAX")))) : 64;
+    G = std::max(1, std::min(std::min(gmax, C.n_cus), G));   // every workgroup must be co-resident (<= 1 per CU)
     const int cap = std::min(LM_CACHE, (nslots + G - 1) / G);          // LDS slots per workgroup
     const size_t lds = sizeof(aloam_factor) * (size_t)cap;
     k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_lm_recs, C.d_lm_seq, C.d_bar_err, out,
