@@ -238,6 +238,7 @@ struct Ctx {
     KindScratch ksv;                     // stack VoxelGrid scratch of stream3
     int* d_tmp_n = nullptr;              // [2] counts scratch of the utility entry points
     int* d_nbr = nullptr;                                // [queries][5] neighbour slots
+    int* d_s2m_nbr = nullptr; int cap_s2m_nbr = 0;       // split registration association: parked neighbours
     float4* d_registered = nullptr;
     int n_registered = 0;
     bool have_map_input = false;

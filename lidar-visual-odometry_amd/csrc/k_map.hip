@@ -417,6 +417,54 @@ __global__ void __launch_bounds__(256) k_s2m_assoc(const float4* __restrict__ cs
     assoc_slots_batched<NB>(cstack, sstack, nc, s0, s1, par, fc, fs, cc, cs, use_fine != 0, out, tabs, park);
 }
 
+// Split association (throughput regime; ALOAM_S2M_SPLIT=0 selects the fused kernel below): the 5-NN by 8-lane groups parks each slot's
+// neighbour positions (+ found | fine-copy flag) in global memory, then k_s2m_fit fits one slot per lane
+// — the same fit_factor on the same neighbours, so the same factor records as the fused kernel.
+constexpr int S2M_NBR = 8;          // ints per parked slot: 5 positions, flags, pad
+__global__ void __launch_bounds__(256) k_s2m_knn(const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc,
+                                                 int s0, int s1, const double* __restrict__ x, KindGrids fc, KindGrids fs,
+                                                 KindGrids cc, KindGrids cs, int use_fine, int* __restrict__ nbr) {
+    __shared__ int tabs[256 / AG][20];
+    double par[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) par[i] = x[i];
+    const int per_wave = WAVE / AG;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
+    for (int base = s0 + wave * per_wave; base < s1; base += nwaves * per_wave) {   // wave-uniform trip count
+        const int qi = base + lane_id() / AG;
+        const bool live = qi < s1;
+        const bool corner = qi < nc;
+        const int li = corner ? qi : qi - nc;
+        const float4 po = live ? (corner ? cstack[li] : sstack[li]) : make_float4(0, 0, 0, 0);
+        const float4 sel = associate_to_map(par, po);
+        int pos[5];
+        const float4* sp;
+        const int found = knn5_fine_coarse(fc, fs, cc, cs, use_fine != 0, corner, sel, live, pos, &sp, tabs[threadIdx.x / AG]);
+        if (live && (lane_id() & (AG - 1)) == 0) {
+            int* o = nbr + (size_t)(qi - s0) * S2M_NBR;
+            *(int4*)o = make_int4(pos[0], pos[1], pos[2], pos[3]);
+            *(int4*)(o + 4) = make_int4(pos[4], found | ((use_fine && sp == (corner ? fc.sp : fs.sp)) ? 256 : 0), 0, 0);
+        }
+    }
+}
+__global__ void __launch_bounds__(256) k_s2m_fit(const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc,
+                                                 int s0, int s1, KindGrids fc, KindGrids fs, KindGrids cc, KindGrids cs,
+                                                 const int* __restrict__ nbr, aloam_factor* __restrict__ out) {
+    for (int qi = s0 + blockIdx.x * blockDim.x + threadIdx.x; qi < s1; qi += gridDim.x * blockDim.x) {
+        const int* o = nbr + (size_t)(qi - s0) * S2M_NBR;
+        const int4 a = *(const int4*)o, b = *(const int4*)(o + 4);
+        const int pos[5] = {a.x, a.y, a.z, a.w, b.x};
+        const int fl = b.y;
+        const bool corner = qi < nc;
+        const float4 po = corner ? cstack[qi] : sstack[qi - nc];
+        const float4* sp = (fl & 256) ? (corner ? fc.sp : fs.sp) : (corner ? cc.sp : cs.sp);
+        aloam_factor f;
+        f.type = -1; f.pad = 0;
+        if ((fl & 255) == 5) fit_factor(corner, po, sp, pos, f);
+        out[qi] = f;
+    }
+}
+
 void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
                       const Grid* gcf, const Grid* gsf, aloam_factor* out) {
     if (s1 <= s0) return;
@@ -426,7 +474,21 @@ void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0
     const KindGrids cc{gc.desc, gc.cell_start, gc.pts, gc.idx}, cs{gs.desc, gs.cell_start, gs.pts, gs.idx};
     const KindGrids fc = fine ? KindGrids{gcf->desc, gcf->cell_start, gcf->pts, gcf->idx} : cc;
     const KindGrids fs = fine ? KindGrids{gsf->desc, gsf->cell_start, gsf->pts, gsf->idx} : cs;
-    if (s1 - s0 >= batch_min) {      // throughput regime: 8 NB points per wave pass, fits on 8 NB lanes
+    // split 5-NN / fit kernels (default; ALOAM_S2M_SPLIT=0: fused): C4 2.74 -> 2.02 ms per registration —
+    // the fp64 fits on every lane instead of 16 of 64, the search waves no longer wait on them
+    const char* spe = getenv("ALOAM_S2M_SPLIT");
+    if (s1 - s0 >= batch_min && !(spe && atoi(spe) == 0)) {
+        const int n = s1 - s0;
+        if (C.cap_s2m_nbr < n) {         // grown on demand, released with the context
+            C.cap_s2m_nbr = std::max(n, 2 * C.cap_s2m_nbr);
+            C.d_s2m_nbr = (int*)dalloc(C, sizeof(int) * S2M_NBR * (size_t)C.cap_s2m_nbr);
+        }
+        const int waves = (n + WAVE / AG - 1) / (WAVE / AG);
+        k_s2m_knn<<<std::max(1, std::min(16384, (waves + 3) / 4)), 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, fc, fs, cc, cs,
+                                                                                      fine, C.d_s2m_nbr);
+        k_s2m_fit<<<std::max(1, std::min(4096, (n + 255) / 256)), 256, 0, C.stream>>>(cq, sq, nc, s0, s1, fc, fs, cc, cs,
+                                                                                      C.d_s2m_nbr, out);
+    } else if (s1 - s0 >= batch_min) {   // throughput regime: 8 NB points per wave pass, fits on 8 NB lanes
         const char* nbe = getenv("ALOAM_S2M_NB");                    // tuning knob: 2, 4, 8
         const int nb = nbe ? atoi(nbe) : 2;
         auto go = [&](auto nbc) {

@@ -156,10 +156,12 @@ def test_s2m_c4_scale_device_resident(gpu_ctx_factory):
         assert np.array_equal(r["x"].view(np.uint64), g["x"].view(np.uint64))
 
 
-@pytest.mark.parametrize("batch_min,fine_cell", [("1", "0.3"), ("1", "0"), ("100000000", "0.3"), ("100000000", "0.15")])
-def test_s2m_assoc_paths_bit_identical(gpu_ctx_factory, monkeypatch, batch_min, fine_cell):
-    """Every association path — latency (8 points per wave pass) or throughput regime (16), with or
-    without the fine-grid first phase (any fine cell) — emits the same factors: the registrations are
+@pytest.mark.parametrize("batch_min,fine_cell,split", [("1", "0.3", "0"), ("1", "0", "0"), ("100000000", "0.3", "0"),
+                                                      ("100000000", "0.15", "0"), ("1", "0.3", "1"), ("1", "0", "1")])
+def test_s2m_assoc_paths_bit_identical(gpu_ctx_factory, monkeypatch, batch_min, fine_cell, split):
+    """Every association path — latency (8 points per wave pass) or throughput regime (16, fused or
+    split into 5-NN and fit kernels), with or without the fine-grid first phase (any fine cell) — emits
+    the same factors: the registrations are
     bit-identical to the plain path (latency regime, coarse grid only) and match the oracle. The map is
     dense (0.1 m lattice) so the fine phase settles most queries."""
     wl = small_workload(half=10.0, map_step=0.1, surf_stride=6, corner_stride=24)
@@ -169,6 +171,7 @@ def test_s2m_assoc_paths_bit_identical(gpu_ctx_factory, monkeypatch, batch_min, 
     ref = loaded_ctx(gpu_ctx_factory, wl).s2m_register(x0)
     monkeypatch.setenv("ALOAM_S2M_BATCH_MIN", batch_min)
     monkeypatch.setenv("ALOAM_S2M_FINE_CELL", fine_cell)
+    monkeypatch.setenv("ALOAM_S2M_SPLIT", split)          # split 5-NN / fit kernels (throughput regime)
     g = loaded_ctx(gpu_ctx_factory, wl).s2m_register(x0)
     assert np.array_equal(g["x"].view(np.uint64), ref["x"].view(np.uint64))
     assert g["lm"] == ref["lm"] and g["surf_num"] == ref["surf_num"] and g["corner_num"] == ref["corner_num"]
