@@ -211,22 +211,19 @@ static void allocate(Ctx& C) {
     C.d_vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
     C.d_vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     C.d_vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
-    C.sort_tmp_bytes = std::max(voxel_sort_tmp_bytes(C.cap_voxel), cube_sort_tmp_bytes(C.cap_map)) + 1024;
-    C.d_sort_tmp = dalloc(C, C.sort_tmp_bytes);
     C.d_ins_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_voxel);
     C.d_ins_val = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     C.d_ins_val2 = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     // lane scratch: lane 0 aliases the buffers above, lane 1 is a second set for stream2
     KindScratch& k0 = C.ks[0];
     k0.vkeys = C.d_vkeys; k0.vkeys2 = C.d_vkeys2; k0.vvals = C.d_vvals; k0.vvals2 = C.d_vvals2;
-    k0.sort_tmp = C.d_sort_tmp; k0.ins_pts = C.d_ins_pts; k0.ins_val = C.d_ins_val; k0.ins_val2 = C.d_ins_val2;
+    k0.ins_pts = C.d_ins_pts; k0.ins_val = C.d_ins_val; k0.ins_val2 = C.d_ins_val2;
     k0.seg_keys = C.d_seg_keys; k0.blk = C.d_blk; k0.map_tmp = C.d_map_tmp;
     KindScratch& k1 = C.ks[1];
     k1.vkeys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)C.cap_voxel);
     k1.vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
     k1.vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     k1.vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
-    k1.sort_tmp = dalloc(C, C.sort_tmp_bytes);
     k1.ins_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_voxel);
     k1.ins_val = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     k1.ins_val2 = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
@@ -238,7 +235,6 @@ static void allocate(Ctx& C) {
     kv.vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
     kv.vvals = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_voxel);
     kv.vvals2 = (int*)dalloc(C, sizeof(int) * ((size_t)C.cap_voxel + 64));
-    kv.sort_tmp = dalloc(C, C.sort_tmp_bytes);
     kv.blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, M / 256 + 1) + 4096));
     HIPCHK(hipStreamCreateWithFlags(&C.stream2, hipStreamNonBlocking));
     for (auto& m : C.mset) {
@@ -514,10 +510,9 @@ static void do_odometry_issue(Ctx& C) {
             hint_c = pend ? std::min(cap_c, C.stack_hint[0] > 0 ? C.stack_hint[0] : cap_c) : cap_c;   // (exact when known)
             hint_s = pend ? std::min(cap_s, C.stack_hint[1] > 0 ? C.stack_hint[1] : cap_s) : cap_s;
             fork_lane1(C);
-            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, hint_c, C.P.mapping_line_resolution, m.cstack,
-                                 C.d_out->stack_n + 2 * t + 0, false);
-            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.surf, m.n + 1, hint_s, C.P.mapping_plane_resolution, m.sstack,
-                                 C.d_out->stack_n + 2 * t + 1, false);
+            voxel_grid_pair_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, hint_c, C.P.mapping_line_resolution, m.cstack,
+                               C.d_out->stack_n + 2 * t + 0, m.surf, m.n + 1, hint_s, C.P.mapping_plane_resolution, m.sstack,
+                               C.d_out->stack_n + 2 * t + 1);
             HIPCHK(hipEventRecord(m.ready, C.stream2));
             m.stacks_pub = true;
         } else {
@@ -561,10 +556,9 @@ static void do_odometry_complete(Ctx& C, aloam_odom_result* R) {
         m.nf = C.features_from_host ? 0 : C.n_full;
         if (C.publish_stacks && (m.nc > hint_c || m.ns > hint_s)) {
             // a count outgrew its hint: redo both stacks with the exact sizes (stream order overwrites)
-            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
-                                 C.d_out->stack_n + 2 * t + 0, false);
-            voxel_grid_sorted_on(C, C.stream2, C.ks[1], m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
-                                 C.d_out->stack_n + 2 * t + 1, false);
+            voxel_grid_pair_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
+                               C.d_out->stack_n + 2 * t + 0, m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
+                               C.d_out->stack_n + 2 * t + 1);
             HIPCHK(hipEventRecord(m.ready, C.stream2));
         }
         // next publish's hints: these sizes + 25% + 1024 (capped by the buffers)
@@ -748,10 +742,9 @@ void use_input_set(Ctx& C, int t) {
 // they depend on the hand-off only, so they run while the previous frame still occupies the stream.
 static void prepare_stacks(Ctx& C, int t) {
     Ctx::MapInSet& m = C.mset[t];
-    voxel_grid_sorted_on(C, C.stream3, C.ksv, m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
-                         C.d_out->stack_n + 2 * t + 0, false);
-    voxel_grid_sorted_on(C, C.stream3, C.ksv, m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
-                         C.d_out->stack_n + 2 * t + 1, false);
+    voxel_grid_pair_on(C, C.stream3, C.ksv, m.corner, m.n + 0, m.nc, C.P.mapping_line_resolution, m.cstack,
+                       C.d_out->stack_n + 2 * t + 0, m.surf, m.n + 1, m.ns, C.P.mapping_plane_resolution, m.sstack,
+                       C.d_out->stack_n + 2 * t + 1);
     HIPCHK(hipEventRecord(m.ready, C.stream3));
     m.stacks = true;
 }

@@ -102,8 +102,7 @@ struct DevOut {
 };
 struct KindScratch {               // per-lane scratch for the map kinds' concurrent work
     unsigned long long *vkeys = nullptr, *vkeys2 = nullptr;   // 2 x cap_voxel, cap_voxel
-    int *vvals = nullptr, *vvals2 = nullptr;                  // cap_voxel, cap_voxel + 64 (+ VoxHdr)
-    void* sort_tmp = nullptr;
+    int *vvals = nullptr, *vvals2 = nullptr;                  // cap_voxel, cap_voxel + 64
     float4* ins_pts = nullptr;
     int *ins_val = nullptr, *ins_val2 = nullptr;
     unsigned long long* seg_keys = nullptr;                   // 4 x cap_map + 32768
@@ -243,8 +242,7 @@ struct Ctx {
     int n_registered = 0;
     bool have_map_input = false;
     int map_frame_count = 0;
-    // voxel-grid scratch (rocprim)
-    void* d_sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
+    // voxel-grid scratch
     unsigned long long *d_vkeys = nullptr, *d_vkeys2 = nullptr;
     int *d_vvals = nullptr, *d_vvals2 = nullptr;
     int cap_voxel = 0;
@@ -341,15 +339,15 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
             int live_hint = 0);
 void lm_eval_only(Ctx& C, const aloam_factor* d_f, int n, const double* d_x, int robust, double* d_res, double* d_jac, double* d_neq);
 void knn_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float radius, int* idx, float* d2);
-size_t voxel_sort_tmp_bytes(int cap);
-size_t cube_sort_tmp_bytes(int cap);
-// lane 0: C.stream + the primary scratch; lane 1: C.stream2 + the second scratch set
+// PCL VoxelGrid of one cloud / a pair of clouds (k_voxel.hip, one workgroup per cloud). The count is read
+// on the device and clamped to cap (a hinted launch). lane 0: C.stream + the primary scratch; lane 1:
+// C.stream2 + the second scratch set
 void voxel_grid_sorted_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* pts, const int* d_n, int cap_n, float leaf,
-                          float4* out, int* d_nout, bool hdr_armed);
-void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane = 0,
-                       bool hdr_armed = false);
-unsigned* voxel_hdr(Ctx& C, int lane);   // bb[6] + nrun of the lane's VoxelGrid header (device)
-void stable_sort_pairs(Ctx& C, unsigned* kin, unsigned* kout, int* vin, int* vout, int n, int end_bit, int lane = 0);
+                          float4* out, int* d_nout);
+void voxel_grid_pair_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* ptsA, const int* d_nA, int capA, float leafA,
+                        float4* outA, int* d_noutA, const float4* ptsB, const int* d_nB, int capB, float leafB, float4* outB,
+                        int* d_noutB);
+void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, float leaf, float4* out, int* d_nout, int lane = 0);
 void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so far
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
 void map_frame_launch(Ctx& C, int input_set);

@@ -16,11 +16,11 @@
 //   insert + rebuild append the stacks to their cubes, counting-sort the map by cube, per-cube
 //                    VoxelGrid of the surrounding cubes (:737-801)
 #include <cstring>
-#include <rocprim/rocprim.hpp>
 
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 #include "eigen_small.hpp"
+#include "pcl_sort.hpp"
 
 namespace aloam {
 #ifdef ALOAM_WSTAMP_MAP
@@ -37,8 +37,6 @@ WSTAMP_DEFINE_TABLE
 #endif
 
 void prof_mark(Ctx& C, int idx);
-void segment_voxel_launch(Ctx& C, const float4* pts, const int* off, const int* seg_list, const int* nseg_p, int max_seg,
-                          float leaf, float4* out, int* seg_nout, unsigned long long* gkeys);
 
 constexpr int MB = 256;
 constexpr int PAD_CUBE = 8191;
@@ -54,16 +52,10 @@ __device__ inline float4 associate_to_map(const double* par, float4 p) {   // :1
     return make_float4((float)(r.x + par[4]), (float)(r.y + par[5]), (float)(r.z + par[6]), p.w);
 }
 
-// also zeroes this frame's mapping round counters and arms the stacks' VoxelGrid headers (saves three
-// launches on the host-issue-bound part of the frame)
-__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* spread, unsigned* vox_bb0, unsigned* vox_bb1,
-                              const double* pose_in) {
+// also zeroes this frame's mapping round counters (saves a launch on the host-issue-bound part of the frame)
+__global__ void k_map_prepare(MapState* m, unsigned char* cube_valid, int* spread, const double* pose_in) {
     __shared__ int valid_num;
     for (int i = threadIdx.x; i < ALOAM_MAX_ROUNDS * ODOM_CNT_SLOTS * ODOM_CNT_STRIDE; i += blockDim.x) spread[i] = 0;
-    if (threadIdx.x < 8) {                      // VoxHdr {bb[6], nrun, pad} of both lanes
-        const unsigned v = threadIdx.x < 3 ? 0xffffffffu : 0u;
-        if (threadIdx.x < 7) { vox_bb0[threadIdx.x] = v; vox_bb1[threadIdx.x] = v; }
-    }
     if (threadIdx.x == 0) {
         for (int k = 0; k < 4; k++) m->q_wodom[k] = pose_in[k];      // the input set's laser_odom_to_init
         for (int k = 0; k < 3; k++) m->t_wodom[k] = pose_in[4 + k];
@@ -533,24 +525,6 @@ __global__ void k_map_update(MapState* m, const int* __restrict__ spread, int ro
     m->t_wmap_wodom[2] = m->parameters[6] - r.z;
 }
 
-// stack point -> map frame -> cube (:739-783). key = cube (or PAD_CUBE when outside the grid)
-__global__ void k_map_insert(const float4* __restrict__ stack, const int* d_n, int ub, const MapState* __restrict__ m,
-                             float4* __restrict__ ins_pts, unsigned* __restrict__ key, int* __restrict__ val) {
-    const int n = *d_n;
-    for (int i = blockIdx.x * MB + threadIdx.x; i < ub; i += gridDim.x * MB) {
-        unsigned k = PAD_CUBE;
-        if (i < n) {
-            const float4 s = associate_to_map(m->parameters, stack[i]);
-            ins_pts[i] = s;
-            const int ci = cube_coord(s.x, m->cenW), cj = cube_coord(s.y, m->cenH), ck = cube_coord(s.z, m->cenD);
-            if (ci >= 0 && ci < CUBE_W && cj >= 0 && cj < CUBE_H && ck >= 0 && ck < CUBE_D)
-                k = (unsigned)(ci + CUBE_W * cj + CUBE_W * CUBE_H * ck);
-        }
-        key[i] = k;
-        val[i] = i;
-    }
-}
-
 // cube bookkeeping arrays: cnt_old, cnt_new, first_old, first_new, off, seg_nout, final_off (each CUBE_N+1)
 struct CubeArrays { int *first_old, *last_old, *first_new, *last_new, *off, *seg_nout, *final_off; };
 // counts from run boundaries (the old map and the sorted new points are both ordered by cube)
@@ -562,28 +536,8 @@ __global__ void k_cube_reset(CubeArrays a) {
         a.last_old[c] = -1; a.last_new[c] = -1; a.first_old[c] = 0x7fffffff; a.first_new[c] = 0x7fffffff; a.seg_nout[c] = 0;
     }
 }
-__global__ void k_cube_count_old(const int* __restrict__ cube, const int* d_n, CubeArrays a) {
-    const int n = *d_n;
-    for (int i = blockIdx.x * MB + threadIdx.x; i < n; i += gridDim.x * MB) {
-        const int c = cube[i];
-        if (c < 0) continue;
-        if (i == 0 || cube[i - 1] != c) a.first_old[c] = i;
-        if (i == n - 1 || cube[i + 1] != c) a.last_old[c] = i;
-    }
-}
-__global__ void k_cube_count_new(const unsigned* __restrict__ skey, int ub, CubeArrays a) {
-    for (int p = blockIdx.x * MB + threadIdx.x; p < ub; p += gridDim.x * MB) {
-        const unsigned c = skey[p];
-        if (c >= (unsigned)CUBE_N) continue;
-        if (p == 0 || skey[p - 1] != c) a.first_new[c] = p;
-        if (p == ub - 1 || skey[p + 1] != c) a.last_new[c] = p;
-    }
-}
 // single block: exclusive scan over cubes of v(c); mode 0: cnt_old+cnt_new -> off ; mode 1: final counts -> final_off
 __device__ __forceinline__ void cube_scan_body(const CubeArrays& a, const unsigned char* __restrict__ valid, int mode, int* total);
-__global__ void __launch_bounds__(1024) k_cube_scan(CubeArrays a, const unsigned char* __restrict__ valid, int mode, int* total) {
-    cube_scan_body(a, valid, mode, total);
-}
 __device__ __forceinline__ void cube_scan_body(const CubeArrays& a, const unsigned char* __restrict__ valid, int mode, int* total) {
     constexpr int PER = (CUBE_N + 1023) / 1024;
     int* dst = mode == 0 ? a.off : a.final_off;
@@ -608,227 +562,67 @@ __device__ __forceinline__ void cube_scan_body(const CubeArrays& a, const unsign
     }
     if (threadIdx.x == 0) { dst[CUBE_N] = tot; if (total) *total = tot; }
 }
-__global__ void k_cube_scatter(const float4* __restrict__ old_pts, const int* __restrict__ old_cube, const int* d_n_old,
-                               const float4* __restrict__ ins_pts, const unsigned* __restrict__ skey, const int* __restrict__ sval,
-                               int ub_new, CubeArrays a, float4* __restrict__ B, int* __restrict__ Bcube) {
-    const int n_old = *d_n_old;
-    const int stride = gridDim.x * MB;
-    for (int i = blockIdx.x * MB + threadIdx.x; i < n_old; i += stride) {
-        const int c = old_cube[i];
-        if (c < 0) continue;
-        const int pos = a.off[c] + (i - a.first_old[c]);
-        B[pos] = old_pts[i];
-        Bcube[pos] = c;
-    }
-    for (int p = blockIdx.x * MB + threadIdx.x; p < ub_new; p += stride) {
-        const unsigned c = skey[p];
-        if (c >= (unsigned)CUBE_N) continue;
-        const int pos = a.off[c] + old_count(a, c) + (p - a.first_new[c]);
-        B[pos] = ins_pts[sval[p]];
-        Bcube[pos] = (int)c;
-    }
-}
 __global__ void k_map_register(const float4* __restrict__ full, int n, const MapState* __restrict__ m, float4* __restrict__ out) {
     const int i = blockIdx.x * MB + threadIdx.x;
     if (i < n) out[i] = associate_to_map(m->parameters, full[i]);
 }
 
-__global__ void k_copy_int(const int* src, int* dst) { *dst = *src; }
 
 // ------------------------------------------------------------------------------------------
-// Per-cube VoxelGrid of the surrounding cubes (:788-801) as ONE stable radix sort: key = (rank of
-// the cube in the surrounding list) << 32 | leaf index inside that cube's own PCL grid (or the point
-// position when PCL's int32 leaf count overflows: pass-through); points of other cubes sort last. Stable => the points of a leaf are summed in the cube's order.
-constexpr unsigned long long CV_NONE = 0x7fffffffffull;   // > any (rank<<32|idx), rank < 125
-struct CubeVox { unsigned bb[125][6]; int minb[125][3]; int mul1[125], mul2[125], ovf[125]; int rank_of[CUBE_N]; int first_run[126]; int nrun; };
-
-__global__ void k_cubevox_init(CubeVox* v, const MapState* m) {
-    for (int i = threadIdx.x; i < CUBE_N; i += blockDim.x) v->rank_of[i] = -1;
-    for (int i = threadIdx.x; i < 125 * 6; i += blockDim.x) (&v->bb[0][0])[i] = (i % 6) < 3 ? 0xffffffffu : 0u;
-    for (int i = threadIdx.x; i < 126; i += blockDim.x) v->first_run[i] = 0x7fffffff;
-    __syncthreads();
-    for (int r = threadIdx.x; r < m->valid_num; r += blockDim.x) v->rank_of[m->valid_ind[r]] = r;
-    if (threadIdx.x == 0) v->nrun = 0;
-}
-// one workgroup per surrounding cube: bbox of its points in B
-__global__ void k_cubevox_bbox(const float4* __restrict__ B, CubeArrays a, const MapState* m, CubeVox* v, float leaf) {
-    __shared__ unsigned sh[6];
-    const int r = blockIdx.x;
-    if (r >= m->valid_num) return;
-    const int c = m->valid_ind[r];
-    if (threadIdx.x < 6) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    __syncthreads();
-    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-    const int p0 = a.off[c], p1 = a.off[c + 1];
-    constexpr int U = 4;                                   // 4 independent loads in flight per thread
-    for (int base = p0 + threadIdx.x; base < p1; base += U * blockDim.x) {
-        float4 q[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int p = base + u * blockDim.x;
-            q[u] = p < p1 ? B[p] : B[base];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const unsigned v[3] = {f2ord(q[u].x), f2ord(q[u].y), f2ord(q[u].z)};
-            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
-        }
-    }
-    for (int d = 0; d < 3; d++) {
-        const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
-        if (lane_id() == 0) { atomicMin(&sh[d], (unsigned)lo); atomicMax(&sh[3 + d], (unsigned)hi); }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int d = 0; d < 6; d++) v->bb[r][d] = sh[d];
-        bool ovf;
-        int minb[3], mul1, mul2;
-        voxel_params(sh, leaf, &ovf, minb, &mul1, &mul2);      // same bbox -> leaf grid as k_voxel.hip
-        for (int d = 0; d < 3; d++) v->minb[r][d] = minb[d];
-        v->mul1[r] = mul1; v->mul2[r] = mul2; v->ovf[r] = ovf;
-    }
-}
-__global__ void k_cubevox_keys(const float4* __restrict__ B, const int* __restrict__ Bcube, CubeArrays a, const CubeVox* __restrict__ v,
-                               float leaf, int ub, unsigned long long* __restrict__ keys, int* __restrict__ vals) {
-    const int total = a.off[CUBE_N];
-    const float inv = 1.0f / leaf;
-    for (int p = blockIdx.x * MB + threadIdx.x; p < ub; p += gridDim.x * MB) {
-        unsigned long long k = CV_NONE;
-        if (p < total) {
-            const int r = v->rank_of[Bcube[p]];
-            if (r >= 0) {
-                const int mb[3] = {v->minb[r][0], v->minb[r][1], v->minb[r][2]};
-                const unsigned idx = v->ovf[r] ? (unsigned)p : voxel_index(B[p], inv, mb, v->mul1[r], v->mul2[r]);
-                k = ((unsigned long long)r << 32) | idx;
-            }
-        }
-        keys[p] = k;
-        vals[p] = p;
-    }
-}
-// run heads (leaf changes) -> global run ids by a block count + small scan, first run of each cube
-__global__ void k_cubevox_flags(const unsigned long long* __restrict__ keys, int ub, int* blk) {
-    __shared__ int sh[MB / WAVE];
-    const int i = blockIdx.x * MB + threadIdx.x;
-    const int f = i < ub && keys[i] != CV_NONE && (i == 0 || keys[i] != keys[i - 1]);
-    const int s = wave_sum_i(f);
-    if (lane_id() == 0) sh[threadIdx.x / WAVE] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < MB / WAVE; w++) t += sh[w]; blk[blockIdx.x] = t; }
-}
-__global__ void k_cubevox_heads(const unsigned long long* __restrict__ keys, int ub, const int* blk, int* heads, CubeVox* v) {
-    __shared__ int sh[MB / WAVE];
-    const int i = blockIdx.x * MB + threadIdx.x;
-    const int f = i < ub && keys[i] != CV_NONE && (i == 0 || keys[i] != keys[i - 1]);
-    const unsigned long long mk = __ballot(f);
-    if (lane_id() == 0) sh[threadIdx.x / WAVE] = __popcll(mk);
-    __syncthreads();
-    int before = blk[blockIdx.x];
-    for (int w = 0; w < (int)(threadIdx.x / WAVE); w++) before += sh[w];
-    if (f) {
-        const int run = before + __popcll(mk & lanemask_lt64());
-        heads[run] = i;
-        const int r = (int)(keys[i] >> 32);
-        if (i == 0 || (int)(keys[i - 1] >> 32) != r) v->first_run[r] = run;
-    }
-}
-// one thread per run: centroid summed in sorted (= cube) order, written at the cube's offset
-__global__ void k_cubevox_centroids(const float4* __restrict__ B, const unsigned long long* __restrict__ keys, const int* __restrict__ vals,
-                                    const int* __restrict__ heads, const int* nrun_p, int ub, const MapState* m, const CubeVox* v,
-                                    CubeArrays a, float4* __restrict__ out) {
-    const int nrun = *nrun_p;
-    const int run = blockIdx.x * MB + threadIdx.x;
-    if (run >= nrun) return;
-    const int h0 = heads[run];
-    int h1 = run + 1 < nrun ? heads[run + 1] : ub;
-    const int r = (int)(keys[h0] >> 32);
-    const int c = m->valid_ind[r];
-    float4 s = B[vals[h0]];
-    int cnt = 1;
-    for (int t = h0 + 1; t < h1 && keys[t] == keys[h0]; t++) {
-        const float4 q = B[vals[t]];
-        s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
-        cnt++;
-    }
-    const float fc = (float)cnt;
-    const int local = run - v->first_run[r];
-    out[a.off[c] + local] = make_float4(s.x / fc, s.y / fc, s.z / fc, s.w / fc);
-    // the last run of the cube records the cube's leaf count
-    const bool last_of_cube = (run + 1 == nrun) || ((int)(keys[heads[run + 1]] >> 32) != r);
-    if (last_of_cube) a.seg_nout[c] = local + 1;
-}
-
-// ------------------------------------------------------------------------------------------
-// Per-cube VoxelGrid of the surrounding cubes in ONE launch (replaces cubevox init / bbox / keys /
-// 39-bit radix sort / flags / scan / heads / centroids): one 1024-thread workgroup per surrounding cube
-// c, over its points in B[off[c], off[c+1]) = the cube's old points, then its appended stack points.
-// The old points are last frame's VoxelGrid output of the cube, i.e. in ascending PCL leaf order, and
-// leaf order is (k, j, i) order whatever the bbox, so they stay sorted: only the appended points are
-// sorted (by (leaf, position), chunk_rank_sort) and merged in by rank (old before new on equal leaves)
-// — the same sequence a stable sort by leaf of the whole cube gives, hence the same centroids (summed in
-// that order) as the device-wide sort. A cube whose old points are not sorted (it was outside the
-// surrounding set when they were appended) or with too many appended points takes a bitonic sort.
-#ifdef ALOAM_WSTAMP_RB
-__device__ int g_rb_info[256][4];
-extern "C" int aloam_dbg_rb_info(int* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rb_info), sizeof(g_rb_info)); }
-__device__ inline void g_dbg_n(int c, int n, int n_o, int uns, float leaf) { const int b = blockIdx.x + (leaf > 0.6f ? 128 : 0); if (blockIdx.x < 128) { g_rb_info[b][0] = c; g_rb_info[b][1] = n; g_rb_info[b][2] = n_o; g_rb_info[b][3] = uns; } }
-#else
-__device__ inline void g_dbg_n(int, int, int, int, float) {}
-#endif
+// Per-cube VoxelGrid of the surrounding cubes (:788-801) in ONE launch: one 1024-thread workgroup per
+// surrounding cube c, over its points in B[off[c], off[c+1]) = the cube's old points, then its appended
+// stack points (the order laserCloudCornerArray[ind] has when downSizeFilter.filter runs). The cube's
+// (leaf, position) pairs are put in PCL's order — libstdc++ std::sort by leaf, pcl_sort.hpp — and every
+// leaf is summed from zero in that order (CentroidPoint), so the cube's new points equal PCL's bit for
+// bit. Cubes up to RBV_CAP points sort in LDS, larger ones in the cube's global scratch.
 constexpr int RBV_T = 1024;
-constexpr int RBV_CAP = 16320;       // cube points whose keys / order live in LDS (more: global scratch)
-constexpr int RBV_NCAP = 4096;       // appended points sorted in LDS (more: the bitonic fallback)
-constexpr size_t RBV_LDS = 256 + 2 * (size_t)RBV_NCAP * 8 + (size_t)RBV_CAP * 4 + (size_t)RBV_CAP * 2;
-constexpr int RBV_PER = 12;          // points per thread held in registers for the bbox and the keys
-constexpr int RBV_RUN = 8;           // sorted positions per thread per centroid pass (n > RBV_T x RBV_RUN: more passes)
+constexpr int RBV_CAP = 7168;        // cube points sorted in LDS (more: global scratch)
+constexpr int RBV_SC = ps_scratch_ints(RBV_T);
+constexpr size_t RBV_HDR = 64;
+constexpr size_t RBV_LDS = RBV_HDR + 4 * (size_t)RBV_SC + 16 * (size_t)RBV_CAP + 4 * (size_t)ps_seg_ints(ps_segcap(RBV_CAP));
+constexpr int RBV_PER = 8;           // points per thread held in registers for the bbox and the keys
 static_assert(RBV_LDS <= 160 * 1024, "LDS");
-struct RbvShared { unsigned bb[6]; int unsorted; int nrun; };
-
-__device__ __forceinline__ void rbv_bitonic_u64(unsigned long long* k, int n2) {   // global or LDS, whole block
-    for (int size = 2; size <= n2; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < n2 / 2; t += blockDim.x) {
-                const int i = 2 * t - (t & (stride - 1)), j = i + stride;
-                const bool asc = (i & size) == 0;
-                const unsigned long long x = k[i], y = k[j];
-                if ((x > y) == asc) { k[i] = y; k[j] = x; }
-            }
-            __syncthreads();
-        }
-}
-
-// barrier for data that lives in LDS when the cube fits, in global scratch otherwise
-template <bool FITS> __device__ __forceinline__ void rbv_bar() { if (FITS) lds_barrier(); else __syncthreads(); }
+struct RbvShared { unsigned bb[6]; int bad; int pad; };
 
 template <bool FITS>
-__device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n, int n_o,
+__device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n,
                                          float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr, const int* fb) {
     RbvShared& SH = *(RbvShared*)smem;
-    unsigned long long* nk = (unsigned long long*)(smem + 256);
-    unsigned long long* nk2 = nk + RBV_NCAP;               // merge sort ping-pong
-    unsigned* lkeys = (unsigned*)(nk2 + RBV_NCAP);
-    unsigned short* lorder = (unsigned short*)(lkeys + RBV_CAP);
-    const int n_n = n - n_o;
+    int* sc = (int*)(smem + RBV_HDR);
+    const int tid = threadIdx.x;
+    unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, stop positions, segments
+    unsigned long long* E;
+    int *Lp, *Rp, *seg;
+    if (FITS) {
+        E = (unsigned long long*)(smem + RBV_HDR + 4 * (size_t)RBV_SC);
+        Lp = (int*)(E + RBV_CAP);
+        Rp = Lp + RBV_CAP;
+        seg = Rp + RBV_CAP;
+    } else {
+        E = gseg;
+        Lp = (int*)(gseg + n);
+        Rp = Lp + n;
+        seg = (int*)(gseg + 2 * (size_t)n);
+    }
     RBSTAMP(0);
-    if (threadIdx.x < 6) SH.bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    if (threadIdx.x == 0) { SH.unsorted = 0; SH.nrun = 0; }
+    if (tid < 6) SH.bb[tid] = tid < 3 ? 0xffffffffu : 0u;
+    if (tid == 0) SH.bad = 0;
     lds_barrier();
     // the cube's points: up to RBV_PER per thread in registers (bbox, then keys without a reload)
     float4 pt[RBV_PER];
 #pragma unroll
     for (int u = 0; u < RBV_PER; u++) {
-        const int t = threadIdx.x + u * RBV_T;
+        const int t = tid + u * RBV_T;
         pt[u] = t < n ? B[p0 + t] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const float inv = 1.0f / leaf;
-    unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, order, bitonic (2n)
-    unsigned* keys = FITS ? lkeys : (unsigned*)gseg;      // compile-time choice: ds_* or global, never flat
-    int* gorder = (int*)(gseg + (n + 1) / 2);
+    auto put = [&](int t, unsigned k) { E[t] = ((unsigned long long)k << 32) | (unsigned)t; };
     int minb[3], mul1, mul2;
     // Leaf keys without the bbox (fb != null): the cube's points lie in its 50 m box, so leaf indices
     // taken from a fixed base below the box, 10 bits per axis, order exactly like PCL's (k, j, i)-linear
     // index over the bbox grid and are equal exactly when PCL's are (PCL's int-overflow pass-through
-    // cannot occur with under 1024 leaves per axis). A key out of range falls back to the bbox path.
+    // cannot occur with under 1024 leaves per axis); std::sort only sees comparisons, so the order it
+    // leaves is the same. A key out of range falls back to the bbox path.
     bool slow = fb == nullptr;
     if (!slow) {
         for (int d = 0; d < 3; d++) minb[d] = fb[d];
@@ -843,177 +637,94 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
         };
 #pragma unroll
         for (int u = 0; u < RBV_PER; u++) {
-            const int t = threadIdx.x + u * RBV_T;
-            if (t < n) keys[t] = fast_key(pt[u]);
+            const int t = tid + u * RBV_T;
+            if (t < n) put(t, fast_key(pt[u]));
         }
-        for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) keys[t] = fast_key(B[p0 + t]);
-        if (__ballot(bad) && lane_id() == 0) SH.unsorted = 2;
-        rbv_bar<FITS>();
-        slow = SH.unsorted == 2;
-        if (slow) {
-            lds_barrier();
-            if (threadIdx.x == 0) SH.unsorted = 0;
-        }
+        for (int t = tid + RBV_PER * RBV_T; t < n; t += RBV_T) put(t, fast_key(B[p0 + t]));
+        if (__ballot(bad) && lane_id() == 0) SH.bad = 1;
+        lds_barrier();
+        slow = SH.bad != 0;
     }
     if (slow) {
-    {   // bbox (ordered-int encoding)
-        unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+        {   // bbox (ordered-int encoding)
+            unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+#pragma unroll
+            for (int u = 0; u < RBV_PER; u++) {
+                if (tid + u * RBV_T >= n) continue;
+                const unsigned v[3] = {f2ord(pt[u].x), f2ord(pt[u].y), f2ord(pt[u].z)};
+#pragma unroll
+                for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+            }
+            for (int t = tid + RBV_PER * RBV_T; t < n; t += RBV_T) {   // beyond the register tile
+                const float4 p = B[p0 + t];
+                const unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
+#pragma unroll
+                for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+            }
+#pragma unroll
+            for (int d = 0; d < 3; d++) {
+                const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
+                if (lane_id() == 0) { atomicMin(&SH.bb[d], (unsigned)lo); atomicMax(&SH.bb[3 + d], (unsigned)hi); }
+            }
+        }
+        lds_barrier();
+        bool ovf;
+        voxel_params(SH.bb, leaf, &ovf, minb, &mul1, &mul2);    // same bbox -> leaf grid as k_voxel.hip
+        if (ovf) {                            // PCL's int overflow: pass-through (every point its own leaf)
+            for (int t = tid; t < n; t += RBV_T) Cf[p0 + t] = B[p0 + t];
+            if (tid == 0) a.seg_nout[c] = n;
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < RBV_PER; u++) {
-            if (threadIdx.x + u * RBV_T >= n) continue;
-            const unsigned v[3] = {f2ord(pt[u].x), f2ord(pt[u].y), f2ord(pt[u].z)};
-#pragma unroll
-            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+            const int t = tid + u * RBV_T;
+            if (t < n) put(t, voxel_index(pt[u], inv, minb, mul1, mul2));
         }
-        for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) {   // beyond the register tile
-            const float4 p = B[p0 + t];
-            const unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
-#pragma unroll
-            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
-        }
-#pragma unroll
-        for (int d = 0; d < 3; d++) {
-            const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
-            if (lane_id() == 0) { atomicMin(&SH.bb[d], (unsigned)lo); atomicMax(&SH.bb[3 + d], (unsigned)hi); }
-        }
+        for (int t = tid + RBV_PER * RBV_T; t < n; t += RBV_T) put(t, voxel_index(B[p0 + t], inv, minb, mul1, mul2));
     }
-    lds_barrier();
-    bool ovf;
-    voxel_params(SH.bb, leaf, &ovf, minb, &mul1, &mul2);    // same bbox -> leaf grid as k_voxel.hip
-    if (ovf) {                            // PCL's int overflow: pass-through (every point its own leaf)
-        for (int t = threadIdx.x; t < n; t += RBV_T) Cf[p0 + t] = B[p0 + t];
-        if (threadIdx.x == 0) a.seg_nout[c] = n;
-        return;
-    }
-#pragma unroll
-    for (int u = 0; u < RBV_PER; u++) {
-        const int t = threadIdx.x + u * RBV_T;
-        if (t < n) keys[t] = voxel_index(pt[u], inv, minb, mul1, mul2);
-    }
-    for (int t = threadIdx.x + RBV_PER * RBV_T; t < n; t += RBV_T) keys[t] = voxel_index(B[p0 + t], inv, minb, mul1, mul2);
-    rbv_bar<FITS>();
-    }
+    if (FITS) lds_barrier(); else __syncthreads();
     RBSTAMP(1);
-    for (int t = threadIdx.x; t + 1 < n_o; t += RBV_T)
-        if (keys[t] > keys[t + 1]) SH.unsorted = 1;
-    rbv_bar<FITS>();
-    auto put_order = [&](int pos, int idx) { if (FITS) lorder[pos] = (unsigned short)idx; else gorder[pos] = idx; };
-    if (!SH.unsorted && n_n <= RBV_NCAP) {
-        // appended points: sort (leaf, position) keys, then merge with the sorted old points along the
-        // merge path (each thread: one diagonal binary search, then its contiguous run of outputs)
-        const int n2 = (n_n + WAVE - 1) / WAVE * WAVE;
-        for (int j = threadIdx.x; j < n2; j += RBV_T)
-            nk[j] = j < n_n ? (((unsigned long long)keys[n_o + j] << 32) | (unsigned)j) : ~0ull;
-        rbv_bar<FITS>();
-        RBSTAMP(2);
-        const unsigned long long* nks = n2 > 0 ? block_merge_sort<unsigned long long, 4>(nk, nk2, n2) : nk;   // ends with a barrier
-        RBSTAMP(3);
-        const int per = (n + RBV_T - 1) / RBV_T;
-        const int d0 = min(n, (int)threadIdx.x * per), d1 = min(n, d0 + per);
-        if (d0 < d1) {
-            int lo = max(0, d0 - n_n), hi = min(d0, n_o);   // old points among the first d0 outputs
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (keys[mid] <= (unsigned)(nks[d0 - 1 - mid] >> 32)) lo = mid + 1; else hi = mid;   // old first on ties
-            }
-            int i = lo, j = d0 - lo;
-            for (int d = d0; d < d1; d++) {
-                const bool take_old = i < n_o && (j >= n_n || keys[i] <= (unsigned)(nks[j] >> 32));
-                if (take_old) { put_order(d, i); i++; }
-                else { put_order(d, n_o + (int)(nks[j] & 0xffffffffu)); j++; }
-            }
-        }
-    } else {
-        // bitonic sort of (leaf, position) over the cube (global scratch; rare: see above)
-        int n2 = 1;
-        while (n2 < n) n2 <<= 1;
-        unsigned long long* bk = gseg + (size_t)2 * n;      // n2 < 2n slots
-        for (int t = threadIdx.x; t < n2; t += RBV_T)
-            bk[t] = t < n ? (((unsigned long long)keys[t] << 32) | (unsigned)t) : ~0ull;
+    if (n <= RBV_T * PS_MAX_CHUNK) {
+        pcl_std_sort<RBV_T, !FITS>(E, n, Lp, Rp, sc, seg, FITS ? ps_segcap(RBV_CAP) : ps_segcap(n));
+    } else {                                  // beyond the parallel replay's reach: one thread
+        if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();
-        rbv_bitonic_u64(bk, n2);
-        for (int t = threadIdx.x; t < n; t += RBV_T) put_order(t, (int)(bk[t] & 0xffffffffu));
     }
-    rbv_bar<FITS>();
     RBSTAMP(4);
-    // runs of equal leaves in sorted order -> centroids, fp32 in sorted order. Thread k owns sorted
-    // positions [k per, (k+1) per): head flags, one block scan for the run numbers, all its points loaded
-    // at once, then each head sums its run (reading past the thread's range from global memory).
-    auto ord = [&](int pos) { return FITS ? (int)lorder[pos] : gorder[pos]; };
-    auto put_run = [&](int run, float4 v, int k) { Cf[p0 + run] = div4_by_count(v, k); };
-    for (int base = 0; base < n; base += RBV_T * RBV_RUN) {
-        const int per = min(RBV_RUN, (n - base + RBV_T - 1) / RBV_T);
-        const int t0 = base + threadIdx.x * per;
-        int oi[RBV_RUN];
-        unsigned kk[RBV_RUN];
-        int nh = 0;
-        unsigned kprev = 0;
-        if (t0 < n && t0 > 0) kprev = keys[ord(t0 - 1)];
-#pragma unroll
-        for (int u = 0; u < RBV_RUN; u++) {
-            const int t = t0 + u;
-            oi[u] = (u < per && t < n) ? ord(t) : 0;
-            kk[u] = (u < per && t < n) ? keys[oi[u]] : 0;
-        }
-        float4 pv[RBV_RUN];
-#pragma unroll
-        for (int u = 0; u < RBV_RUN; u++) pv[u] = (u < per && t0 + u < n) ? B[p0 + oi[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int u = 0; u < RBV_RUN; u++) {
-            const int t = t0 + u;
-            if (u < per && t < n && (t == 0 || kk[u] != (u ? kk[u - 1] : kprev))) nh++;
-        }
-        int tot;
-        int run = SH.nrun + block_exscan<RBV_T, true>(nh, &tot);
-        if (base == 0) RBSTAMP(7);
-        // each run: heads in the thread's range, summed in order (registers, then global past the range)
+    // runs of equal leaves in sorted order -> centroids (fp32 from zero, in sorted order) at the cube's
+    // offset; thread k owns sorted positions [k C, (k+1) C), a run is summed by the thread of its head
+    const int C = (n + RBV_T - 1) / RBV_T;
+    const int q0 = min(n, tid * C), q1 = min(n, q0 + C);
+    int nh = 0;
+    for (int q = q0; q < q1; q++) nh += (q == 0 || ps_key(E[q]) != ps_key(E[q - 1]));
+    int run = nh, dummy = 0, tot, td;
+    ps_exscan2<RBV_T>(run, dummy, sc + 8, tot, td);
+    for (int q = q0; q < q1; q++) {
+        const unsigned k = ps_key(E[q]);
+        if (!(q == 0 || k != ps_key(E[q - 1]))) continue;
         float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
         int cnt = 0;
-        bool open = false;
+        for (int t = q; t < n; t += 4) {        // 4 points in flight per step
+            unsigned long long e[4];
+            bool in[4];
+            float4 v[4];
 #pragma unroll
-        for (int u = 0; u < RBV_RUN; u++) {
-            const int t = t0 + u;
-            if (!(u < per && t < n)) continue;
-            const bool head = t == 0 || kk[u] != (u ? kk[u - 1] : kprev);
-            if (head) {
-                if (open) { put_run(run, cc, cnt); run++; }
-                cc = pv[u]; cnt = 1; open = true;
-            } else if (open) {
-                cc.x += pv[u].x; cc.y += pv[u].y; cc.z += pv[u].z; cc.w += pv[u].w; cnt++;
-            }
+            for (int u = 0; u < 4; u++) { e[u] = t + u < n ? E[t + u] : ~0ull; }
+            bool go = true;
+#pragma unroll
+            for (int u = 0; u < 4; u++) { go = go && t + u < n && ps_key(e[u]) == k; in[u] = go; }
+#pragma unroll
+            for (int u = 0; u < 4; u++) if (in[u]) v[u] = B[p0 + (int)(e[u] & 0xffffffffu)];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (in[u]) { cc.x += v[u].x; cc.y += v[u].y; cc.z += v[u].z; cc.w += v[u].w; cnt++; }
+            if (!in[3]) break;
         }
-#ifdef ALOAM_WSTAMP_RB
-        lds_barrier();
-        if (base == 0) RBSTAMP(6);
-#endif
-        if (open) {   // the last run begun here may continue into the next threads' positions
-            const unsigned lf = kk[min(per, n - t0) - 1];
-            for (int t = t0 + per; t < n; t += 8) {        // 8 positions per step: one load latency per 8 points
-                int o8[8];
-                bool in8[8];
-                float4 q8[8];
-                bool go = true;
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    o8[u] = t + u < n ? ord(t + u) : 0;
-                    go = go && t + u < n && keys[o8[u]] == lf;
-                    in8[u] = go;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u++) if (in8[u]) q8[u] = B[p0 + o8[u]];
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (in8[u]) { cc.x += q8[u].x; cc.y += q8[u].y; cc.z += q8[u].z; cc.w += q8[u].w; cnt++; }
-                if (!in8[7]) break;
-            }
-            put_run(run, cc, cnt);
-        }
-        lds_barrier();                    // (the centroid stores are left in flight)
-        if (threadIdx.x == 0) SH.nrun += tot;
-        lds_barrier();
+        Cf[p0 + run] = div4_by_count(cc, cnt);
+        run++;
     }
     RBSTAMP(5);
-    if (threadIdx.x == 0) { a.seg_nout[c] = SH.nrun; g_dbg_n(c, n, n_o, SH.unsorted, leaf); }
+    if (tid == 0) a.seg_nout[c] = tot;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1179,7 +890,6 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
     const CubeArrays& a = K.a;
     const int p0 = a.off[c], n = a.off[c + 1] - p0;
     if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
-    const int n_o = old_count(a, c);
     int fbv[3];
     const int* fb = nullptr;
     if (K.fast_keys) {                    // leaf base below the cube's box (cube_coord: x in [50 (ci - cen) - 25, +50])
@@ -1188,8 +898,8 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
         for (int d = 0; d < 3; d++) fbv[d] = (int)floorf((float)(50.0 * (cc[d] - cen[d]) - 26.0) * inv);
         fb = fbv;
     }
-    if (n <= RBV_CAP) rbv_cube<true>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr, fb);
-    else rbv_cube<false>(smem, K.B, a, c, p0, n, n_o, K.leaf, K.Cf, K.gscr, fb);
+    if (n <= RBV_CAP) rbv_cube<true>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb);
+    else rbv_cube<false>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb);
 }
 
 __global__ void __launch_bounds__(1024) k_rb_final_scan(RbKinds P, const unsigned char* __restrict__ valid) {
@@ -1214,35 +924,8 @@ __global__ void k_rb_final(RbKinds P, const unsigned char* __restrict__ valid) {
     }
 }
 
-__global__ void k_cube_final_reset(const float4* __restrict__ B, const int* __restrict__ Bcube, const float4* __restrict__ Cf,
-                                   const unsigned char* __restrict__ valid, CubeArrays a, float4* __restrict__ A, int* __restrict__ Acube) {
-    const int total = a.off[CUBE_N];
-    for (int p = blockIdx.x * MB + threadIdx.x; p < total; p += gridDim.x * MB) {
-        const int c = Bcube[p];
-        const int local = p - a.off[c];
-        if (!valid[c]) { A[a.final_off[c] + local] = B[p]; Acube[a.final_off[c] + local] = c; }
-        else if (local < a.seg_nout[c]) { A[a.final_off[c] + local] = Cf[p]; Acube[a.final_off[c] + local] = c; }
-    }
-    for (int c = blockIdx.x * MB + threadIdx.x; c <= CUBE_N; c += gridDim.x * MB) {   // next rebuild's run tables
-        a.last_old[c] = -1; a.last_new[c] = -1; a.first_old[c] = 0x7fffffff; a.first_new[c] = 0x7fffffff;
-    }
-}
-
-size_t cube_sort_tmp_bytes(int cap) {
-    size_t bytes = 0;
-    HIPCHK(rocprim::radix_sort_pairs((void*)nullptr, bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr, (int*)nullptr, (int*)nullptr,
-                                     (unsigned)cap, 0, 39, (hipStream_t)0));
-    return bytes;
-}
-
-__global__ void k_scan_small_m(int* a, int nb, int* total) {
-    block_scan_array(a, nb, total);
-}
-
 // ------------------------------------------------------------------------------------------
 static int nblk(int n) { return std::max(1, std::min(2048, (n + MB - 1) / MB)); }
-// 0: the per-cube VoxelGrid as one device-wide radix sort + 12 launches (round-1 path, kept for A/B)
-static const int g_rebuild_fused = getenv("ALOAM_REBUILD_FUSED") ? atoi(getenv("ALOAM_REBUILD_FUSED")) : 1;
 
 static CubeArrays cube_arrays(Ctx& C, int which) {
     CubeArrays a;
@@ -1290,61 +973,6 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     HIPCHK(hipGetLastError());
 }
 
-static int g_map_exp();
-static void rebuild_map(Ctx& C, int which, int ub_new, const float4* stack, const int* d_stack_n, float leaf) {
-    hipStream_t st = (which && !(g_map_exp() & 8)) ? C.stream2 : C.stream;   // the kinds rebuild concurrently
-    KindScratch& K = C.ks[which];
-    float4* A = which == 0 ? C.d_mc : C.d_ms;
-    int* Acube = which == 0 ? C.d_mc_cube : C.d_ms_cube;
-    float4* B = which == 0 ? C.d_mc2 : C.d_ms2;
-    int* Bcube = which == 0 ? C.d_mc2_cube : C.d_ms2_cube;
-    const int n_old_ub = which == 0 ? C.n_mc : C.n_ms;
-    int* d_n_old = C.d_map_n + which;
-    // scratch carving: cube arrays live in d_cube_cnt ([7][CUBE_N+1])
-    CubeArrays a;
-    int* base = C.d_cube_cnt + which * 7 * (CUBE_N + 1);
-    a.first_old = base; a.last_old = base + (CUBE_N + 1); a.first_new = base + 2 * (CUBE_N + 1);
-    a.last_new = base + 3 * (CUBE_N + 1); a.off = base + 4 * (CUBE_N + 1); a.seg_nout = base + 5 * (CUBE_N + 1);
-    a.final_off = base + 6 * (CUBE_N + 1);
-    if (C.n_mc + C.n_ms + 2 * ub_new > C.cap_map) throw ApiError{ALOAM_E_CAPACITY, "map capacity exceeded"};
-    unsigned* k1 = (unsigned*)K.vkeys;
-    unsigned* k2 = (unsigned*)K.vkeys2;
-    k_map_insert<<<nblk(ub_new), MB, 0, st>>>(stack, d_stack_n, ub_new, C.d_map, K.ins_pts, k1, K.ins_val);
-    if (ub_new > 0) {
-        size_t bytes = C.sort_tmp_bytes;
-        HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, k1, k2, K.ins_val, K.ins_val2, (unsigned)ub_new, 0, 13, st));
-    }
-    k_cube_reset<<<(CUBE_N + 1 + 255) / 256, 256, 0, st>>>(a);
-    k_cube_count_old<<<nblk(n_old_ub), MB, 0, st>>>(Acube, d_n_old, a);
-    k_cube_count_new<<<nblk(ub_new), MB, 0, st>>>(k2, ub_new, a);
-    k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 0, nullptr);
-    k_cube_scatter<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(A, Acube, d_n_old, K.ins_pts, k2, K.ins_val2, ub_new, a, B, Bcube);
-    // per-cube VoxelGrid of the surrounding cubes into Cf at the same offsets (one stable radix sort)
-    float4* Cf = K.map_tmp;
-    const int ub_tot = n_old_ub + ub_new;
-    CubeVox* cv = (CubeVox*)K.seg_keys;                         // scratch header
-    unsigned long long* vk1 = K.seg_keys + 32768;
-    unsigned long long* vk2 = vk1 + (size_t)C.cap_map;
-    int* vv1 = (int*)(vk2 + (size_t)C.cap_map);
-    int* vv2 = vv1 + (size_t)C.cap_map;
-    int* heads = vv2 + (size_t)C.cap_map;
-    const int nbt = (ub_tot + MB - 1) / MB;
-    k_cubevox_init<<<1, 1024, 0, st>>>(cv, C.d_map);
-    k_cubevox_bbox<<<125, 256, 0, st>>>(B, a, C.d_map, cv, leaf);
-    k_cubevox_keys<<<nblk(ub_tot), MB, 0, st>>>(B, Bcube, a, cv, leaf, ub_tot, vk1, vv1);
-    if (ub_tot > 0) {
-        size_t bytes = C.sort_tmp_bytes;
-        HIPCHK(rocprim::radix_sort_pairs(K.sort_tmp, bytes, vk1, vk2, vv1, vv2, (unsigned)ub_tot, 0, 39, st));
-        k_cubevox_flags<<<nbt, MB, 0, st>>>(vk2, ub_tot, K.blk);
-        k_scan_small_m<<<1, 1024, 0, st>>>(K.blk, nbt, &cv->nrun);
-        k_cubevox_heads<<<nbt, MB, 0, st>>>(vk2, ub_tot, K.blk, heads, cv);
-        k_cubevox_centroids<<<nbt, MB, 0, st>>>(B, vk2, vv2, heads, &cv->nrun, ub_tot, C.d_map, cv, a, Cf);
-    }
-    k_cube_scan<<<1, 1024, 0, st>>>(a, C.d_cube_valid, 1, d_n_old);
-    k_cube_final_reset<<<nblk(n_old_ub + ub_new), MB, 0, st>>>(B, Bcube, Cf, C.d_cube_valid, a, A, Acube);
-    HIPCHK(hipGetLastError());
-}
-
 // one-time state of the rebuild's run tables (afterwards every rebuild leaves them reset)
 void rebuild_init(Ctx& C) {
     static bool attr = false;
@@ -1370,7 +998,6 @@ static const int g_assoc_blocks = getenv("ALOAM_ASSOC_BLOCKS") ? atoi(getenv("AL
 static const int g_fit_split = getenv("ALOAM_FIT_SPLIT") ? atoi(getenv("ALOAM_FIT_SPLIT")) : 0;   // tuning knob
 static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 8;   // tuning knob: lanes per query (C3, serial on 256 CUs: 8 / 16 / 32 = 25.5 / 19.9 / 29.0 us; pipeline on 128 CUs: 8 / 16 = 22.2 / 24.6 us)
 static const int g_map_u = getenv("ALOAM_MAP_U") ? atoi(getenv("ALOAM_MAP_U")) : 4;     // tuning knob: loads in flight
-static int g_map_exp() { return g_exp; }
 __global__ void k_noop() {}
 // ALOAM_MAP_PHASES (profiling aid): GPU time of the frame's phases from events on the frame's stream,
 // read back two frames later (that frame is complete by then), means printed every 200 frames
@@ -1407,8 +1034,7 @@ void map_frame_launch(Ctx& C, int X) {
     const bool deferred = in.pstk;   // stacks copied right before the rounds (forward_stacks_pending)
     if (in.stacks || (in.stacks_pub && !deferred)) HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
     if (g_map_phases) map_phase(C, 0);
-    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_map_spread, voxel_hdr(C, 0), voxel_hdr(C, 1),
-                                     in.pose);
+    k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_map_spread, in.pose);
     k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
     const GridBuild gb[2] = {{&C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid},
                              {&C.g_map_surf, C.d_ms, C.d_map_n + 1, std::max(C.n_ms, 1), C.d_ms_cube, C.d_cube_valid}};
@@ -1424,10 +1050,8 @@ void map_frame_launch(Ctx& C, int X) {
     } else if (in.stacks) {
         HIPCHK(hipStreamWaitEvent(st, in.ready, 0));
     } else {
-        fork_lane1(C);
-        voxel_grid_sorted(C, in.corner, in.n + 0, ub_c, C.P.mapping_line_resolution, in.cstack, stack_n + 0, 0, true);
-        voxel_grid_sorted(C, in.surf, in.n + 1, ub_s, C.P.mapping_plane_resolution, in.sstack, stack_n + 1, 1, true);
-        join_lane1(C);
+        voxel_grid_pair_on(C, st, C.ks[0], in.corner, in.n + 0, ub_c, C.P.mapping_line_resolution, in.cstack, stack_n + 0,
+                           in.surf, in.n + 1, ub_s, C.P.mapping_plane_resolution, in.sstack, stack_n + 1);
     }
     in.stacks = false;
     in.stacks_pub = false;
@@ -1467,13 +1091,8 @@ void map_frame_launch(Ctx& C, int X) {
     k_map_update<<<1, 64, 0, st>>>(C.d_map, C.d_map_spread, std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS),
                                    C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS);
     if (g_exp & 4) {                 // (profiling experiment 4: skip the map update — results invalid)
-    } else if (g_rebuild_fused) {
-        rebuild_maps(C, in.cstack, in.sstack, stack_n, ub_c, ub_s);
     } else {
-        fork_lane1(C);
-        rebuild_map(C, 0, ub_c, in.cstack, stack_n + 0, C.P.mapping_line_resolution);
-        rebuild_map(C, 1, ub_s, in.sstack, stack_n + 1, C.P.mapping_plane_resolution);
-        join_lane1(C);
+        rebuild_maps(C, in.cstack, in.sstack, stack_n, ub_c, ub_s);
     }
     if (g_map_phases) map_phase(C, 3);
     if (in.nf > 0)

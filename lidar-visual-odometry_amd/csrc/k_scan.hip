@@ -14,6 +14,7 @@
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 #include "libm_f32.h"
+#include "pcl_sort.hpp"
 
 namespace aloam {
 
@@ -695,7 +696,7 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     }
     const int nc = s_ncand;
     LF_TS(3);
-    // ---- VoxelGrid(0.2) of the candidates (PCL 1.8 applyFilter), points summed in input order ----
+    // ---- VoxelGrid(0.2) of the candidates (PCL 1.8 applyFilter), points summed in PCL's order ----
     if (threadIdx.x < 6) s_bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     __syncthreads();
     {
@@ -728,34 +729,33 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
         divb[d] = maxb - minb[d] + 1;
     }
     const int mul1 = divb[0], mul2 = divb[0] * divb[1];
-    int n2 = 1;                            // big lines: power-of-two bitonic; LDS lines: multiple of 64
-    if (big) while (n2 < nc) n2 <<= 1;
-    else n2 = (nc + WAVE - 1) / WAVE * WAVE;
-    for (int t = threadIdx.x; t < n2; t += LT) {
-        unsigned long long key = ~0ull;
-        if (t < nc) {
-            int k = S[t];
-            unsigned idx;
-            if (overflow) idx = (unsigned)t;   // PCL copies the input through unchanged
-            else {
-                int i0 = (int)(floorf(X[k] * inv) - (float)minb[0]);
-                int i1 = (int)(floorf(Y[k] * inv) - (float)minb[1]);
-                int i2 = (int)(floorf(Z[k] * inv) - (float)minb[2]);
-                idx = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
-            }
-            key = ((unsigned long long)idx << 32) | (unsigned)t;
+    for (int t = threadIdx.x; t < nc; t += LT) {
+        const int k = S[t];
+        unsigned idx;
+        if (overflow) idx = (unsigned)t;   // PCL copies the input through unchanged
+        else {
+            int i0 = (int)(floorf(X[k] * inv) - (float)minb[0]);
+            int i1 = (int)(floorf(Y[k] * inv) - (float)minb[1]);
+            int i2 = (int)(floorf(Z[k] * inv) - (float)minb[2]);
+            idx = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
         }
-        keys[t] = key;
+        keys[t] = ((unsigned long long)idx << 32) | (unsigned)t;
     }
     __syncthreads();
     LF_TS(4);
+    // PCL's order of the (leaf, index) pairs: libstdc++ std::sort by leaf (pcl_sort.hpp). X / Y / Z are
+    // free from here on (the centroids read the cloud): they hold the stop positions and the segments;
+    // LDS lines keep the chunk scratch in the merge-sort buffer, big lines in their (unused) LDS arrays.
+    static_assert((size_t)LINE_LDS_CAP * 8 >= 4 * (size_t)ps_scratch_ints(LT), "chunk scratch in the sort buffer");
+    static_assert((size_t)LINE_LDS_CAP * 4 >= 4 * (size_t)ps_seg_ints(ps_segcap(LINE_LDS_CAP)), "segments in Z");
+    static_assert(line_lds_bytes() - LINE_HDR >= 4 * (size_t)ps_scratch_ints(LT), "big lines: chunk scratch in LDS");
     if (!big) {
-        if (n2 > 0 && block_merge_sort<unsigned long long, LINE_LDS_CAP / LT>(keys, sorted, n2) != keys) {
-            for (int t = threadIdx.x; t < n2; t += LT) keys[t] = sorted[t];
-            __syncthreads();
-        }
+        pcl_std_sort<LT, false>(keys, nc, (int*)X, (int*)Y, (int*)sorted, (int*)Z, ps_segcap(LINE_LDS_CAP));
+    } else if (nc <= LT * PS_MAX_CHUNK) {
+        pcl_std_sort<LT, true>(keys, nc, (int*)X, (int*)Y, (int*)smem, (int*)Z, ps_segcap(nc));
     } else {
-        bitonic_sort_u64(keys, n2);
+        if (threadIdx.x == 0) ps_serial_std_sort(keys, nc);
+        __syncthreads();
     }
     LF_TS(5);
     // run heads -> centroids; run r's head position stored in S[nc + r] region? reuse Cv as int
@@ -779,9 +779,8 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     LF_TS(6);
     for (int r = threadIdx.x; r < nrun; r += LT) {
         const int h0 = heads[r], h1 = (r + 1 < nrun) ? heads[r + 1] : nc;
-        int k = S[(int)(keys[h0] & 0xffffffffu)];
-        float4 c = cloud[off0 + k];
-        for (int t = h0 + 1; t < h1; t++) {
+        float4 c = make_float4(0.f, 0.f, 0.f, 0.f);      // CentroidPoint's accumulators start at zero
+        for (int t = h0; t < h1; t++) {
             float4 p = cloud[off0 + S[(int)(keys[t] & 0xffffffffu)]];
             c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
         }

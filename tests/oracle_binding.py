@@ -61,14 +61,16 @@ def lib():
         L.oracle_colpiv_qr_5x3.argtypes = [C.POINTER(C.c_double)] * 3
         L.oracle_introsort_keys.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]
         L.oracle_libstdcxx_sort_keys.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]
+        L.oracle_pcl_replay_check.argtypes = [C.c_int, C.c_int, C.c_ulonglong]
         _lib = L
     return _lib
 
 
 class Oracle:
-    """Three reference nodes' state in one object, same call surface as the HIP context."""
+    """Three reference nodes' state in one object, same call surface as the HIP context.
+    voxel_order 1 (default): PCL's VoxelGrid order (libstdc++ std::sort), the reference's; 0: stable."""
 
-    def __init__(self, params=None, voxel_order=0):
+    def __init__(self, params=None, voxel_order=1):
         self.p = params if params is not None else abi.default_params(64)
         self.h = lib().oracle_create(C.byref(self.p))
         lib().oracle_set_voxel_order(self.h, voxel_order)
@@ -183,7 +185,7 @@ def lm_solve(factors, x, max_iter=4):
     return x, (s.iterations, s.successful_steps, s.termination, s.num_residual_blocks, s.initial_cost, s.final_cost)
 
 
-def voxel_grid(pts, leaf, order=0):
+def voxel_grid(pts, leaf, order=1):
     pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 4)
     c, b = abi.make_cloud(len(pts))
     lib().oracle_voxel_grid(abi.fptr(pts), len(pts), leaf, order, C.byref(c))
@@ -213,6 +215,11 @@ def colpiv_qr_5x3(A, b):
     x = np.zeros(3)
     lib().oracle_colpiv_qr_5x3(abi.dptr(A), abi.dptr(b), abi.dptr(x))
     return x
+
+
+def pcl_replay_check(trials, max_n, seed=7):
+    """Mismatches of the level-parallel std::sort replay (the device algorithm's host twin) vs libstdc++."""
+    return lib().oracle_pcl_replay_check(trials, max_n, seed)
 
 
 def introsort_perm(keys, libstdcxx=False):

@@ -155,15 +155,36 @@ def test_knn_radius(gpu_ctx_factory):
 
 
 def test_voxel_grid_matches_pcl_semantics(gpu_ctx_factory):
+    """aloam_voxel_grid vs PCL 1.8's applyFilter (the oracle, order 1 = libstdc++ std::sort of the
+    (leaf, index) pairs): bit-exact centroids, across the device's three sort paths — in LDS (n <= 6144),
+    in global scratch (6144 < n <= ~63k), one-thread serial replay (beyond) — and degenerate key sets."""
     ctx = gpu_ctx_factory(64)
     pts = synth.scan("hdl64", 4)
     pts[:, 3] = np.arange(len(pts)) % 64 * 0.01
-    for leaf in (0.2, 0.4, 0.8):
-        vg = ctx.voxel_grid(pts, leaf)
-        vo = ob.voxel_grid(pts, leaf, order=0)
-        assert np.array_equal(bits(vg), bits(vo)), leaf
-        vp = ob.voxel_grid(pts, leaf, order=1)   # PCL's own (introsort) summation order
-        np.testing.assert_allclose(vg, vp, rtol=1e-5, atol=1e-5)
+    for n in (1, 2, 15, 16, 17, 300, 6144, 6145, 20000, 60000, len(pts)):
+        for leaf in ((0.2, 0.4, 0.8) if n in (300, 20000) else (0.4,)):
+            vg = ctx.voxel_grid(pts[:n], leaf)
+            vp = ob.voxel_grid(pts[:n], leaf, order=1)
+            assert vg.shape == vp.shape, (n, leaf)
+            assert np.array_equal(bits(vg), bits(vp)), (n, leaf)
+    rng = np.random.default_rng(11)
+    for case in ("one_leaf", "two_leaves", "sorted", "descending", "few_leaves"):
+        m = 5000
+        q = np.zeros((m, 4), np.float32)
+        if case == "one_leaf":
+            q[:, :3] = rng.uniform(0.01, 0.19, (m, 3))
+        elif case == "two_leaves":
+            q[:, :3] = rng.uniform(0.01, 0.19, (m, 3)) + (rng.integers(0, 2, (m, 1)) * 0.4)
+        elif case == "sorted":
+            q[:, 0] = np.arange(m) * 0.25 + 0.1
+        elif case == "descending":
+            q[:, 0] = (m - np.arange(m)) * 0.25 + 0.1
+        else:
+            q[:, :3] = rng.integers(0, 4, (m, 3)) * 0.2 + rng.uniform(0.01, 0.19, (m, 3))
+        q[:, 3] = rng.uniform(0, 1, m)
+        vg = ctx.voxel_grid(q, 0.2)
+        vp = ob.voxel_grid(q, 0.2, order=1)
+        assert np.array_equal(bits(vg), bits(vp)), case
 
 
 def teacher_forced_odometry_inputs(name, k):

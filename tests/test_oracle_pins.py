@@ -93,6 +93,14 @@ def test_introsort_replica_matches_libstdcxx(n, levels):
         assert np.array_equal(a, b)
 
 
+def test_level_parallel_sort_replay_matches_libstdcxx():
+    """The device computes PCL VoxelGrid's std::sort order level by level (csrc/pcl_sort.hpp: every
+    Hoare partition from its left / right stop sequences). Its host twin must leave exactly libstdc++'s
+    std::sort order on duplicate-heavy (leaf, index) arrays of every shape."""
+    assert ob.pcl_replay_check(2500, 6000, seed=7) == 0
+    assert ob.pcl_replay_check(20, 70000, seed=8) == 0
+
+
 @pytest.fixture(scope="module")
 def host_libm(tmp_path_factory):
     d = tmp_path_factory.mktemp("lm")
