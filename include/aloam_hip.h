@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ALOAM_ABI_VERSION 2
+#define ALOAM_ABI_VERSION 3
 
 /* error codes */
 #define ALOAM_OK             0
@@ -231,6 +231,26 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
 int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k,
                      float radius, int* d_idx, float* d_d2);
 
+/* TicToc stage names of the reference (printf'ed per scan), as indices of aloam_timing.tictoc_ms */
+#define ALOAM_TT_PREPARE            0   /* "prepare time"              scanRegistration.cpp:128-254 */
+#define ALOAM_TT_SEPARATE_POINTS    1   /* "seperate points time"      :269-410 (includes "sort q time" :287-289) */
+#define ALOAM_TT_SCAN_REGISTRATION  2   /* "scan registration time"    :127-456 */
+#define ALOAM_TT_DATA_ASSOCIATION   3   /* "data association time"     laserOdometry.cpp:382-564, summed over rounds */
+#define ALOAM_TT_SOLVER             4   /* "solver time"               :570-577, summed over rounds */
+#define ALOAM_TT_OPTIMIZATION_TWICE 5   /* "optimization twice time"   :363-579 */
+#define ALOAM_TT_PUBLICATION        6   /* "publication time"          :585-664 (compose, last clouds, kd-trees, publish) */
+#define ALOAM_TT_WHOLE_ODOMETRY     7   /* "whole laserOdometry time"  :353-665 */
+#define ALOAM_TT_MAP_PREPARE        8   /* "map prepare time"          laserMapping.cpp:311-552 (recentring, surround, stacks) */
+#define ALOAM_TT_BUILD_TREE         9   /* "build tree time"           :557-560 */
+#define ALOAM_TT_MAP_ASSOCIATION   10   /* "mapping data assosiation time" :574-710, summed over rounds */
+#define ALOAM_TT_MAP_SOLVER        11   /* "mapping solver time"       :712-721, summed over rounds */
+#define ALOAM_TT_MAP_OPTIMIZATION  12   /* "mapping optimization time" :556-728 */
+#define ALOAM_TT_ADD_POINTS        13   /* "add points time"           :736-784 (transformUpdate + insertion) */
+#define ALOAM_TT_FILTER            14   /* "filter time"               :787-802 */
+#define ALOAM_TT_MAPPING_PUB       15   /* "mapping pub time"          :804-850 (registered cloud) */
+#define ALOAM_TT_WHOLE_MAPPING     16   /* "whole mapping time"        :307-852 */
+#define ALOAM_TICTOC_N             17
+
 /* Timing of the last pipeline call, measured with HIP events on the context's stream. */
 typedef struct aloam_timing {
     float scan_registration_ms;
@@ -246,6 +266,9 @@ typedef struct aloam_timing {
     int   knn_launches;
     double knn_bytes;         /* its algorithmic bytes: sum_q (16 + 16 |C27(q)|) + 8 k Q         */
     double knn_streamed_bytes;/* bytes it actually streamed (both phases of the two-phase search)   */
+    /* the reference's TicToc stage surface (tic_toc.h; printed by the three nodes), GPU time of the
+     * same phases from HIP events on the stage's stream, indexed by ALOAM_TT_* below */
+    float tictoc_ms[ALOAM_TICTOC_N];
 } aloam_timing;
 int aloam_set_profiling(aloam_ctx* ctx, int enable);
 int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);

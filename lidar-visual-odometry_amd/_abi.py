@@ -130,7 +130,15 @@ class Timing(C.Structure):
         ("odom_search_launches", C.c_int), ("map_search_launches", C.c_int),
         ("map_search_bytes", C.c_double), ("odom_search_bytes", C.c_double),
         ("knn_ms", C.c_float), ("knn_launches", C.c_int), ("knn_bytes", C.c_double), ("knn_streamed_bytes", C.c_double),
+        ("tictoc_ms", C.c_float * 17),
     ]
+
+
+# the reference's TicToc stage names (include/aloam_hip.h ALOAM_TT_*), in tictoc_ms order
+TICTOC_NAMES = ["prepare time", "seperate points time", "scan registration time", "data association time", "solver time",
+                "optimization twice time", "publication time", "whole laserOdometry time", "map prepare time",
+                "build tree time", "mapping data assosiation time", "mapping solver time", "mapping optimization time",
+                "add points time", "filter time", "mapping pub time", "whole mapping time"]
 
 
 def fptr(a):

@@ -34,6 +34,9 @@ void* dalloc(Ctx& C, size_t bytes) {
 void prof_mark(Ctx& C, int idx) {
     if (C.profiling && C.ev_ready) HIPCHK(hipEventRecord(C.ev[idx], C.stream));
 }
+void prof_phase(Ctx& C, int k) {
+    if (C.profiling && C.ev_ready) HIPCHK(hipEventRecord(C.evp[k], C.stream));
+}
 
 __global__ void k_set2(int* dst, int a, int b) { dst[0] = a; dst[1] = b; }
 
@@ -249,6 +252,7 @@ static void allocate(Ctx& C) {
     std::memset(C.h_meta_pin, 0, sizeof(ScanMeta));
     for (auto& e : C.ev_mdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int i = 0; i < Ctx::NEV; i++) HIPCHK(hipEventCreate(&C.ev[i]));
+    for (int i = 0; i < Ctx::PM_N; i++) HIPCHK(hipEventCreate(&C.evp[i]));
     C.ev_ready = true;
     HIPCHK(hipStreamSynchronize(C.stream));   // all zero-fills and init kernels done
 }
@@ -299,6 +303,11 @@ static void sync(Ctx& C) {
 static float ev_ms(Ctx& C, int a, int b) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, C.ev[a], C.ev[b]) != hipSuccess) return 0.f;
+    return ms;
+}
+static float evh_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
     return ms;
 }
 
@@ -374,6 +383,10 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     if (C.profiling) {
         ensure_meta(C);
         C.timing.scan_registration_ms = ev_ms(C, 0, 1);
+        float* tt = C.timing.tictoc_ms;
+        tt[ALOAM_TT_PREPARE] = evh_ms(C.ev[0], C.evp[Ctx::PM_SCAN_PREP]);
+        tt[ALOAM_TT_SEPARATE_POINTS] = evh_ms(C.evp[Ctx::PM_SCAN_CURV], C.ev[1]);
+        tt[ALOAM_TT_SCAN_REGISTRATION] = C.timing.scan_registration_ms;
     }
     C.have_features = true;
     C.features_from_host = false;
@@ -456,6 +469,7 @@ static void do_odometry_issue(Ctx& C) {
             run_graph(C, slot, C.d_corner_last, C.d_surf_last, rounds, [&] { issue(false, hint); });
         }
         if (g_front_phases) front_phase(C, 3);
+        prof_phase(C, Ctx::PM_ODOM_ROUNDS_END);
         // pairs with build_last_grids(C, true) below; the new last-cloud counts from the device meta
         odom_compose(C, C.n_lsharp, C.n_lflat, pend ? C.d_meta->counts : nullptr);
         C.odom_spread_dirty = false;
@@ -569,10 +583,19 @@ static void do_odometry_complete(Ctx& C, aloam_odom_result* R) {
     }
     if (C.profiling) {
         C.timing.odometry_ms = ev_ms(C, 2, 3);
-        float s = 0;
-        for (int i = 0; i < r.rounds; i++) s += ev_ms(C, 6 + 2 * i, 7 + 2 * i);
+        float s = 0, sol = 0;
+        for (int i = 0; i < r.rounds; i++) {
+            s += ev_ms(C, 6 + 2 * i, 7 + 2 * i);
+            sol += i + 1 < r.rounds ? ev_ms(C, 7 + 2 * i, 6 + 2 * (i + 1)) : evh_ms(C.ev[7 + 2 * i], C.evp[Ctx::PM_ODOM_ROUNDS_END]);
+        }
         C.timing.odom_search_ms = s;
         C.timing.odom_search_launches = r.rounds;
+        float* tt = C.timing.tictoc_ms;
+        tt[ALOAM_TT_DATA_ASSOCIATION] = s;
+        tt[ALOAM_TT_SOLVER] = sol;
+        tt[ALOAM_TT_OPTIMIZATION_TWICE] = r.rounds ? evh_ms(C.ev[6], C.evp[Ctx::PM_ODOM_ROUNDS_END]) : 0.f;
+        tt[ALOAM_TT_PUBLICATION] = r.rounds ? evh_ms(C.evp[Ctx::PM_ODOM_ROUNDS_END], C.ev[3]) : C.timing.odometry_ms;
+        tt[ALOAM_TT_WHOLE_ODOMETRY] = C.timing.odometry_ms;
     }
     if (R) *R = r;
 }
@@ -680,9 +703,25 @@ void mapping_complete(Ctx& C, aloam_map_result* R) {
     for (int k = 0; k < 7; k++) (k < 4 ? r.q_w_curr[k] : r.t_w_curr[k - 4]) = C.h_map.parameters[k];
     if (C.profiling) {
         C.timing.mapping_ms = ev_ms(C, 4, 5);
-        float s = 0;
-        for (int i = 0; i < r.rounds; i++) s += ev_ms(C, 6 + 2 * (ALOAM_MAX_ROUNDS + i), 7 + 2 * (ALOAM_MAX_ROUNDS + i));
+        float s = 0, sol = 0;
+        const int M = ALOAM_MAX_ROUNDS;
+        for (int i = 0; i < r.rounds; i++) {
+            s += ev_ms(C, 6 + 2 * (M + i), 7 + 2 * (M + i));
+            sol += i + 1 < r.rounds ? ev_ms(C, 7 + 2 * (M + i), 6 + 2 * (M + i + 1))
+                                    : evh_ms(C.ev[7 + 2 * (M + i)], C.evp[Ctx::PM_MAP_ROUNDS_END]);
+        }
         C.timing.map_search_ms = s;
+        float* tt = C.timing.tictoc_ms;
+        tt[ALOAM_TT_MAP_PREPARE] = evh_ms(C.ev[4], C.evp[Ctx::PM_MAP_SHIFT]) +
+                                   evh_ms(C.evp[Ctx::PM_MAP_GRIDS], C.evp[Ctx::PM_MAP_ROUNDS_BEGIN]);
+        tt[ALOAM_TT_BUILD_TREE] = evh_ms(C.evp[Ctx::PM_MAP_SHIFT], C.evp[Ctx::PM_MAP_GRIDS]);
+        tt[ALOAM_TT_MAP_ASSOCIATION] = s;
+        tt[ALOAM_TT_MAP_SOLVER] = sol;
+        tt[ALOAM_TT_MAP_OPTIMIZATION] = evh_ms(C.evp[Ctx::PM_MAP_ROUNDS_BEGIN], C.evp[Ctx::PM_MAP_ROUNDS_END]);
+        tt[ALOAM_TT_ADD_POINTS] = evh_ms(C.evp[Ctx::PM_MAP_ROUNDS_END], C.evp[Ctx::PM_MAP_ADD]);
+        tt[ALOAM_TT_FILTER] = evh_ms(C.evp[Ctx::PM_MAP_ADD], C.evp[Ctx::PM_MAP_FILTER]);
+        tt[ALOAM_TT_MAPPING_PUB] = evh_ms(C.evp[Ctx::PM_MAP_FILTER], C.ev[5]);
+        tt[ALOAM_TT_WHOLE_MAPPING] = C.timing.mapping_ms;
         C.timing.map_search_launches = r.rounds;
         // B = sum_q [16 + 16 |C(q)|] + 8 k Q  (k = 5 neighbour slots of 4 B + d2)
         const double Q = (double)(stackn[0] + stackn[1]) * r.rounds;
@@ -935,6 +974,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->stream2) (void)hipStreamSynchronize(C->stream2);
     if (C->stream3) (void)hipStreamSynchronize(C->stream3);
     if (C->ev_ready) for (int i = 0; i < Ctx::NEV; i++) (void)hipEventDestroy(C->ev[i]);
+    if (C->ev_ready) for (int i = 0; i < Ctx::PM_N; i++) (void)hipEventDestroy(C->evp[i]);
     for (auto& g : C->graphs) if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);

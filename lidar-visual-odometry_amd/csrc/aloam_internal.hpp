@@ -257,6 +257,10 @@ struct Ctx {
     // profiling events: [0..1] scan, [2..3] odom, [4..5] map, search pairs after that
     static constexpr int NEV = 6 + 4 * ALOAM_MAX_ROUNDS + 2;   // last two: aloam_knn_device
     hipEvent_t ev[NEV];
+    // phase boundaries inside a stage (profiling only) for the TicToc stage surface (ALOAM_TT_*)
+    enum PhaseMark { PM_SCAN_PREP, PM_SCAN_CURV, PM_ODOM_ROUNDS_END, PM_MAP_SHIFT, PM_MAP_GRIDS, PM_MAP_ROUNDS_BEGIN,
+                     PM_MAP_ROUNDS_END, PM_MAP_ADD, PM_MAP_FILTER, PM_N };
+    hipEvent_t evp[PM_N];
     KindScratch ks[2];
     DevOut* d_out = nullptr;         // device results block (d_odom, d_round_cnt, ... point into it)
     DevOut* h_out = nullptr;         // pinned host mirror
@@ -352,6 +356,7 @@ void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so f
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
 void map_frame_launch(Ctx& C, int input_set);
 void* dalloc(Ctx& C, size_t bytes);
+void prof_phase(Ctx& C, int k);     // records evp[k] on C.stream when profiling
 // the odometry -> mapping hand-off as a value: published buffers (valid until the publish after next),
 // counts and pose; the native pipeline forwards it from its mapping thread (aloam_api.hip)
 struct MapSnapshot {

@@ -967,9 +967,11 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     k_rb_insert<<<dim3(nblk(std::max(n_old, ub)), 2), MB, 0, st>>>(P, C.d_map);
     k_rb_sort_scan<<<2, RBS_T, RBS_LDS, st>>>(P, C.d_cube_valid);
     k_rb_scatter<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P);
+    prof_phase(C, Ctx::PM_MAP_ADD);
     k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
     k_rb_final_scan<<<2, 1024, 0, st>>>(P, C.d_cube_valid);
     k_rb_final<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P, C.d_cube_valid);
+    prof_phase(C, Ctx::PM_MAP_FILTER);
     HIPCHK(hipGetLastError());
 }
 
@@ -1036,10 +1038,12 @@ void map_frame_launch(Ctx& C, int X) {
     if (g_map_phases) map_phase(C, 0);
     k_map_prepare<<<1, 256, 0, st>>>(C.d_map, C.d_cube_valid, C.d_map_spread, in.pose);
     k_map_shift<<<dim3(nblk(std::max(C.n_mc, C.n_ms)), 2), MB, 0, st>>>(C.d_mc_cube, C.d_ms_cube, C.d_map_n, C.d_map);
+    prof_phase(C, Ctx::PM_MAP_SHIFT);
     const GridBuild gb[2] = {{&C.g_map_corner, C.d_mc, C.d_map_n + 0, std::max(C.n_mc, 1), C.d_mc_cube, C.d_cube_valid},
                              {&C.g_map_surf, C.d_ms, C.d_map_n + 1, std::max(C.n_ms, 1), C.d_ms_cube, C.d_cube_valid}};
     grid_build_multi(C, gb, 2);
     k_map_gate<<<1, 1, 0, st>>>(C.d_map, C.g_map_corner.desc, C.g_map_surf.desc);
+    prof_phase(C, Ctx::PM_MAP_GRIDS);
     // stacks (:542-550): voxelised on stream3 when the input came as a hand-off, else here in two lanes
     if (deferred) {
         forward_stacks_pending(C, X);
@@ -1057,6 +1061,7 @@ void map_frame_launch(Ctx& C, int X) {
     in.stacks_pub = false;
     const int nq = ub_c + ub_s;
     if (g_map_phases) map_phase(C, 1);
+    prof_phase(C, Ctx::PM_MAP_ROUNDS_BEGIN);
     C.t_rounds_issued = std::chrono::steady_clock::now();
     if (nq > 0) {
         if (nq > C.cap_factors) throw ApiError{ALOAM_E_CAPACITY, "factor capacity exceeded"};
@@ -1088,6 +1093,7 @@ void map_frame_launch(Ctx& C, int X) {
         else run_graph(C, 2 + X, in.cstack, in.sstack, rounds, [&] { issue(false, hint); });
     }
     if (g_map_phases) map_phase(C, 2);
+    prof_phase(C, Ctx::PM_MAP_ROUNDS_END);
     k_map_update<<<1, 64, 0, st>>>(C.d_map, C.d_map_spread, std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS),
                                    C.d_round_cnt + 2 * ALOAM_MAX_ROUNDS);
     if (g_exp & 4) {                 // (profiling experiment 4: skip the map update — results invalid)

@@ -876,7 +876,9 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
                                              C.d_sid, C.d_ori, C.d_hist, nb, C.d_meta);
         k_bucket_scan<<<N_SCANS, BK_T, 0, st>>>(C.d_hist, nb, N_SCANS, C.d_meta, C.d_hoff);
         k_bucket_scatter<<<nb, SB, 0, st>>>(C.d_cl, C.d_meta, C.d_sid, C.d_ori, C.d_hoff, nb, N_SCANS, C.d_cloud);
+        prof_phase(C, Ctx::PM_SCAN_PREP);
         k_curvature<<<nb, SB, 0, st>>>(C.d_cloud, C.d_meta, C.d_curv);
+        prof_phase(C, Ctx::PM_SCAN_CURV);
         const size_t lds = line_lds_bytes();
         k_line_features<<<N_SCANS, LT, lds, st>>>(C.d_cloud, C.d_curv, C.d_meta, N_SCANS, C.d_scratch_xyz,
                                                   C.d_scratch_keys, C.d_scratch_i, C.d_line_sharp, C.d_line_lsharp,
@@ -884,6 +886,9 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
         k_concat<<<N_SCANS, 256, 0, st>>>(C.d_cloud, C.d_line_sharp, C.d_line_lsharp, C.d_line_flat, C.d_line_cnt,
                                           C.d_line_lf, N_SCANS, C.d_meta, C.d_sharp, C.d_sharp_idx, C.d_lsharp,
                                           C.d_lsharp_idx, C.d_flat, C.d_flat_idx, C.d_lflat, C.d_odom_nq);
+    } else {
+        prof_phase(C, Ctx::PM_SCAN_PREP);
+        prof_phase(C, Ctx::PM_SCAN_CURV);
     }
     HIPCHK(hipGetLastError());
 }

@@ -24,9 +24,12 @@ constexpr int VX_SEGCAP_LDS = ps_segcap(VX_LDS_N);
 constexpr int VX_SEGCAP_G = (int)((160 * 1024 - 64 - 4 * (size_t)VX_SC) / (4 * 9));
 constexpr int VX_NMAX = (VX_SEGCAP_G - 1) * (PS_THRESHOLD + 1) < VX_T * PS_MAX_CHUNK ? (VX_SEGCAP_G - 1) * (PS_THRESHOLD + 1) : VX_T * PS_MAX_CHUNK;
 constexpr size_t VX_HDR = 64;
-constexpr size_t VX_LDS = VX_HDR + 4 * (size_t)VX_SC + 16 * (size_t)VX_LDS_N + 4 * (size_t)ps_seg_ints(VX_SEGCAP_LDS);
+// launch size: the larger of the two layouts (LDS mode: keys + stop positions + segments; global mode:
+// the segments of up to VX_NMAX points)
+constexpr size_t VX_LDS_A = VX_HDR + 4 * (size_t)VX_SC + 16 * (size_t)VX_LDS_N + 4 * (size_t)ps_seg_ints(VX_SEGCAP_LDS);
+constexpr size_t VX_LDS_B = VX_HDR + 4 * (size_t)VX_SC + 4 * (size_t)ps_seg_ints(VX_SEGCAP_G);
+constexpr size_t VX_LDS = VX_LDS_A > VX_LDS_B ? VX_LDS_A : VX_LDS_B;
 static_assert(VX_LDS <= 160 * 1024, "LDS");
-static_assert(VX_HDR + 4 * (size_t)VX_SC + 4 * (size_t)ps_seg_ints(VX_SEGCAP_G) <= 160 * 1024, "LDS (global mode)");
 static_assert(ps_segcap(VX_NMAX) <= VX_SEGCAP_G, "segments");
 
 struct VoxJob {

@@ -306,7 +306,7 @@ __device__ void pcl_std_sort(unsigned long long* E, const int n, int* Lpos, int*
             }
             BL[s] = bL; TR[s] = eR; KK[s] = k; CUT[s] = cut;
         }
-        lds_barrier();
+        ps_bar<G>();                             // (the segment arrays may be in global memory)
         // (4) the swaps: left stop j <-> right stop j for j < k (disjoint pairs, one thread each)
         if (tid < nch && mL) {
             int s = sidx[tid];

@@ -47,6 +47,7 @@ def lib():
         L.oracle_process_scan.argtypes = [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(abi.OdomResult),
                                           C.POINTER(abi.MapResult)]
         L.oracle_stage_times.argtypes = [vp, C.POINTER(C.c_double)]
+        L.oracle_tictoc.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_get_map_cloud.argtypes = [vp, C.c_int, C.POINTER(abi.Cloud)]
         L.oracle_get_registered_cloud.argtypes = [vp, C.POINTER(abi.Cloud)]
         L.oracle_eval_factors.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int,
@@ -154,6 +155,12 @@ class Oracle:
         t = (C.c_double * 3)()
         lib().oracle_stage_times(self.h, t)
         return list(t)
+
+    def tictoc(self):
+        """The reference's TicToc stage times (ms) of the last calls, keyed by the printed names."""
+        t = (C.c_double * len(abi.TICTOC_NAMES))()
+        lib().oracle_tictoc(self.h, t)
+        return dict(zip(abi.TICTOC_NAMES, list(t)))
 
     def map_cloud(self, which, cap=4_000_000):
         c, b = abi.make_cloud(cap)
