@@ -480,6 +480,9 @@ def main():
             m = min(len(otraj), len(traj))
             ate = float(np.sqrt(np.mean(np.sum((np.array(traj[:m]) - np.array(otraj[:m])) ** 2, axis=1))))
             result["ate_delta_vs_oracle_m"] = ate
+            # the oracle's VoxelGrids sum every leaf in PCL 1.8's order (libstdc++ std::sort of the (leaf,
+            # index) pairs), the order the device reproduces (csrc/pcl_sort.hpp)
+            result["ate_delta_vs_pcl_order_m"] = ate
             result["ate_frames"] = m
             result["gpu_vs_cpu"] = round(value / world / cpu_value, 2) if cpu_value else None
             result["gpu_vs_cpu_box"] = round(value / world / cb["box"]["scans_per_s"], 2)

@@ -353,7 +353,7 @@ class Context:
     def timing(self):
         t = abi.Timing()
         self._check(lib().aloam_get_timing(self.h, C.byref(t)))
-        return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
+        return abi.timing_to_dict(t)
 
 
 def s2m_register_group(contexts, x):
@@ -418,7 +418,7 @@ class Pipeline:
     def _timing(self, stage):
         t = abi.Timing()
         self._check(lib().aloam_pipeline_timing(self.h, stage, C.byref(t)))
-        return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
+        return abi.timing_to_dict(t)
 
     def set_profiling(self, on):
         self._check(lib().aloam_pipeline_set_profiling(self.h, int(on)))

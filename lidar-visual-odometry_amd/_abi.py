@@ -134,6 +134,13 @@ class Timing(C.Structure):
     ]
 
 
+def timing_to_dict(t):
+    """aloam_timing -> dict (tictoc_ms as a list in ALOAM_TT_* order, see TICTOC_NAMES)."""
+    d = {k: getattr(t, k) for k, _ in Timing._fields_}
+    d["tictoc_ms"] = list(d["tictoc_ms"])
+    return d
+
+
 # the reference's TicToc stage names (include/aloam_hip.h ALOAM_TT_*), in tictoc_ms order
 TICTOC_NAMES = ["prepare time", "seperate points time", "scan registration time", "data association time", "solver time",
                 "optimization twice time", "publication time", "whole laserOdometry time", "map prepare time",

@@ -31,6 +31,17 @@ void* dalloc(Ctx& C, size_t bytes) {
     return p;
 }
 
+void dfree(Ctx& C, void* p) {
+    if (!p) return;
+    HIPCHK(hipStreamSynchronize(C.stream));      // launches queued on the context's stream may still use it
+    for (size_t i = 0; i < C.bufs.size(); i++)
+        if (C.bufs[i].p == p) {
+            C.bufs.erase(C.bufs.begin() + (long)i);
+            break;
+        }
+    HIPCHK(hipFree(p));
+}
+
 void prof_mark(Ctx& C, int idx) {
     if (C.profiling && C.ev_ready) HIPCHK(hipEventRecord(C.ev[idx], C.stream));
 }
@@ -420,6 +431,7 @@ static void build_last_grids(Ctx& C, bool flags_preset = false, int cap_c = -1, 
 static void do_odometry_issue(Ctx& C) {
     if (!C.have_features) throw ApiError{ALOAM_E_STATE, "odometry before any features"};
     if (C.fp_active) throw ApiError{ALOAM_E_STATE, "an issued odometry scan has not been completed"};
+    if (!C.front_failed.empty()) throw ApiError{ALOAM_E_STATE, "context unusable after a failed publish: " + C.front_failed};
     aloam_odom_result r{};
     hipStream_t st = C.stream;
     prof_mark(C, 2);
@@ -510,7 +522,18 @@ static void do_odometry_issue(Ctx& C) {
         j.counts = m.n;
         j.pose_dst = m.pose;
         j.pose_src = C.d_odom->q_w;                    // q_w[4], t_w[3] adjacent (OdomState)
-        if (C.pre_publish) { auto f = std::move(C.pre_publish); C.pre_publish = nullptr; f(); }
+        if (C.pre_publish) {
+            // the hand-off wait runs after this scan's rounds and compose were queued: a failure here
+            // leaves the front half-advanced, so the context refuses further scans instead of continuing
+            auto f = std::move(C.pre_publish);
+            C.pre_publish = nullptr;
+            try {
+                f();
+            } catch (const HipError& e) {
+                C.front_failed = e.msg;
+                throw;
+            }
+        }
         const int live = std::max(std::max(C.stack_hint[0], C.stack_hint[1]), 1);   // grid-stride copy: any size is correct
         k_forward_map_input<<<dim3(std::max(1, std::min(1024, (std::min(live, std::max(cap_s, cap_c)) + 255) / 256)), 3), 256, 0, st>>>(j);
         HIPCHK(hipGetLastError());
@@ -1337,9 +1360,11 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
     const char* fe = getenv("ALOAM_KNN_FINE");    // read per call (tests compare both paths in one process)
     const float fine_frac = fe ? (float)atof(fe) : 0.3f;
     const bool two_phase = fine_frac > 0.f && fine_frac < 1.f;
-    if (two_phase && C.g_knn_fine.cap < std::max(n, 1)) {
+    if (two_phase && C.g_knn_fine.cap < std::max(n, 1)) {   // grown on demand (the old grid given back)
+        const int cap = std::max(std::max(n, 1), C.g_knn_fine.cap * 2);
+        if (C.g_knn_fine.cap) grid_free(C, C.g_knn_fine);
         Grid g{};
-        grid_alloc(C, g, std::max(std::max(n, 1), C.g_knn_fine.cap * 2), radius * fine_frac, 1, true);
+        grid_alloc(C, g, cap, radius * fine_frac, 1, true);
         C.g_knn_fine = g;
     }
     set_counts2(C, C.d_knn_n, n, 0);

@@ -283,6 +283,7 @@ struct Ctx {
     struct FrontPend { aloam_odom_result r; bool pend; int t, hint_c, hint_s; };
     FrontPend fp{};
     bool fp_active = false;
+    std::string front_failed;      // a publish's hand-off wait failed mid-scan: the front state is half-advanced
     // run right before the next publish launch (2-stage pipeline: wait until the mapping stage has copied
     // the hand-off that last used the target input set), then cleared; the scan's registration and
     // odometry rounds are queued by then, so the wait holds back the publish only
@@ -356,6 +357,8 @@ void fork_lane1(Ctx& C);   // stream2 waits for everything queued on stream so f
 void join_lane1(Ctx& C);   // stream waits for everything queued on stream2 so far
 void map_frame_launch(Ctx& C, int input_set);
 void* dalloc(Ctx& C, size_t bytes);
+void dfree(Ctx& C, void* p);           // a dalloc'd buffer given back (after the context's stream drains)
+void grid_free(Ctx& C, Grid& g);
 void prof_phase(Ctx& C, int k);     // records evp[k] on C.stream when profiling
 // the odometry -> mapping hand-off as a value: published buffers (valid until the publish after next),
 // counts and pose; the native pipeline forwards it from its mapping thread (aloam_api.hip)

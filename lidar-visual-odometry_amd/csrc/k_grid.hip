@@ -145,6 +145,12 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_in
     HIPCHK(hipGetLastError());
 }
 
+void grid_free(Ctx& C, Grid& g) {
+    for (void* p : {(void*)g.desc, (void*)g.cell_count, (void*)g.cell_start, (void*)g.blk, (void*)g.pts, (void*)g.idx, (void*)g.pcell})
+        dfree(C, p);
+    g = Grid{};
+}
+
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of,
                 const unsigned char* cube_valid) {
     const GridBuild b{&g, pts, d_n, cap_n, cube_of, cube_valid};

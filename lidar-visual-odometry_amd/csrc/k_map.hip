@@ -471,7 +471,8 @@ void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0
     const char* spe = getenv("ALOAM_S2M_SPLIT");
     if (s1 - s0 >= batch_min && !(spe && atoi(spe) == 0)) {
         const int n = s1 - s0;
-        if (C.cap_s2m_nbr < n) {         // grown on demand, released with the context
+        if (C.cap_s2m_nbr < n) {         // grown on demand (the old buffer given back)
+            dfree(C, C.d_s2m_nbr);
             C.cap_s2m_nbr = std::max(n, 2 * C.cap_s2m_nbr);
             C.d_s2m_nbr = (int*)dalloc(C, sizeof(int) * S2M_NBR * (size_t)C.cap_s2m_nbr);
         }
@@ -576,10 +577,9 @@ __global__ void k_map_register(const float4* __restrict__ full, int n, const Map
 // leaf is summed from zero in that order (CentroidPoint), so the cube's new points equal PCL's bit for
 // bit. Cubes up to RBV_CAP points sort in LDS, larger ones in the cube's global scratch.
 constexpr int RBV_T = 1024;
-constexpr int RBV_CAP = 7168;        // cube points sorted in LDS (more: global scratch)
-constexpr int RBV_SC = ps_scratch_ints(RBV_T);
+constexpr int RBV_CAP = 14336;       // cube points sorted in LDS (more: global scratch)
 constexpr size_t RBV_HDR = 64;
-constexpr size_t RBV_LDS = RBV_HDR + 4 * (size_t)RBV_SC + 16 * (size_t)RBV_CAP + 4 * (size_t)ps_seg_ints(ps_segcap(RBV_CAP));
+constexpr size_t RBV_LDS = RBV_HDR + 8 * (size_t)RBV_CAP + 4 * (size_t)ps_scratch_ints_global(RBV_T, RBV_CAP);
 constexpr int RBV_PER = 8;           // points per thread held in registers for the bbox and the keys
 static_assert(RBV_LDS <= 160 * 1024, "LDS");
 struct RbvShared { unsigned bb[6]; int bad; int pad; };
@@ -588,22 +588,12 @@ template <bool FITS>
 __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n,
                                          float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr, const int* fb) {
     RbvShared& SH = *(RbvShared*)smem;
-    int* sc = (int*)(smem + RBV_HDR);
     const int tid = threadIdx.x;
-    unsigned long long* gseg = gscr + 4 * (size_t)p0;      // 4 u64 per point: keys, stop positions, segments
-    unsigned long long* E;
-    int *Lp, *Rp, *seg;
-    if (FITS) {
-        E = (unsigned long long*)(smem + RBV_HDR + 4 * (size_t)RBV_SC);
-        Lp = (int*)(E + RBV_CAP);
-        Rp = Lp + RBV_CAP;
-        seg = Rp + RBV_CAP;
-    } else {
-        E = gseg;
-        Lp = (int*)(gseg + n);
-        Rp = Lp + n;
-        seg = (int*)(gseg + 2 * (size_t)n);
-    }
+    // keys in LDS when the cube fits, else in the cube's global scratch (staged through the same LDS
+    // buffer by the sort); the sort's scratch behind the buffer
+    unsigned long long* EL = (unsigned long long*)(smem + RBV_HDR);
+    unsigned long long* E = FITS ? EL : gscr + 4 * (size_t)p0;
+    int* sc = (int*)(smem + RBV_HDR + 8 * (size_t)RBV_CAP);
     RBSTAMP(0);
     if (tid < 6) SH.bb[tid] = tid < 3 ? 0xffffffffu : 0u;
     if (tid == 0) SH.bad = 0;
@@ -684,8 +674,10 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     }
     if (FITS) lds_barrier(); else __syncthreads();
     RBSTAMP(1);
-    if (n <= RBV_T * PS_MAX_CHUNK) {
-        pcl_std_sort<RBV_T, !FITS>(E, n, Lp, Rp, sc, seg, FITS ? ps_segcap(RBV_CAP) : ps_segcap(n));
+    if (FITS) {
+        pcl_std_sort<RBV_T, true>(E, n, sc, RBV_CAP);
+    } else if (n <= RBV_T * PS_MAX_CHUNK) {
+        pcl_std_sort_global<RBV_T>(E, n, EL, RBV_CAP, sc);
     } else {                                  // beyond the parallel replay's reach: one thread
         if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();
@@ -698,7 +690,7 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     int nh = 0;
     for (int q = q0; q < q1; q++) nh += (q == 0 || ps_key(E[q]) != ps_key(E[q - 1]));
     int run = nh, dummy = 0, tot, td;
-    ps_exscan2<RBV_T>(run, dummy, sc + 8, tot, td);
+    ps_exscan2<RBV_T>(run, dummy, sc + 16, tot, td);
     for (int q = q0; q < q1; q++) {
         const unsigned k = ps_key(E[q]);
         if (!(q == 0 || k != ps_key(E[q - 1]))) continue;

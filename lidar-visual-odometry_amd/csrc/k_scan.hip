@@ -743,16 +743,16 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     }
     __syncthreads();
     LF_TS(4);
-    // PCL's order of the (leaf, index) pairs: libstdc++ std::sort by leaf (pcl_sort.hpp). X / Y / Z are
-    // free from here on (the centroids read the cloud): they hold the stop positions and the segments;
-    // LDS lines keep the chunk scratch in the merge-sort buffer, big lines in their (unused) LDS arrays.
-    static_assert((size_t)LINE_LDS_CAP * 8 >= 4 * (size_t)ps_scratch_ints(LT), "chunk scratch in the sort buffer");
-    static_assert((size_t)LINE_LDS_CAP * 4 >= 4 * (size_t)ps_seg_ints(ps_segcap(LINE_LDS_CAP)), "segments in Z");
-    static_assert(line_lds_bytes() - LINE_HDR >= 4 * (size_t)ps_scratch_ints(LT), "big lines: chunk scratch in LDS");
+    // PCL's order of the (leaf, index) pairs: libstdc++ std::sort by leaf (pcl_sort.hpp); LDS lines keep
+    // the sort's scratch in the merge-sort buffer, big lines in their (unused) LDS arrays.
+    static_assert((size_t)LINE_LDS_CAP * 8 >= 4 * (size_t)ps_scratch_ints(LT, LINE_LDS_CAP, false), "sort scratch in the sort buffer");
+    static_assert(LINE_LDS_CAP <= PS_WMAX, "LDS lines are one wave segment");
+    constexpr int LINE_STAGE = 12288;      // big lines: sort segments staged through the (unused) LDS arrays
+    static_assert(line_lds_bytes() - LINE_HDR >= 8 * (size_t)LINE_STAGE + 4 * (size_t)ps_scratch_ints_global(LT, LINE_STAGE), "big lines: sort staging in LDS");
     if (!big) {
-        pcl_std_sort<LT, false>(keys, nc, (int*)X, (int*)Y, (int*)sorted, (int*)Z, ps_segcap(LINE_LDS_CAP));
+        pcl_std_sort<LT, false>(keys, nc, (int*)sorted, LINE_LDS_CAP);
     } else if (nc <= LT * PS_MAX_CHUNK) {
-        pcl_std_sort<LT, true>(keys, nc, (int*)X, (int*)Y, (int*)smem, (int*)Z, ps_segcap(nc));
+        pcl_std_sort_global<LT>(keys, nc, (unsigned long long*)smem, LINE_STAGE, (int*)(smem + 8 * (size_t)LINE_STAGE));
     } else {
         if (threadIdx.x == 0) ps_serial_std_sort(keys, nc);
         __syncthreads();
@@ -779,11 +779,8 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     LF_TS(6);
     for (int r = threadIdx.x; r < nrun; r += LT) {
         const int h0 = heads[r], h1 = (r + 1 < nrun) ? heads[r + 1] : nc;
-        float4 c = make_float4(0.f, 0.f, 0.f, 0.f);      // CentroidPoint's accumulators start at zero
-        for (int t = h0; t < h1; t++) {
-            float4 p = cloud[off0 + S[(int)(keys[t] & 0xffffffffu)]];
-            c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
-        }
+        int nrs;                                          // CentroidPoint: from zero, in sorted order
+        const float4 c = ps_run_sum(keys, nc, h0, ps_key(keys[h0]), [&](int i) { return cloud[off0 + S[i]]; }, nrs);
         const float cnt = (float)(h1 - h0);
         line_lf[off0 + r] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
     }

@@ -12,38 +12,50 @@
 
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
+#ifdef ALOAM_PS_TIMING           // profiling builds only: per-level stamps of the sort of workgroup 0
+__device__ unsigned long long g_ps_ts[64][6];
+__device__ int g_ps_nseg[64];
+#define PS_TS(level, k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && (level) < 64) { g_ps_ts[level][k] = wall_clock64(); if ((k) == 0) g_ps_nseg[level] = hdr[(level) == 60 ? 2 : 0]; } } while (0)
+__device__ unsigned long long g_ps_w[16][8];
+#define PS_CLK() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#define PS_WSTAT(slot, v) do { if (blockIdx.x == 0) { auto& w_ = g_ps_w[threadIdx.x / 64][slot]; w_ = w_ + (unsigned long long)(v); } } while (0)
+// per-wave counters of workgroup 0's wave phase (cycles waiting, partitioning, #partitions, elements
+// partitioned, cycles in leaves, #leaves), accumulated since the last call; read and cleared
+extern "C" int aloam_dbg_ps_w(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ps_w), sizeof(g_ps_w)) != hipSuccess) return -1;
+    static unsigned long long zero[16][8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ps_w), zero, sizeof(zero));
+}
+extern "C" int aloam_dbg_ps_ts(unsigned long long* out, int* nseg) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ps_ts), sizeof(g_ps_ts)) != hipSuccess) return -1;
+    return (int)hipMemcpyFromSymbol(nseg, HIP_SYMBOL(g_ps_nseg), sizeof(g_ps_nseg));
+}
+#endif
 #include "pcl_sort.hpp"
 
 namespace aloam {
 
 constexpr int VX_T = 1024;
-constexpr int VX_LDS_N = 6144;                              // clouds up to this size are sorted in LDS
-constexpr int VX_SC = ps_scratch_ints(VX_T);
-constexpr int VX_SEGCAP_LDS = ps_segcap(VX_LDS_N);
-// global mode: the segments stay in LDS, which bounds the parallel replay at VX_NMAX points
-constexpr int VX_SEGCAP_G = (int)((160 * 1024 - 64 - 4 * (size_t)VX_SC) / (4 * 9));
-constexpr int VX_NMAX = (VX_SEGCAP_G - 1) * (PS_THRESHOLD + 1) < VX_T * PS_MAX_CHUNK ? (VX_SEGCAP_G - 1) * (PS_THRESHOLD + 1) : VX_T * PS_MAX_CHUNK;
+constexpr int VX_LDS_N = 14336;                             // clouds up to this size are sorted in LDS
+constexpr int VX_NMAX = VX_T * PS_MAX_CHUNK;                // parallel replay up to this size (beyond: one thread)
 constexpr size_t VX_HDR = 64;
-// launch size: the larger of the two layouts (LDS mode: keys + stop positions + segments; global mode:
-// the segments of up to VX_NMAX points)
-constexpr size_t VX_LDS_A = VX_HDR + 4 * (size_t)VX_SC + 16 * (size_t)VX_LDS_N + 4 * (size_t)ps_seg_ints(VX_SEGCAP_LDS);
-constexpr size_t VX_LDS_B = VX_HDR + 4 * (size_t)VX_SC + 4 * (size_t)ps_seg_ints(VX_SEGCAP_G);
-constexpr size_t VX_LDS = VX_LDS_A > VX_LDS_B ? VX_LDS_A : VX_LDS_B;
+constexpr size_t VX_LDS = VX_HDR + 8 * (size_t)VX_LDS_N + 4 * (size_t)ps_scratch_ints_global(VX_T, VX_LDS_N);
 static_assert(VX_LDS <= 160 * 1024, "LDS");
-static_assert(ps_segcap(VX_NMAX) <= VX_SEGCAP_G, "segments");
 
 struct VoxJob {
     const float4* pts; const int* d_n; int cap; float leaf;
     float4* out; int* d_nout;
-    unsigned long long* gE; int* gL; int* gR;   // global scratch (cap_voxel each): keys, stop positions
+    unsigned long long* gE;      // global scratch (cap_voxel keys) for clouds above VX_LDS_N
 };
 struct VoxJobs { VoxJob j[2]; };
 
-template <bool G>
-__device__ void vox_sort_and_reduce(const VoxJob& J, int n, unsigned long long* E, int* Lp, int* Rp, int* sc, int* seg, int segcap) {
+// E: the keys (LDS: EL itself; global: gE, staged through EL by the sort); sc behind EL
+__device__ void vox_sort_and_reduce(const VoxJob& J, int n, unsigned long long* E, unsigned long long* EL, int* sc) {
     const int tid = threadIdx.x;
-    if (n <= VX_NMAX) {
-        pcl_std_sort<VX_T, G>(E, n, Lp, Rp, sc, seg, segcap);
+    if (E == EL) {
+        pcl_std_sort<VX_T, true>(E, n, sc, VX_LDS_N);
+    } else if (n <= VX_NMAX) {
+        pcl_std_sort_global<VX_T>(E, n, EL, VX_LDS_N, sc);
     } else {                                                  // beyond the parallel replay's reach: one thread
         if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();
@@ -55,17 +67,12 @@ __device__ void vox_sort_and_reduce(const VoxJob& J, int n, unsigned long long* 
     for (int p = p0; p < p1; p++) nh += (p == 0 || ps_key(E[p]) != ps_key(E[p - 1]));
     int run, dummy = 0, tot, td;
     run = nh;
-    ps_exscan2<VX_T>(run, dummy, sc + 8, tot, td);
+    ps_exscan2<VX_T>(run, dummy, sc + 16, tot, td);
     for (int p = p0; p < p1; p++) {
         const unsigned k = ps_key(E[p]);
         if (!(p == 0 || k != ps_key(E[p - 1]))) continue;
-        float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-        int cnt = 0;
-        for (int t = p; t < n && ps_key(E[t]) == k; t++) {
-            const float4 q = J.pts[(int)(E[t] & 0xffffffffu)];
-            c.x += q.x; c.y += q.y; c.z += q.z; c.w += q.w;
-            cnt++;
-        }
+        int cnt;
+        const float4 c = ps_run_sum(E, n, p, k, [&](int i) { return J.pts[i]; }, cnt);
         const float fc = (float)cnt;
         J.out[run] = make_float4(c.x / fc, c.y / fc, c.z / fc, c.w / fc);
         run++;
@@ -77,7 +84,8 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const VoxJob& J = P.j[blockIdx.x];
     unsigned* bb = (unsigned*)smem;
-    int* sc = (int*)(smem + VX_HDR);
+    unsigned long long* EL = (unsigned long long*)(smem + VX_HDR);   // keys, or the staging buffer
+    int* sc = (int*)(EL + VX_LDS_N);
     const int tid = threadIdx.x;
     // a hinted launch never reads past its launch size (the exact-size redo replaces the result)
     const int n = min(*J.d_n, J.cap);
@@ -108,23 +116,10 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P) {
         return;
     }
     const float inv = 1.0f / J.leaf;
-    if (n <= VX_LDS_N) {
-        unsigned long long* E = (unsigned long long*)(smem + VX_HDR + 4 * (size_t)VX_SC);
-        int* Lp = (int*)(E + VX_LDS_N);
-        int* Rp = Lp + VX_LDS_N;
-        int* seg = Rp + VX_LDS_N;
-        for (int t = tid; t < n; t += VX_T) E[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
-        lds_barrier();
-        vox_sort_and_reduce<false>(J, n, E, Lp, Rp, sc, seg, VX_SEGCAP_LDS);
-    } else {
-        unsigned long long* E = J.gE;
-        int* Lp = J.gL;
-        int* Rp = J.gR;
-        int* seg = (int*)(smem + VX_HDR + 4 * (size_t)VX_SC);
-        for (int t = tid; t < n; t += VX_T) E[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
-        __syncthreads();
-        vox_sort_and_reduce<true>(J, n, E, Lp, Rp, sc, seg, VX_SEGCAP_G);
-    }
+    unsigned long long* E = n <= VX_LDS_N ? EL : J.gE;
+    for (int t = tid; t < n; t += VX_T) E[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
+    __syncthreads();
+    vox_sort_and_reduce(J, n, E, EL, sc);
 }
 
 static void vox_attr() {
@@ -135,13 +130,12 @@ static void vox_attr() {
     }
 }
 
-// global scratch per cloud (cap_voxel each): keys (u64), left / right stop positions (int)
+// global scratch per cloud: cap_voxel u64 keys
 static VoxJob vox_job(Ctx& C, KindScratch& K, int which, const float4* pts, const int* d_n, int cap, float leaf, float4* out,
                       int* d_nout) {
     VoxJob j;
     j.pts = pts; j.d_n = d_n; j.cap = cap; j.leaf = leaf; j.out = out; j.d_nout = d_nout;
-    if (which == 0) { j.gE = K.vkeys; j.gL = (int*)(K.vkeys + C.cap_voxel); j.gR = j.gL + C.cap_voxel; }
-    else { j.gE = K.vkeys2; j.gL = K.vvals; j.gR = K.vvals2; }
+    j.gE = which == 0 ? K.vkeys : K.vkeys2;
     return j;
 }
 

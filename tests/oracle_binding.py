@@ -50,6 +50,7 @@ def lib():
         L.oracle_tictoc.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_get_map_cloud.argtypes = [vp, C.c_int, C.POINTER(abi.Cloud)]
         L.oracle_get_registered_cloud.argtypes = [vp, C.POINTER(abi.Cloud)]
+        L.oracle_cube_check.argtypes = [vp, C.POINTER(C.c_int)]
         L.oracle_eval_factors.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int,
                                           C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.oracle_lm_solve.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(abi.LMSummary)]
@@ -166,6 +167,13 @@ class Oracle:
         c, b = abi.make_cloud(cap)
         lib().oracle_get_map_cloud(self.h, which, C.byref(c))
         return b[:min(c.n, cap)].copy()
+
+    def cube_check(self):
+        """{cen: (W, H, D), points, misplaced, cubes}: every stored point re-bucketed directly with the
+        current cube centre (oracle_cube_check)."""
+        o = (C.c_int * 6)()
+        lib().oracle_cube_check(self.h, o)
+        return {"cen": (o[0], o[1], o[2]), "points": o[3], "misplaced": o[4], "cubes": o[5]}
 
     def registered_cloud(self, cap=400_000):
         c, b = abi.make_cloud(cap)

@@ -1,0 +1,176 @@
+// tests/ps_emu.cpp — host emulation of one HIP workgroup running csrc/pcl_sort.hpp.
+//
+// Every lane is a std::thread; the wave collectives the sort uses (ballot, shfl, readlane /
+// readfirstlane, DPP scans, all-reduces, the wave barrier) are a wave-wide std::barrier around a shared
+// exchange slot, lds_barrier / __syncthreads a workgroup-wide one, the LDS atomics host atomics. The
+// device code is compiled unchanged (PS_HOST_EMU skips its HIP include), so its partition arithmetic,
+// work queue and workgroup phase are checked against libstdc++'s std::sort on the CPU.
+// Test infrastructure: built and run by tests/test_pcl_sort_emu.py.
+#include <algorithm>
+#include <atomic>
+#include <barrier>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <random>
+#include <thread>
+#include <vector>
+
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define WAVE 64
+
+struct Dim3 { unsigned x = 0, y = 0, z = 0; };
+static thread_local Dim3 threadIdx;
+static thread_local int t_lane = 0, t_wave = 0;
+
+struct WaveCtx {
+    std::unique_ptr<std::barrier<>> bar;
+    unsigned long long slot[WAVE];
+    unsigned long long out;
+};
+static std::vector<std::unique_ptr<WaveCtx>> g_waves;
+static std::unique_ptr<std::barrier<>> g_block;
+
+static inline WaveCtx& W() { return *g_waves[t_wave]; }
+static inline void wave_sync() { W().bar->arrive_and_wait(); }
+// every lane deposits v, all see all
+template <typename F>
+static inline unsigned long long wave_collect(unsigned long long v, F f) {
+    WaveCtx& w = W();
+    w.slot[t_lane] = v;
+    wave_sync();
+    unsigned long long r = f(w.slot);
+    wave_sync();
+    return r;
+}
+
+namespace aloam {
+inline int lane_id() { return t_lane; }
+inline int wave_incl_scan(int v) {
+    return (int)wave_collect((unsigned long long)(unsigned)v, [](const unsigned long long* s) {
+        int acc = 0;
+        for (int i = 0; i <= t_lane; i++) acc += (int)(unsigned)s[i];
+        return (unsigned long long)(unsigned)acc;
+    });
+}
+inline int readlane_i(int v, int lane) {
+    return (int)wave_collect((unsigned long long)(unsigned)v, [lane](const unsigned long long* s) { return s[lane]; });
+}
+template <int NS, typename F>
+inline unsigned allreduce_u32(unsigned v, F op) {
+    static_assert(NS == 6, "whole-wave reductions only");
+    return (unsigned)wave_collect(v, [&op](const unsigned long long* s) {
+        unsigned a = (unsigned)s[0];
+        for (int i = 1; i < WAVE; i++) a = op(a, (unsigned)s[i]);
+        return (unsigned long long)a;
+    });
+}
+inline int wave_sum_i(int v) { return (int)allreduce_u32<6>((unsigned)v, [](unsigned a, unsigned b) { return a + b; }); }
+inline void lds_barrier() { g_block->arrive_and_wait(); }
+}  // namespace aloam
+
+static inline unsigned long long __ballot(bool p) {
+    return wave_collect(p ? 1ull : 0ull, [](const unsigned long long* s) {
+        unsigned long long m = 0;
+        for (int i = 0; i < WAVE; i++) m |= (s[i] ? 1ull : 0ull) << i;
+        return m;
+    });
+}
+static inline int __shfl(int v, int src, int) {
+    return (int)wave_collect((unsigned long long)(unsigned)v, [src](const unsigned long long* s) { return s[src & 63]; });
+}
+static inline int __builtin_amdgcn_readfirstlane(int v) { return aloam::readlane_i(v, 0); }
+static inline void __builtin_amdgcn_wave_barrier() { wave_sync(); }
+static inline void __builtin_amdgcn_fence(int, const char*) { std::atomic_thread_fence(std::memory_order_seq_cst); }
+static inline void __builtin_amdgcn_s_sleep(int) { std::this_thread::yield(); }
+static inline void __syncthreads() { g_block->arrive_and_wait(); }
+static inline int __popc(unsigned x) { return __builtin_popcount(x); }
+static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+static inline int __clz(int x) { return __builtin_clz((unsigned)x); }
+static inline int atomicAdd(int* p, int v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+#define __HIP_MEMORY_SCOPE_WORKGROUP 0
+#define __hip_atomic_fetch_add(p, v, o, sc) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
+#define __hip_atomic_load(p, o, sc) __atomic_load_n((p), __ATOMIC_SEQ_CST)
+#define __hip_atomic_store(p, v, o, sc) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
+using std::max;
+using std::min;
+#define PS_HOST_EMU 1
+#include "../lidar-visual-odometry_amd/csrc/pcl_sort.hpp"
+
+// mode 0: LDS sort (BIG = n may exceed one wave segment); mode 1: global sort staged through an LDS
+// buffer of `cap` elements
+template <int NT, bool BIG>
+static bool run_case(std::vector<unsigned long long>& E, int nmax, int mode, int cap) {
+    std::vector<int> sc(mode ? aloam::ps_scratch_ints_global(NT, cap) : aloam::ps_scratch_ints(NT, nmax, BIG));
+    std::vector<unsigned long long> EL(mode ? cap : 0);
+    g_waves.clear();
+    for (int w = 0; w < NT / WAVE; w++) {
+        auto c = std::make_unique<WaveCtx>();
+        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        g_waves.push_back(std::move(c));
+    }
+    g_block = std::make_unique<std::barrier<>>(NT);
+    const int n = (int)E.size();
+    std::vector<std::thread> th;
+    for (int t = 0; t < NT; t++)
+        th.emplace_back([&, t] {
+            threadIdx.x = t;
+            t_lane = t % WAVE;
+            t_wave = t / WAVE;
+            if (mode) aloam::pcl_std_sort_global<NT>(E.data(), n, EL.data(), cap, sc.data());
+            else aloam::pcl_std_sort<NT, BIG>(E.data(), n, sc.data(), nmax);
+        });
+    for (auto& x : th) x.join();
+    return true;
+}
+
+#ifndef NTHREADS
+#define NTHREADS 128
+#endif
+int main(int argc, char** argv) {
+    const int trials = argc > 1 ? atoi(argv[1]) : 40;
+    std::mt19937_64 rng(argc > 2 ? strtoull(argv[2], nullptr, 10) : 5);
+    int bad = 0;
+    for (int t = 0; t < trials; t++) {
+        const bool big = t % 2 == 1;
+        int n = big ? 4000 + (int)(rng() % 4000) : 1 + (int)(rng() % 4096);
+        if (t % 9 == 0) n = 1 + (int)(rng() % 40);
+        const unsigned kinds = 1 + (unsigned)(rng() % (t % 3 == 0 ? 4 : (t % 3 == 1 ? 300 : 100000)));
+        std::vector<unsigned long long> E(n);
+        for (int i = 0; i < n; i++) {
+            unsigned k;
+            switch (t % 4) {
+                case 0: k = (unsigned)(rng() % kinds); break;
+                case 1: k = (unsigned)(i / (1 + (int)(rng() % 4))) % kinds; break;
+                case 2: k = (unsigned)((n - i) / 3) % kinds; break;
+                default: k = i < n / 2 ? (unsigned)(i / 8) : (unsigned)(rng() % kinds);
+            }
+            E[i] = ((unsigned long long)k << 32) | (unsigned)i;
+        }
+        std::vector<unsigned long long> A = E;
+        std::sort(A.begin(), A.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
+        // every third big case: the global sort, staged through a buffer of a fraction of n
+        const int mode = big && t % 3 == 0;
+        const int cap = mode ? 600 + (int)(rng() % 2000) : 0;
+        if (NTHREADS == 1024) {                  // the device's workgroup size (16 waves)
+            if (big) run_case<1024, true>(E, n, mode, cap);
+            else run_case<1024, false>(E, n, 0, 0);
+        } else {
+            if (big) run_case<128, true>(E, n, mode, cap);  // 2 waves: the work queue; n > 4096: the workgroup phase
+            else run_case<128, false>(E, n, 0, 0);
+        }
+        if (A != E) {
+            bad++;
+            int first = 0;
+            while (first < n && A[first] == E[first]) first++;
+            std::printf("mismatch trial %d n %d kinds %u big %d mode %d cap %d first diff at %d\n", t, n, kinds, (int)big, mode, cap, first);
+        }
+    }
+    std::printf("trials %d mismatches %d\n", trials, bad);
+    return bad != 0;
+}

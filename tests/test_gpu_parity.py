@@ -253,6 +253,34 @@ def test_mapping_frames_teacher_forced(gpu_ctx_factory):
     np.testing.assert_allclose(mc_g, mc_o, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("axis", ["+x", "-x", "+y", "-y", "+z", "-z"])
+def test_mapping_cube_recentring(gpu_ctx_factory, axis):
+    """Cube recentring (laserMapping.cpp:325-507) on the device: teacher-forced frames cross the +-x, +-y
+    (375 m) / +-z (125 m) thresholds while the grid holds points, one frame shifting twice
+    (tests/recentre_seq.py). Every frame's counts and pose, and the whole cube grid (every cube's points
+    in cube order) match the oracle bit for bit."""
+    import recentre_seq
+    ctx = gpu_ctx_factory(64)
+    orc = ob.Oracle(abi.default_params(64))
+    cen = []
+    for k, (c, s, q, t) in enumerate(recentre_seq.sequence(axis)):
+        ctx.set_mapping_input(c, s, q, t)
+        orc.set_mapping_input(c, s, q, t)
+        mg = ctx.mapping()
+        mo = orc.mapping()
+        for key in ("optimized", "map_corner_num", "map_surf_num", "corner_stack_num", "surf_stack_num",
+                    "corner_num", "surf_num", "map_total_points"):
+            assert mg[key] == mo[key], (axis, k, key, mg[key], mo[key])
+        np.testing.assert_allclose(mg["q_w_curr"], mo["q_w_curr"], rtol=POSE_RTOL, atol=1e-9)
+        np.testing.assert_allclose(mg["t_w_curr"], mo["t_w_curr"], rtol=POSE_RTOL, atol=1e-7)
+        cen.append(orc.cube_check()["cen"])
+        for which in (0, 1):
+            g, o = ctx.map_cloud(which), orc.map_cloud(which)
+            assert g.shape == o.shape, (axis, k, which, g.shape, o.shape)
+            assert np.array_equal(bits(g), bits(o)), (axis, k, which, int(np.sum(bits(g) != bits(o))))
+    assert len(set(cen)) >= 4, cen
+
+
 def test_pipeline_sequence_ate(gpu_ctx_factory):
     """Free-running pipeline over a short HDL-64 sequence: trajectories agree (ATE delta)."""
     ctx = gpu_ctx_factory(64)
@@ -362,6 +390,105 @@ def test_pipeline_matches_single_context(lvo, stages):
         np.testing.assert_allclose(o["t_w_curr"], o_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(m["t_w_curr"], m_ref["t_w_curr"], rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(m["q_w_curr"], m_ref["q_w_curr"], rtol=1e-9, atol=1e-12)
+
+
+def _run_pipeline(lvo, p, frames, stages):
+    pipe = lvo.Pipeline(p, stages=stages)
+    ods, mps = [], []
+    for f in frames:
+        od, mp = pipe.push(f)
+        if od is not None:
+            ods.append(od)
+        if mp is not None:
+            mps.append(mp)
+    for od, mp in pipe.flush():
+        if od is not None:
+            ods.append(od)
+        if mp is not None:
+            mps.append(mp)
+    pipe.close()
+    return ods, mps
+
+
+def _assert_pipeline_vs_oracle(p, frames, ods, mps):
+    orc = ob.Oracle(p)
+    ref = [orc.process_scan(f) for f in frames]
+    published = [k for k, (o, _) in enumerate(ref) if o["publish_to_mapping"]]
+    assert len(ods) == len(frames) and len(mps) == len(published), (len(ods), len(mps), published)
+    for k, (od, (oo, _)) in enumerate(zip(ods, ref)):
+        for key in ("publish_to_mapping", "corner_correspondence", "plane_correspondence"):
+            assert od[key] == oo[key], (k, key, od[key], oo[key])
+        np.testing.assert_allclose(od["t_w_curr"], oo["t_w_curr"], rtol=POSE_RTOL, atol=1e-7)
+    for mp, k in zip(mps, published):
+        mo = ref[k][1]
+        for key in ("optimized", "map_corner_num", "map_surf_num", "corner_stack_num", "surf_stack_num",
+                    "corner_num", "surf_num", "map_total_points"):
+            assert mp[key] == mo[key], (k, key, mp[key], mo[key])
+        np.testing.assert_allclose(mp["t_w_curr"], mo["t_w_curr"], rtol=POSE_RTOL, atol=1e-7)
+        np.testing.assert_allclose(mp["q_w_curr"], mo["q_w_curr"], rtol=POSE_RTOL, atol=1e-9)
+    return published
+
+
+_PIPE_MODES = [(2, "2"), (2, "1"), (3, "2")]          # (stages, ALOAM_PIPE_LAG): results returned 2 or 1 scans late
+
+
+@pytest.mark.parametrize("stages,lag", _PIPE_MODES)
+def test_pipeline_mapping_skip_frame_two(lvo, monkeypatch, stages, lag):
+    """mapping_skip_frame = 2 (laserOdometry.cpp:274, :643): odometry publishes every second scan to
+    mapping; the native pipeline maps exactly those, as the oracle."""
+    monkeypatch.setenv("ALOAM_PIPE_LAG", lag)
+    p = abi.default_params(64)
+    p.mapping_skip_frame = 2
+    frames = [synth.scan("hdl64", k) for k in range(7)]
+    ods, mps = _run_pipeline(lvo, p, frames, stages)
+    assert _assert_pipeline_vs_oracle(p, frames, ods, mps) == [0, 2, 4, 6]
+
+
+@pytest.mark.parametrize("stages,lag", _PIPE_MODES)
+def test_pipeline_feature_count_jump(lvo, monkeypatch, stages, lag):
+    """Sparse sweeps (every 5th return) followed by full ones: the feature and stack counts jump past the
+    sizes the previous frame's launches were sized for (the hinted stack VoxelGrid redoes at the exact
+    size); every stage still matches the oracle."""
+    monkeypatch.setenv("ALOAM_PIPE_LAG", lag)
+    p = abi.default_params(64)
+    frames = _jump_frames()
+    ods, mps = _run_pipeline(lvo, p, frames, stages)
+    _assert_pipeline_vs_oracle(p, frames, ods, mps)
+
+
+def _jump_frames():
+    return [synth.scan("hdl64", k)[::5] for k in range(3)] + [synth.scan("hdl64", k) for k in range(3, 6)]
+
+
+_POLL_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from lvo_amd_loader import lvo
+import test_gpu_parity as T
+p = lvo.abi.default_params(64)
+p.mapping_skip_frame = int(sys.argv[2])
+frames = T._jump_frames()
+ods, mps = T._run_pipeline(lvo, p, frames, 2)
+T._assert_pipeline_vs_oracle(p, frames, ods, mps)
+print("ok", len(ods), len(mps))
+"""
+
+
+@pytest.mark.parametrize("skip", [1, 2])
+def test_pipeline_poll_mode(skip):
+    """ALOAM_PIPE_POLL=1 (read once per process, so in a child): mapping results are handed back as
+    they complete instead of at a fixed lag; sparse -> dense jump, skip_frame 1 and 2, against the
+    oracle."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, ALOAM_PIPE_POLL="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = subprocess.run([sys.executable, "-c", _POLL_SCRIPT, here, str(skip)], env=env, capture_output=True,
+                         text=True, timeout=110, cwd=here)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert out.stdout.strip().splitlines()[-1].startswith("ok 6")
 
 
 _SIDE_SCRIPT = r"""

@@ -1,0 +1,23 @@
+"""The device's PCL-order sort (csrc/pcl_sort.hpp) compiled for the host and run under a lane-per-thread
+emulation of one workgroup (tests/ps_emu.cpp): its wave-level partitions, work queue and workgroup
+phase leave exactly libstdc++'s std::sort order. CPU test (the GPU tests check the kernels themselves)."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def emu(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("psemu") / "ps_emu"
+    subprocess.check_call(["g++", "-std=c++20", "-O1", "-pthread", "-w", "-o", str(exe), os.path.join(HERE, "ps_emu.cpp")])
+    return str(exe)
+
+
+def test_device_sort_matches_libstdcxx_under_emulation(emu):
+    # 2 waves of 64 lanes; sizes up to 4096 (one wave segment) and 4000-8000 (workgroup phase first)
+    r = subprocess.run([emu, "5", "11"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
