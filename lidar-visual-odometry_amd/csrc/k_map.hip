@@ -20,7 +20,7 @@
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 #include "eigen_small.hpp"
-#include "pcl_sort.hpp"
+#include "ls_sort.hpp"
 
 namespace aloam {
 #ifdef ALOAM_WSTAMP_MAP
@@ -577,9 +577,10 @@ __global__ void k_map_register(const float4* __restrict__ full, int n, const Map
 // leaf is summed from zero in that order (CentroidPoint), so the cube's new points equal PCL's bit for
 // bit. Cubes up to RBV_CAP points sort in LDS, larger ones in the cube's global scratch.
 constexpr int RBV_T = 1024;
-constexpr int RBV_CAP = 14336;       // cube points sorted in LDS (more: global scratch)
+constexpr int RBV_CPW = 10;          // ls_sort: 64-position chunks per wave
+constexpr int RBV_CAP = RBV_T * RBV_CPW;   // cube points sorted in LDS (more: global scratch, staged)
 constexpr size_t RBV_HDR = 64;
-constexpr size_t RBV_LDS = RBV_HDR + 8 * (size_t)RBV_CAP + 4 * (size_t)ps_scratch_ints_global(RBV_T, RBV_CAP);
+constexpr size_t RBV_LDS = RBV_HDR + 8 * (size_t)RBV_CAP + ls_global_scratch_bytes(RBV_T, RBV_CAP);
 constexpr int RBV_PER = 8;           // points per thread held in registers for the bbox and the keys
 static_assert(RBV_LDS <= 160 * 1024, "LDS");
 struct RbvShared { unsigned bb[6]; int bad; int pad; };
@@ -674,10 +675,29 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     }
     if (FITS) lds_barrier(); else __syncthreads();
     RBSTAMP(1);
+    // A cube that received no points this frame holds the previous filter's output: one point per leaf in
+    // leaf order. With its keys strictly increasing every leaf is a single point, and std::sort leaves the
+    // order as is, so the filter returns every point summed from zero (0 + x: -0 becomes +0) over 1.
+    if (new_count(a, c) == 0) {
+        if (tid == 0) SH.bad = 0;
+        if (FITS) lds_barrier(); else __syncthreads();
+        bool up = true;
+        for (int t = tid; t + 1 < n; t += RBV_T) up = up && ps_key(E[t]) < ps_key(E[t + 1]);
+        if (__ballot(!up) && lane_id() == 0) SH.bad = 1;
+        __syncthreads();
+        if (SH.bad == 0) {
+            for (int t = tid; t < n; t += RBV_T) {
+                const float4 v = B[p0 + t];
+                Cf[p0 + t] = div4_by_count(make_float4(0.f + v.x, 0.f + v.y, 0.f + v.z, 0.f + v.w), 1);
+            }
+            if (tid == 0) a.seg_nout[c] = n;
+            return;
+        }
+    }
     if (FITS) {
-        pcl_std_sort<RBV_T, true>(E, n, sc, RBV_CAP);
+        ls_sort<RBV_T, RBV_CPW>(E, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, RBV_CAP);
     } else if (n <= RBV_T * PS_MAX_CHUNK) {
-        pcl_std_sort_global<RBV_T>(E, n, EL, RBV_CAP, sc);
+        ls_sort_global<RBV_T, RBV_CPW>(E, n, EL, RBV_CAP, (unsigned char*)sc);
     } else {                                  // beyond the parallel replay's reach: one thread
         if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();

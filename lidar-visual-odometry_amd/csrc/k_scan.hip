@@ -14,7 +14,7 @@
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 #include "libm_f32.h"
-#include "pcl_sort.hpp"
+#include "ls_sort.hpp"
 
 namespace aloam {
 
@@ -745,14 +745,15 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     LF_TS(4);
     // PCL's order of the (leaf, index) pairs: libstdc++ std::sort by leaf (pcl_sort.hpp); LDS lines keep
     // the sort's scratch in the merge-sort buffer, big lines in their (unused) LDS arrays.
-    static_assert((size_t)LINE_LDS_CAP * 8 >= 4 * (size_t)ps_scratch_ints(LT, LINE_LDS_CAP, false), "sort scratch in the sort buffer");
-    static_assert(LINE_LDS_CAP <= PS_WMAX, "LDS lines are one wave segment");
-    constexpr int LINE_STAGE = 12288;      // big lines: sort segments staged through the (unused) LDS arrays
-    static_assert(line_lds_bytes() - LINE_HDR >= 8 * (size_t)LINE_STAGE + 4 * (size_t)ps_scratch_ints_global(LT, LINE_STAGE), "big lines: sort staging in LDS");
+    constexpr int LINE_CPW = LINE_LDS_CAP / LT;    // ls_sort: 64-position chunks per wave
+    static_assert((size_t)LINE_LDS_CAP * 8 >= ls_scratch_bytes(LT, LINE_LDS_CAP) && LINE_CPW * LT == LINE_LDS_CAP, "sort scratch in the sort buffer");
+    constexpr int LINE_STAGE_CPW = 10;
+    constexpr int LINE_STAGE = LT * LINE_STAGE_CPW;   // big lines: sort segments staged through the (unused) LDS arrays
+    static_assert(line_lds_bytes() - LINE_HDR >= 8 * (size_t)LINE_STAGE + ls_global_scratch_bytes(LT, LINE_STAGE), "big lines: sort staging in LDS");
     if (!big) {
-        pcl_std_sort<LT, false>(keys, nc, (int*)sorted, LINE_LDS_CAP);
+        ls_sort<LT, LINE_CPW>(keys, nc, nc > 1 ? 2 * (31 - __builtin_clz((unsigned)nc)) : 0, (unsigned char*)sorted, LINE_LDS_CAP);
     } else if (nc <= LT * PS_MAX_CHUNK) {
-        pcl_std_sort_global<LT>(keys, nc, (unsigned long long*)smem, LINE_STAGE, (int*)(smem + 8 * (size_t)LINE_STAGE));
+        ls_sort_global<LT, LINE_STAGE_CPW>(keys, nc, (unsigned long long*)smem, LINE_STAGE, smem + 8 * (size_t)LINE_STAGE);
     } else {
         if (threadIdx.x == 0) ps_serial_std_sort(keys, nc);
         __syncthreads();
@@ -790,6 +791,13 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     LF_TS(7);
 }
 
+// oversized lines (rare): not inlined, so their global-scratch body does not load the LDS path's registers
+__device__ __noinline__ void line_features_big(const float4* __restrict__ cloud, const float* __restrict__ gcurv, const ScanMeta* meta,
+                                               int N_SCANS, float4* g_xyz, unsigned long long* g_keys, int* g_i, int* line_sharp,
+                                               int* line_lsharp, int* line_flat, int* line_cnt, float4* line_lf, lds_u8* smem) {
+    line_features_body<true>(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf,
+                             (unsigned char*)smem);
+}
 __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__ cloud, const float* __restrict__ gcurv,
                                                       const ScanMeta* meta, int N_SCANS,
                                                       float4* g_xyz, unsigned long long* g_keys, int* g_i,
@@ -797,7 +805,7 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
                                                       float4* line_lf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int nl_ = meta->line_off[blockIdx.x + 1] - meta->line_off[blockIdx.x];
-    if (nl_ > LINE_LDS_CAP) line_features_body<true>(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, smem_raw);
+    if (nl_ > LINE_LDS_CAP) line_features_big(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, (lds_u8*)smem_raw);
     else line_features_body<false>(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, smem_raw);
 }
 

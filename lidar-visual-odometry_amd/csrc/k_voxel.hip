@@ -31,15 +31,16 @@ extern "C" int aloam_dbg_ps_ts(unsigned long long* out, int* nseg) {
     return (int)hipMemcpyFromSymbol(nseg, HIP_SYMBOL(g_ps_nseg), sizeof(g_ps_nseg));
 }
 #endif
-#include "pcl_sort.hpp"
+#include "ls_sort.hpp"
 
 namespace aloam {
 
 constexpr int VX_T = 1024;
-constexpr int VX_LDS_N = 14336;                             // clouds up to this size are sorted in LDS
+constexpr int VX_CPW = 10;                                  // ls_sort: 64-position chunks per wave
+constexpr int VX_LDS_N = VX_T * VX_CPW;                     // clouds up to this size are sorted in LDS
 constexpr int VX_NMAX = VX_T * PS_MAX_CHUNK;                // parallel replay up to this size (beyond: one thread)
 constexpr size_t VX_HDR = 64;
-constexpr size_t VX_LDS = VX_HDR + 8 * (size_t)VX_LDS_N + 4 * (size_t)ps_scratch_ints_global(VX_T, VX_LDS_N);
+constexpr size_t VX_LDS = VX_HDR + 8 * (size_t)VX_LDS_N + ls_global_scratch_bytes(VX_T, VX_LDS_N);
 static_assert(VX_LDS <= 160 * 1024, "LDS");
 
 struct VoxJob {
@@ -53,9 +54,9 @@ struct VoxJobs { VoxJob j[2]; };
 __device__ void vox_sort_and_reduce(const VoxJob& J, int n, unsigned long long* E, unsigned long long* EL, int* sc) {
     const int tid = threadIdx.x;
     if (E == EL) {
-        pcl_std_sort<VX_T, true>(E, n, sc, VX_LDS_N);
+        ls_sort<VX_T, VX_CPW>(EL, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, VX_LDS_N);
     } else if (n <= VX_NMAX) {
-        pcl_std_sort_global<VX_T>(E, n, EL, VX_LDS_N, sc);
+        ls_sort_global<VX_T, VX_CPW>(E, n, EL, VX_LDS_N, (unsigned char*)sc);
     } else {                                                  // beyond the parallel replay's reach: one thread
         if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();

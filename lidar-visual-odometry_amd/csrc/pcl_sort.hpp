@@ -196,7 +196,7 @@ __device__ inline void ps_heap_sort(unsigned long long* first, unsigned long lon
 // The whole std::sort by one thread (arrays beyond NT * PS_MAX_CHUNK elements): introsort_loop with an
 // explicit stack (the right part is pushed, the left continued — disjoint ranges, same result), then
 // __final_insertion_sort.
-__device__ inline void ps_serial_std_sort(unsigned long long* E, int n) {
+__device__ __noinline__ void ps_serial_std_sort(unsigned long long* E, int n) {
     if (n <= 1) return;
     int sf[64], sl[64], sd[64], sp = 0;
     sf[0] = 0; sl[0] = n; sd[0] = 2 * (31 - __builtin_clz((unsigned)n)); sp = 1;

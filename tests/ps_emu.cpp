@@ -22,6 +22,7 @@
 #define __device__
 #define __host__
 #define __forceinline__ inline
+#define __noinline__
 #define WAVE 64
 
 struct Dim3 { unsigned x = 0, y = 0, z = 0; };
@@ -72,6 +73,7 @@ inline unsigned allreduce_u32(unsigned v, F op) {
 }
 inline int wave_sum_i(int v) { return (int)allreduce_u32<6>((unsigned)v, [](unsigned a, unsigned b) { return a + b; }); }
 inline void lds_barrier() { g_block->arrive_and_wait(); }
+inline unsigned long long lanemask_lt64() { return t_lane == 0 ? 0ull : (~0ull >> (64 - t_lane)); }
 }  // namespace aloam
 
 static inline unsigned long long __ballot(bool p) {
@@ -93,6 +95,12 @@ static inline int __popc(unsigned x) { return __builtin_popcount(x); }
 static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 static inline int __clz(int x) { return __builtin_clz((unsigned)x); }
 static inline int atomicAdd(int* p, int v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+static inline int atomicMin(int* p, int v) {
+    int o = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+    while (v < o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {}
+    return o;
+}
+static inline unsigned long long atomicOr(unsigned long long* p, unsigned long long v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
 #define __hip_atomic_fetch_add(p, v, o, sc) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
 #define __hip_atomic_load(p, o, sc) __atomic_load_n((p), __ATOMIC_SEQ_CST)
@@ -101,6 +109,54 @@ using std::max;
 using std::min;
 #define PS_HOST_EMU 1
 #include "../lidar-visual-odometry_amd/csrc/pcl_sort.hpp"
+#include "../lidar-visual-odometry_amd/csrc/ls_sort.hpp"
+
+// the level-synchronous sort (csrc/ls_sort.hpp) on one emulated workgroup of NT threads
+template <int NT, int CPW>
+static void run_ls(std::vector<unsigned long long>& E) {
+    const int n = (int)E.size(), nmax = NT * CPW;
+    std::vector<unsigned long long> scr((aloam::ls_scratch_bytes(NT, nmax) + 7) / 8);
+    g_waves.clear();
+    for (int w = 0; w < NT / WAVE; w++) {
+        auto c = std::make_unique<WaveCtx>();
+        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        g_waves.push_back(std::move(c));
+    }
+    g_block = std::make_unique<std::barrier<>>(NT);
+    const int d0 = n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0;
+    std::vector<std::thread> th;
+    for (int t = 0; t < NT; t++)
+        th.emplace_back([&, t] {
+            threadIdx.x = t;
+            t_lane = t % WAVE;
+            t_wave = t / WAVE;
+            aloam::ls_sort<NT, CPW>(E.data(), n, d0, (unsigned char*)scr.data(), nmax);
+        });
+    for (auto& x : th) x.join();
+}
+// csrc/ls_sort.hpp's global sort: split in "global" memory by the workgroup phase of pcl_sort.hpp, segments
+// staged through an LDS buffer of `cap` elements and sorted there by ls_sort
+template <int NT, int CPW>
+static void run_ls_global(std::vector<unsigned long long>& E, int cap) {
+    const int n = (int)E.size();
+    std::vector<unsigned long long> scr((aloam::ls_global_scratch_bytes(NT, cap) + 7) / 8), EL(cap);
+    g_waves.clear();
+    for (int w = 0; w < NT / WAVE; w++) {
+        auto c = std::make_unique<WaveCtx>();
+        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        g_waves.push_back(std::move(c));
+    }
+    g_block = std::make_unique<std::barrier<>>(NT);
+    std::vector<std::thread> th;
+    for (int t = 0; t < NT; t++)
+        th.emplace_back([&, t] {
+            threadIdx.x = t;
+            t_lane = t % WAVE;
+            t_wave = t / WAVE;
+            aloam::ls_sort_global<NT, CPW>(E.data(), n, EL.data(), cap, (unsigned char*)scr.data());
+        });
+    for (auto& x : th) x.join();
+}
 
 // mode 0: LDS sort (BIG = n may exceed one wave segment); mode 1: global sort staged through an LDS
 // buffer of `cap` elements
@@ -135,10 +191,13 @@ static bool run_case(std::vector<unsigned long long>& E, int nmax, int mode, int
 int main(int argc, char** argv) {
     const int trials = argc > 1 ? atoi(argv[1]) : 40;
     std::mt19937_64 rng(argc > 2 ? strtoull(argv[2], nullptr, 10) : 5);
+    const int lsm = argc > 3 ? atoi(argv[3]) : 0;        // 1: csrc/ls_sort.hpp (n <= 128 * 16); 2: its global sort
+    const bool ls = lsm == 1;
     int bad = 0;
     for (int t = 0; t < trials; t++) {
         const bool big = t % 2 == 1;
         int n = big ? 4000 + (int)(rng() % 4000) : 1 + (int)(rng() % 4096);
+        if (ls) n = 1 + (int)(rng() % 2048);
         if (t % 9 == 0) n = 1 + (int)(rng() % 40);
         const unsigned kinds = 1 + (unsigned)(rng() % (t % 3 == 0 ? 4 : (t % 3 == 1 ? 300 : 100000)));
         std::vector<unsigned long long> E(n);
@@ -157,7 +216,9 @@ int main(int argc, char** argv) {
         // every third big case: the global sort, staged through a buffer of a fraction of n
         const int mode = big && t % 3 == 0;
         const int cap = mode ? 600 + (int)(rng() % 2000) : 0;
-        if (NTHREADS == 1024) {                  // the device's workgroup size (16 waves)
+        if (lsm == 2) run_ls_global<128, 16>(E, 300 + (int)(rng() % 1748));
+        else if (ls) run_ls<128, 16>(E);
+        else if (NTHREADS == 1024) {                  // the device's workgroup size (16 waves)
             if (big) run_case<1024, true>(E, n, mode, cap);
             else run_case<1024, false>(E, n, 0, 0);
         } else {

@@ -156,12 +156,13 @@ def test_knn_radius(gpu_ctx_factory):
 
 def test_voxel_grid_matches_pcl_semantics(gpu_ctx_factory):
     """aloam_voxel_grid vs PCL 1.8's applyFilter (the oracle, order 1 = libstdc++ std::sort of the
-    (leaf, index) pairs): bit-exact centroids, across the device's three sort paths — in LDS (n <= 6144),
-    in global scratch (6144 < n <= ~63k), one-thread serial replay (beyond) — and degenerate key sets."""
+    (leaf, index) pairs): bit-exact centroids, across the device's three sort paths — in LDS (ls_sort.hpp,
+    n <= 11264), split in global scratch then staged through LDS (11264 < n <= 65536), one-thread serial
+    replay (beyond) — and degenerate key sets."""
     ctx = gpu_ctx_factory(64)
     pts = synth.scan("hdl64", 4)
     pts[:, 3] = np.arange(len(pts)) % 64 * 0.01
-    for n in (1, 2, 15, 16, 17, 300, 6144, 6145, 20000, 60000, len(pts)):
+    for n in (1, 2, 15, 16, 17, 300, 6144, 11264, 11265, 20000, 60000, len(pts)):
         for leaf in ((0.2, 0.4, 0.8) if n in (300, 20000) else (0.4,)):
             vg = ctx.voxel_grid(pts[:n], leaf)
             vp = ob.voxel_grid(pts[:n], leaf, order=1)

@@ -21,3 +21,17 @@ def test_device_sort_matches_libstdcxx_under_emulation(emu):
     r = subprocess.run([emu, "5", "11"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+def test_ls_sort_matches_libstdcxx_under_emulation(emu):
+    # csrc/ls_sort.hpp on 2 emulated waves (n <= 128 * 16): every introsort level of every segment at once
+    r = subprocess.run([emu, "50", "13", "1"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
+
+
+def test_ls_sort_global_matches_libstdcxx_under_emulation(emu):
+    # csrc/ls_sort.hpp's global sort (n 4000-8000, split to segments <= cap, each sorted in the LDS buffer)
+    r = subprocess.run([emu, "16", "17", "2"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
