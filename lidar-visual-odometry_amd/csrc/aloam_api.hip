@@ -233,6 +233,7 @@ static void allocate(Ctx& C) {
     k0.vkeys = C.d_vkeys; k0.vkeys2 = C.d_vkeys2; k0.vvals = C.d_vvals; k0.vvals2 = C.d_vvals2;
     k0.ins_pts = C.d_ins_pts; k0.ins_val = C.d_ins_val; k0.ins_val2 = C.d_ins_val2;
     k0.seg_keys = C.d_seg_keys; k0.blk = C.d_blk; k0.map_tmp = C.d_map_tmp;
+    k0.cube_segl = (int*)dalloc(C, sizeof(int) * (size_t)125 * (1 + 3 * 320));
     KindScratch& k1 = C.ks[1];
     k1.vkeys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)C.cap_voxel);
     k1.vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);
@@ -244,6 +245,7 @@ static void allocate(Ctx& C) {
     k1.seg_keys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (4 * (size_t)M + 32768));
     k1.blk = (int*)dalloc(C, sizeof(int) * (std::max(nb, M / 256 + 1) + 4096));
     k1.map_tmp = (float4*)dalloc(C, sizeof(float4) * M);
+    k1.cube_segl = (int*)dalloc(C, sizeof(int) * (size_t)125 * (1 + 3 * 320));
     KindScratch& kv = C.ksv;            // stream3: the stacks' VoxelGrid (vkeys, vvals, sort, blk only)
     kv.vkeys = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * 2 * (size_t)C.cap_voxel);
     kv.vkeys2 = (unsigned long long*)dalloc(C, sizeof(unsigned long long) * (size_t)C.cap_voxel);

@@ -106,6 +106,7 @@ struct KindScratch {               // per-lane scratch for the map kinds' concur
     float4* ins_pts = nullptr;
     int *ins_val = nullptr, *ins_val2 = nullptr;
     unsigned long long* seg_keys = nullptr;                   // 4 x cap_map + 32768
+    int* cube_segl = nullptr;                                 // per surrounding cube: sort segment list (125 x LS_SEGL)
     int* blk = nullptr;
     float4* map_tmp = nullptr;
 };

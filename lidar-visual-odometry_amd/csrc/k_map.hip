@@ -585,9 +585,51 @@ constexpr int RBV_PER = 8;           // points per thread held in registers for 
 static_assert(RBV_LDS <= 160 * 1024, "LDS");
 struct RbvShared { unsigned bb[6]; int bad; int pad; };
 
+// the cube's sorted (leaf, position) pairs -> centroids (fp32 from zero, in sorted order) at the cube's
+// offset; thread k owns sorted positions [k C, (k+1) C), a run is summed by the thread of its head
+__device__ __forceinline__ void rbv_reduce(const unsigned long long* E, const float4* __restrict__ B, CubeArrays a, int c, int p0,
+                                           int n, float4* __restrict__ Cf, int* sc) {
+    const int tid = threadIdx.x;
+    const int C = (n + RBV_T - 1) / RBV_T;
+    const int q0 = min(n, tid * C), q1 = min(n, q0 + C);
+    int nh = 0;
+    for (int q = q0; q < q1; q++) nh += (q == 0 || ps_key(E[q]) != ps_key(E[q - 1]));
+    int run = nh, dummy = 0, tot, td;
+    ps_exscan2<RBV_T>(run, dummy, sc + 16, tot, td);
+    for (int q = q0; q < q1; q++) {
+        const unsigned k = ps_key(E[q]);
+        if (!(q == 0 || k != ps_key(E[q - 1]))) continue;
+        float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int cnt = 0;
+        for (int t = q; t < n; t += 4) {        // 4 points in flight per step
+            unsigned long long e[4];
+            bool in[4];
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) { e[u] = t + u < n ? E[t + u] : ~0ull; }
+            bool go = true;
+#pragma unroll
+            for (int u = 0; u < 4; u++) { go = go && t + u < n && ps_key(e[u]) == k; in[u] = go; }
+#pragma unroll
+            for (int u = 0; u < 4; u++) if (in[u]) v[u] = B[p0 + (int)(e[u] & 0xffffffffu)];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (in[u]) { cc.x += v[u].x; cc.y += v[u].y; cc.z += v[u].z; cc.w += v[u].w; cnt++; }
+            if (!in[3]) break;
+        }
+        Cf[p0 + run] = div4_by_count(cc, cnt);
+        run++;
+    }
+    if (tid == 0) a.seg_nout[c] = tot;
+}
+
+// FITS: the whole cube in LDS. Else (n <= 65536): keys in the cube's global scratch, split into segments of
+// <= seg_limit elements whose list goes to segl (count 0: the cube is finished here) for k_rb_cubeseg and
+// k_rb_cubered; beyond 65536 points one thread sorts (rare).
 template <bool FITS>
 __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n,
-                                         float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr, const int* fb) {
+                                         float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr, const int* fb,
+                                         int* segl, int seg_limit) {
     RbvShared& SH = *(RbvShared*)smem;
     const int tid = threadIdx.x;
     // keys in LDS when the cube fits, else in the cube's global scratch (staged through the same LDS
@@ -697,46 +739,15 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     if (FITS) {
         ls_sort<RBV_T, RBV_CPW>(E, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, RBV_CAP);
     } else if (n <= RBV_T * PS_MAX_CHUNK) {
-        ls_sort_global<RBV_T, RBV_CPW>(E, n, EL, RBV_CAP, (unsigned char*)sc);
+        ls_split_to_list<RBV_T>(E, n, seg_limit, segl, (unsigned char*)sc);   // -> k_rb_cubeseg, k_rb_cubered
+        return;
     } else {                                  // beyond the parallel replay's reach: one thread
         if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();
     }
     RBSTAMP(4);
-    // runs of equal leaves in sorted order -> centroids (fp32 from zero, in sorted order) at the cube's
-    // offset; thread k owns sorted positions [k C, (k+1) C), a run is summed by the thread of its head
-    const int C = (n + RBV_T - 1) / RBV_T;
-    const int q0 = min(n, tid * C), q1 = min(n, q0 + C);
-    int nh = 0;
-    for (int q = q0; q < q1; q++) nh += (q == 0 || ps_key(E[q]) != ps_key(E[q - 1]));
-    int run = nh, dummy = 0, tot, td;
-    ps_exscan2<RBV_T>(run, dummy, sc + 16, tot, td);
-    for (int q = q0; q < q1; q++) {
-        const unsigned k = ps_key(E[q]);
-        if (!(q == 0 || k != ps_key(E[q - 1]))) continue;
-        float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
-        int cnt = 0;
-        for (int t = q; t < n; t += 4) {        // 4 points in flight per step
-            unsigned long long e[4];
-            bool in[4];
-            float4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) { e[u] = t + u < n ? E[t + u] : ~0ull; }
-            bool go = true;
-#pragma unroll
-            for (int u = 0; u < 4; u++) { go = go && t + u < n && ps_key(e[u]) == k; in[u] = go; }
-#pragma unroll
-            for (int u = 0; u < 4; u++) if (in[u]) v[u] = B[p0 + (int)(e[u] & 0xffffffffu)];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (in[u]) { cc.x += v[u].x; cc.y += v[u].y; cc.z += v[u].z; cc.w += v[u].w; cnt++; }
-            if (!in[3]) break;
-        }
-        Cf[p0 + run] = div4_by_count(cc, cnt);
-        run++;
-    }
+    rbv_reduce(E, B, a, c, p0, n, Cf, sc);
     RBSTAMP(5);
-    if (tid == 0) a.seg_nout[c] = tot;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -748,6 +759,7 @@ struct RbKind {
     float4* B; int* Bcube;                                // old + appended points grouped by cube
     float4* ins_pts; unsigned* k1; int* v2;               // appended points in the map frame, cube keys, ranks
     float4* Cf; unsigned long long* gscr;                 // per-cube VoxelGrid output / global scratch
+    int* segl;                                            // per surrounding cube: its sort's segment list
     CubeArrays a;
     int fast_keys;                                        // leaf keys from the cube box (< 1024 leaves per axis)
 };
@@ -893,7 +905,7 @@ __global__ void k_rb_scatter(RbKinds P) {
     }
 }
 
-__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState* __restrict__ m) {
+__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState* __restrict__ m, int seg_limit, int fit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RbKind& K = P.k[blockIdx.y];
     const int r = blockIdx.x;
@@ -910,8 +922,34 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
         for (int d = 0; d < 3; d++) fbv[d] = (int)floorf((float)(50.0 * (cc[d] - cen[d]) - 26.0) * inv);
         fb = fbv;
     }
-    if (n <= RBV_CAP) rbv_cube<true>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb);
-    else rbv_cube<false>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb);
+    int* segl = K.segl + (size_t)r * LS_SEGL;
+    if (threadIdx.x == 0) segl[0] = 0;            // finished here unless split below
+    if (n <= fit) rbv_cube<true>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb, segl, seg_limit);
+    else rbv_cube<false>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb, segl, seg_limit);
+}
+
+// the segments of the split cubes, RBV_SEGW workgroups per cube (blockIdx.x = cube slot * RBV_SEGW + w)
+constexpr int RBV_SEGW = 8;
+__global__ void __launch_bounds__(RBV_T) k_rb_cubeseg(RbKinds P, const MapState* __restrict__ m) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RbKind& K = P.k[blockIdx.y];
+    const int r = blockIdx.x / RBV_SEGW, w = blockIdx.x % RBV_SEGW;
+    if (r >= m->valid_num) return;
+    const int* segl = K.segl + (size_t)r * LS_SEGL;
+    if (segl[0] == 0) return;
+    const int p0 = K.a.off[m->valid_ind[r]];
+    unsigned long long* EL = (unsigned long long*)(smem + RBV_HDR);
+    ls_sort_list<RBV_T, RBV_CPW>(K.gscr + 4 * (size_t)p0, segl, w, RBV_SEGW, EL, RBV_CAP, (unsigned char*)(EL + RBV_CAP));
+}
+__global__ void __launch_bounds__(RBV_T) k_rb_cubered(RbKinds P, const MapState* __restrict__ m) {
+    __shared__ int sc[16 + 2 * (RBV_T / WAVE) + 2];
+    const RbKind& K = P.k[blockIdx.y];
+    const int r = blockIdx.x;
+    if (r >= m->valid_num) return;
+    if (K.segl[(size_t)r * LS_SEGL] == 0) return;
+    const int c = m->valid_ind[r];
+    const int p0 = K.a.off[c], n = K.a.off[c + 1] - p0;
+    rbv_reduce(K.gscr + 4 * (size_t)p0, K.B, K.a, c, p0, n, K.Cf, sc);
 }
 
 __global__ void __launch_bounds__(1024) k_rb_final_scan(RbKinds P, const unsigned char* __restrict__ valid) {
@@ -971,6 +1009,7 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
         k.v2 = K.ins_val2;
         k.Cf = K.map_tmp;
         k.gscr = K.seg_keys + 32768;
+        k.segl = K.cube_segl;
         k.a = cube_arrays(C, w);
         static const bool bbox_keys = getenv("ALOAM_RB_BBOX") && atoi(getenv("ALOAM_RB_BBOX")) == 1;   // A/B knob
         k.fast_keys = !bbox_keys && k.leaf > 0.f && 53.0 / k.leaf + 2.0 < 1024.0;
@@ -980,7 +1019,13 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     k_rb_sort_scan<<<2, RBS_T, RBS_LDS, st>>>(P, C.d_cube_valid);
     k_rb_scatter<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P);
     prof_phase(C, Ctx::PM_MAP_ADD);
-    k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
+    // tuning knobs: segment size of the split cubes' parallel sorts; cubes up to `fit` points are sorted
+    // whole by their own workgroup, larger ones split
+    static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
+    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_FIT")))) : RBV_CAP;
+    k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit);
+    k_rb_cubeseg<<<dim3(125 * RBV_SEGW, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
+    k_rb_cubered<<<dim3(125, 2), RBV_T, 0, st>>>(P, C.d_map);
     k_rb_final_scan<<<2, 1024, 0, st>>>(P, C.d_cube_valid);
     k_rb_final<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P, C.d_cube_valid);
     prof_phase(C, Ctx::PM_MAP_FILTER);
@@ -992,6 +1037,7 @@ void rebuild_init(Ctx& C) {
     static bool attr = false;
     if (!attr) {
         HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubevox, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBV_LDS));
+        HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubeseg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBV_LDS));
         HIPCHK(hipFuncSetAttribute((const void*)k_rb_sort_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBS_LDS));
         attr = true;
     }

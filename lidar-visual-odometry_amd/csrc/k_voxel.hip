@@ -47,21 +47,20 @@ struct VoxJob {
     const float4* pts; const int* d_n; int cap; float leaf;
     float4* out; int* d_nout;
     unsigned long long* gE;      // global scratch (cap_voxel keys) for clouds above VX_LDS_N
+    int* gseg;                   // their segment list (LS_SEGL ints; count 0: the cloud is done)
 };
 struct VoxJobs { VoxJob j[2]; };
 
-// E: the keys (LDS: EL itself; global: gE, staged through EL by the sort); sc behind EL
-__device__ void vox_sort_and_reduce(const VoxJob& J, int n, unsigned long long* E, unsigned long long* EL, int* sc) {
+// Clouds above VX_LDS_N are sorted by several workgroups: k_vox_pcl splits them into segments of at most
+// g_vox_seg elements, k_vox_seg sorts the segments in parallel (VX_SEGW workgroups per cloud), k_vox_reduce
+// sums the leaves.
+constexpr int VX_SEGW = 16;
+static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : 4096;   // tuning knob
+static_assert(ls_split_scratch_bytes(VX_T, VX_LDS_N) <= ls_global_scratch_bytes(VX_T, VX_LDS_N), "split scratch");
+
+// runs of equal leaves in sorted E -> centroids in leaf order; each run summed in sorted order by its head
+__device__ void vox_reduce(const VoxJob& J, int n, const unsigned long long* E, int* sc) {
     const int tid = threadIdx.x;
-    if (E == EL) {
-        ls_sort<VX_T, VX_CPW>(EL, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, VX_LDS_N);
-    } else if (n <= VX_NMAX) {
-        ls_sort_global<VX_T, VX_CPW>(E, n, EL, VX_LDS_N, (unsigned char*)sc);
-    } else {                                                  // beyond the parallel replay's reach: one thread
-        if (tid == 0) ps_serial_std_sort(E, n);
-        __syncthreads();
-    }
-    // runs of equal leaves -> centroids in leaf order; each run summed in sorted order by its head
     const int C = (n + VX_T - 1) / VX_T;
     const int p0 = min(n, tid * C), p1 = min(n, p0 + C);
     int nh = 0;
@@ -81,7 +80,7 @@ __device__ void vox_sort_and_reduce(const VoxJob& J, int n, unsigned long long* 
     if (tid == 0) *J.d_nout = tot;
 }
 
-__global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P) {
+__global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const VoxJob& J = P.j[blockIdx.x];
     unsigned* bb = (unsigned*)smem;
@@ -90,6 +89,7 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P) {
     const int tid = threadIdx.x;
     // a hinted launch never reads past its launch size (the exact-size redo replaces the result)
     const int n = min(*J.d_n, J.cap);
+    if (n <= VX_LDS_N || n > VX_NMAX) { if (tid == 0) J.gseg[0] = 0; }   // done here (the others: split)
     if (n <= 0) { if (tid == 0) *J.d_nout = 0; return; }
     if (tid < 6) bb[tid] = tid < 3 ? 0xffffffffu : 0u;
     __syncthreads();
@@ -113,20 +113,74 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P) {
     voxel_params(bb, J.leaf, &ovf, minb, &mul1, &mul2);
     if (ovf) {                               // PCL: leaf count overflows int32 -> output = input
         for (int t = tid; t < n; t += VX_T) J.out[t] = J.pts[t];
-        if (tid == 0) *J.d_nout = n;
+        if (tid == 0) { *J.d_nout = n; J.gseg[0] = 0; }
         return;
     }
     const float inv = 1.0f / J.leaf;
-    unsigned long long* E = n <= VX_LDS_N ? EL : J.gE;
+    if (n <= VX_LDS_N) {
+        for (int t = tid; t < n; t += VX_T) EL[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
+        lds_barrier();
+        ls_sort<VX_T, VX_CPW>(EL, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, VX_LDS_N);
+        vox_reduce(J, n, EL, sc);
+        return;
+    }
+    unsigned long long* E = J.gE;
     for (int t = tid; t < n; t += VX_T) E[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
     __syncthreads();
-    vox_sort_and_reduce(J, n, E, EL, sc);
+    if (n <= VX_NMAX) {
+        ls_split_to_list<VX_T>(E, n, seg_limit, J.gseg, (unsigned char*)sc);   // -> k_vox_seg, k_vox_reduce
+        return;
+    }
+    if (tid == 0) ps_serial_std_sort(E, n);   // beyond the parallel replay's reach: one thread (rare)
+    __syncthreads();
+    vox_reduce(J, n, E, sc);
+}
+
+__global__ void __launch_bounds__(VX_T) k_vox_seg(VoxJobs P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const VoxJob& J = P.j[blockIdx.y];
+    if (J.gseg[0] == 0) return;
+    unsigned long long* EL = (unsigned long long*)(smem + VX_HDR);
+    ls_sort_list<VX_T, VX_CPW>(J.gE, J.gseg, blockIdx.x, gridDim.x, EL, VX_LDS_N, (unsigned char*)(EL + VX_LDS_N));
+}
+
+// the leaves of a split cloud, VX_REDW workgroups per cloud: workgroup w owns sorted positions [w R, (w+1) R)
+// and counts the run heads before them itself (a pass over the keys) for its output offset
+constexpr int VX_REDW = 16;
+__global__ void __launch_bounds__(VX_T) k_vox_reduce(VoxJobs P) {
+    __shared__ int sc[16 + 2 * (VX_T / WAVE) + 2];
+    const VoxJob& J = P.j[blockIdx.y];
+    if (J.gseg[0] == 0) return;
+    const int n = min(*J.d_n, J.cap), tid = threadIdx.x;
+    const int R = (n + gridDim.x - 1) / gridDim.x;
+    const int q0 = min(n, (int)blockIdx.x * R), q1 = min(n, q0 + R);
+    const unsigned long long* E = J.gE;
+    int before = 0;
+    for (int p = tid; p < q0; p += VX_T) before += (p == 0 || ps_key(E[p]) != ps_key(E[p - 1]));
+    const int C = (q1 - q0 + VX_T - 1) / VX_T;
+    const int p0 = min(q1, q0 + tid * C), p1 = min(q1, p0 + C);
+    int nh = 0;
+    for (int p = p0; p < p1; p++) nh += (p == 0 || ps_key(E[p]) != ps_key(E[p - 1]));
+    int run = nh, bsum = before, tot, tb;
+    ps_exscan2<VX_T>(run, bsum, sc + 16, tot, tb);
+    run += tb;                                   // heads before this workgroup's range
+    for (int p = p0; p < p1; p++) {
+        const unsigned k = ps_key(E[p]);
+        if (!(p == 0 || k != ps_key(E[p - 1]))) continue;
+        int cnt;
+        const float4 c = ps_run_sum(E, n, p, k, [&](int i) { return J.pts[i]; }, cnt);
+        const float fc = (float)cnt;
+        J.out[run] = make_float4(c.x / fc, c.y / fc, c.z / fc, c.w / fc);
+        run++;
+    }
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) *J.d_nout = tb + tot;
 }
 
 static void vox_attr() {
     static bool done = false;
     if (!done) {
         HIPCHK(hipFuncSetAttribute((const void*)k_vox_pcl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)VX_LDS));
+        HIPCHK(hipFuncSetAttribute((const void*)k_vox_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)VX_LDS));
         done = true;
     }
 }
@@ -137,6 +191,7 @@ static VoxJob vox_job(Ctx& C, KindScratch& K, int which, const float4* pts, cons
     VoxJob j;
     j.pts = pts; j.d_n = d_n; j.cap = cap; j.leaf = leaf; j.out = out; j.d_nout = d_nout;
     j.gE = which == 0 ? K.vkeys : K.vkeys2;
+    j.gseg = which == 0 ? K.vvals : K.vvals2;
     return j;
 }
 
@@ -148,7 +203,11 @@ void voxel_grid_pair_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* pt
     VoxJobs P;
     P.j[0] = vox_job(C, K, 0, ptsA, d_nA, std::max(capA, 0), leafA, outA, d_noutA);
     P.j[1] = vox_job(C, K, 1, ptsB, d_nB, std::max(capB, 0), leafB, outB, d_noutB);
-    k_vox_pcl<<<2, VX_T, VX_LDS, st>>>(P);
+    k_vox_pcl<<<2, VX_T, VX_LDS, st>>>(P, g_vox_seg);
+    if (std::max(capA, capB) > VX_LDS_N) {
+        k_vox_seg<<<dim3(VX_SEGW, 2), VX_T, VX_LDS, st>>>(P);
+        k_vox_reduce<<<dim3(VX_REDW, 2), VX_T, 0, st>>>(P);
+    }
     HIPCHK(hipGetLastError());
 }
 
@@ -159,7 +218,11 @@ void voxel_grid_sorted_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* 
     VoxJobs P;
     P.j[0] = vox_job(C, K, 0, pts, d_n, std::max(cap_n, 0), leaf, out, d_nout);
     P.j[1] = P.j[0];
-    k_vox_pcl<<<1, VX_T, VX_LDS, st>>>(P);
+    k_vox_pcl<<<1, VX_T, VX_LDS, st>>>(P, g_vox_seg);
+    if (cap_n > VX_LDS_N) {
+        k_vox_seg<<<dim3(VX_SEGW, 1), VX_T, VX_LDS, st>>>(P);
+        k_vox_reduce<<<dim3(VX_REDW, 1), VX_T, 0, st>>>(P);
+    }
     HIPCHK(hipGetLastError());
 }
 

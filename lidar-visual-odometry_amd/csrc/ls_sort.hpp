@@ -36,6 +36,10 @@
 namespace aloam {
 
 constexpr int LS_INACT = 0xffff;
+#ifndef LS_TAIL_DEF
+#define LS_TAIL_DEF 256                   // (tests vary it)
+#endif
+constexpr int LS_TAIL = LS_TAIL_DEF;     // the waves take over when every active segment has <= this many elements
 
 // LDS scratch (bytes, 8-byte aligned sections) for n <= nmax elements sorted by NT threads
 __host__ __device__ constexpr int ls_nc(int nmax) { return (nmax + 63) / 64; }
@@ -92,6 +96,202 @@ __device__ __forceinline__ unsigned long long ls_with_seg(unsigned long long e, 
     return (e & ~0xffff0000ull) | ((unsigned long long)(unsigned)s << 16);
 }
 
+__device__ __forceinline__ unsigned long long ls_shfl64(unsigned long long v, int src) {
+    return ((unsigned long long)(unsigned)__shfl((int)(v >> 32), src, WAVE) << 32) | (unsigned)__shfl((int)v, src, WAVE);
+}
+
+// __move_median_to_first(f, f + 1, mid, l - 1) as ps_median_to_first, also returning pick - f
+__device__ __forceinline__ unsigned ls_median_to_first(unsigned long long* E, int f, int l, int* off) {
+    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+    const unsigned ka = ps_key(E[a]), kb = ps_key(E[b]), kc = ps_key(E[c]);
+    int pick;
+    if (ka < kb) pick = kb < kc ? b : (ka < kc ? c : a);
+    else pick = ka < kc ? a : (kb < kc ? c : b);
+    const unsigned long long ef = E[f], ep = E[pick];
+    E[f] = ep;
+    E[pick] = ef;
+    *off = pick - f;
+    return ps_key(ep);
+}
+
+// ---- one wave, one segment (the last, sparse levels) ----------------------------------------------------
+// Whole introsort subtree of a segment [f, f + m), m <= 64, from depth d, in registers: lane i holds
+// position f + i. Every level partitions all of its > 16-element sub-segments at once (each lane knows its
+// sub-segment from the boundary bits): median of (a + 1, mid, b - 1) moved to a, the Hoare swaps LS[j] <->
+// RS[j] for j < k as lane gathers, the cut from k. Depth exhausted: heap sort (std::__partial_sort) of the
+// remaining > 16 sub-segments by one lane each. Then every final sub-segment of <= 16 is stably ranked (the
+// final insertion sort) and written back.
+__device__ __forceinline__ void ws_small(unsigned long long* E, const int f, const int m, int d) {
+    const int lane = lane_id();
+    const unsigned long long lt = lanemask_lt64(), le = lt | (1ull << lane), gt = ~le;
+    const unsigned long long all = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+    const bool in = lane < m;
+    unsigned long long e = in ? E[f + lane] : ~0ull;
+    unsigned k = ps_key(e);
+    unsigned long long starts = 1ull;
+    int a = 0, b = m;
+    for (;;) {
+        a = ps_msb(starts & le);
+        const unsigned long long nb = starts & gt & all;
+        b = nb ? __builtin_ctzll(nb) : m;
+        const bool act = in && b - a > PS_THRESHOLD;
+        if (!__ballot(act)) break;
+        if (d == 0) {                                    // (rare) heap sort the > 16 sub-segments
+            if (in) E[f + lane] = e;
+            ps_wsync<false>();
+            if (act && lane == a) ps_heap_sort(E + f + a, E + f + b);
+            ps_wsync<false>();
+            e = in ? E[f + lane] : ~0ull;
+            k = ps_key(e);
+            ps_wsync<false>();
+            break;
+        }
+        d--;
+        const int mid = a + (b - a) / 2;
+        const unsigned ka = (unsigned)__shfl((int)k, act ? a + 1 : lane, WAVE);
+        const unsigned kb = (unsigned)__shfl((int)k, act ? mid : lane, WAVE);
+        const unsigned kc = (unsigned)__shfl((int)k, act ? b - 1 : lane, WAVE);
+        int pick;
+        if (ka < kb) pick = kb < kc ? mid : (ka < kc ? b - 1 : a + 1);
+        else pick = ka < kc ? a + 1 : (kb < kc ? b - 1 : mid);
+        int src = lane;
+        if (act) src = lane == a ? pick : (lane == pick ? a : lane);
+        e = ls_shfl64(e, src);
+        k = ps_key(e);
+        const unsigned K = (unsigned)__shfl((int)k, act ? a : lane, WAVE);
+        const bool isL = act && lane > a && k >= K, isR = act && k <= K;
+        const unsigned long long mL = __ballot(isL), mR = __ballot(isR);
+        const unsigned long long segm = (b >= 64 ? ~0ull : ((1ull << b) - 1ull)) & ~((1ull << a) - 1ull);
+        const unsigned long long sL = mL & segm, sR = mR & segm;
+        const int nL = __popcll(sL), nR = __popcll(sR);
+        src = lane;
+        bool swL = false;
+        if (isL) {
+            const int j = __popcll(sL & lt);
+            if (j < nR) {
+                const int q = ps_select_bit(sR, nR - 1 - j);
+                if (lane < q) { src = q; swL = true; }
+            }
+        }
+        if (isR && !swL) {
+            const int i = nR - 1 - __popcll(sR & lt);
+            if (i < nL) {
+                const int p2 = ps_select_bit(sL, i);
+                if (p2 < lane) src = p2;
+            }
+        }
+        e = ls_shfl64(e, src);
+        k = ps_key(e);
+        const int kk = __popcll(__ballot(swL) & segm);
+        int cut = 0x7fffffff;
+        if (kk < nL) cut = ps_select_bit(sL, kk);
+        if (kk >= 1) cut = min(cut, ps_select_bit(sR, nR - kk));
+        starts |= __ballot(act && lane == cut);
+    }
+    int r = lane;
+    if (__ballot(in && b - a <= PS_THRESHOLD)) {
+        int c = a;
+#pragma unroll
+        for (int i = 0; i < PS_THRESHOLD; i++) {
+            const unsigned ki = (unsigned)__shfl((int)k, min(a + i, WAVE - 1), WAVE);
+            c += a + i < b && (ki < k || (ki == k && a + i < lane));
+        }
+        if (b - a <= PS_THRESHOLD) r = c;
+    }
+    if (in) E[f + r] = e;
+    ps_wsync<false>();
+}
+
+// Partition of [f, l) (l - f > 64) by one wave; returns the cut. Chunk u = positions f + 64u + lane; lane u
+// keeps chunk u's stop masks and their exclusive prefixes (l - f <= 4096). Right stops are scattered to
+// RS[f + ascending rank]; every left stop of rank j reads its partner RS[j] = RS[f + nR - 1 - j] and swaps
+// when it lies before it (a prefix of the left stops: the loop ends at the first chunk with a refusal).
+// cut = min(first non-swapping left stop, partners of the swapping ones).
+__device__ __forceinline__ int ws_partition(unsigned long long* E, const int f, const int l, unsigned short* RS) {
+    const int lane = lane_id();
+    const unsigned long long lt = lanemask_lt64();
+    int k0 = 0;
+    PS_SAME(k0 = (int)ps_median_to_first(E, f, l));
+    const unsigned K = (unsigned)ps_u(k0);
+    ps_wsync<false>();
+    const int nch = ps_u((l - f + 63) >> 6);
+    unsigned long long myL = 0, myR = 0;
+    for (int u = 0; u < nch; u++) {
+        const int p = f + (u << 6) + lane;
+        const bool inn = p < l;
+        const unsigned kk = inn ? ps_keyat(E, p) : 0u;
+        const unsigned long long bl = __ballot(inn && p > f && kk >= K);
+        const unsigned long long br = __ballot(inn && kk <= K);
+        myL = lane == u ? bl : myL;
+        myR = lane == u ? br : myR;
+    }
+    const int cl = __popcll(myL), cr = __popcll(myR);
+    const int iL = wave_incl_scan(cl), iR = wave_incl_scan(cr);
+    const int pL = iL - cl, pR = iR - cr;
+    const int nR = ps_u(readlane_i(iR, WAVE - 1));
+    for (int u = 0; u < nch; u++) {
+        const unsigned long long bR = ps_rl64(myR, u);
+        const int pRu = ps_u(readlane_i(pR, u));
+        if ((bR >> lane) & 1ull) RS[f + pRu + __popcll(bR & lt)] = (unsigned short)(f + (u << 6) + lane);
+    }
+    ps_wsync<false>();
+    int cand = 0x7fffffff;
+    for (int u = 0; u < nch; u++) {
+        const unsigned long long bL = ps_rl64(myL, u);
+        if (bL == 0ull) continue;
+        const int pLu = ps_u(readlane_i(pL, u));
+        const int p = f + (u << 6) + lane;
+        const bool isL = (bL >> lane) & 1ull;
+        bool sw = false;
+        int q = 0;
+        if (isL) {
+            const int j = pLu + __popcll(bL & lt);
+            if (j < nR) { q = RS[f + nR - 1 - j]; sw = p < q; }
+            cand = min(cand, sw ? q : p);
+        }
+        if (sw) {
+            const unsigned long long ep = E[p], eq = E[q];
+            E[p] = eq;
+            E[q] = ep;
+        }
+        if (__ballot(isL && !sw)) break;                 // the rest of the left stops do not swap
+    }
+    const int cut = ps_u((int)allreduce_u32<6>((unsigned)cand, [](unsigned x, unsigned y) { return x < y ? x : y; }));
+    ps_wsync<false>();
+    PS_CHECK(cut > f && cut < l, "ws cut: f %d l %d cut %d\n", f, l, cut);
+    return cut;
+}
+
+// introsort_loop of one segment by one wave: partitions while > 64 elements (right children on a lane
+// stack), the <= 64-element parts in registers
+__device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, int d, unsigned short* RS) {
+    const int lane = lane_id();
+    int sp = 0, stf = 0, stl = 0, std_ = 0;
+    for (;;) {
+        for (;;) {
+            if (l - f <= WAVE) {
+                if (l - f >= 2) ws_small(E, f, l - f, d);
+                break;
+            }
+            if (d == 0) {
+                PS_SAME(ps_heap_sort(E + f, E + l));
+                ps_wsync<false>();
+                break;
+            }
+            d = ps_u(d - 1);
+            const int cut = ws_partition(E, f, l, RS);
+            stf = lane == sp ? cut : stf;
+            stl = lane == sp ? l : stl;
+            std_ = lane == sp ? d : std_;
+            sp = ps_u(sp + 1);
+            l = ps_u(cut);
+        }
+        if (sp == 0) break;
+        sp = ps_u(sp - 1);
+        f = ps_u(readlane_i(stf, sp)); l = ps_u(readlane_i(stl, sp)); d = ps_u(readlane_i(std_, sp));
+    }
+}
+
 // std::sort(E, E + n) by key (E[i] >> 32) as libstdc++ orders it, from introsort depth d0 (a whole sort:
 // 2 floor(log2 n); a segment of a larger sort: its remaining depth), E and scratch in LDS, n <= NT * CPW,
 // payloads (E[i] & 0xffffffff) < 2^16. All NT threads call it with the same arguments; it ends with a
@@ -116,8 +316,10 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
     if (n > PS_THRESHOLD && d0 > 0) {
         ns = 1;
         if (tid == 0) {
-            S.seg(0, 0)[0] = 0; S.seg(0, 1)[0] = n; S.seg(0, 2)[0] = d0;
-            S.seg(0, 3)[0] = (int)ps_median_to_first(E, 0, n);
+            int o = 0;
+            S.seg(0, 0)[0] = 0; S.seg(0, 1)[0] = n;
+            S.seg(0, 3)[0] = (int)ls_median_to_first(E, 0, n, &o);
+            S.seg(0, 2)[0] = d0 | (o << 8);
         }
     } else if (n > PS_THRESHOLD) {
         if (tid == 0) ps_heap_sort(E, E + n);
@@ -234,9 +436,10 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         {
             unsigned long long* actn = S.act + (b ? 0 : 32);
             int* cnt = &S.hdr[8 + (b ^ 1)];
+            int* mx = &S.hdr[12 + (b ^ 1)];
             int aL = 0, aR = 0, f = 0, l = 0, cut = 0, d = 0;
             if (tid < ns) {
-                f = F[tid]; l = L[tid]; d = D[tid] - 1; cut = S.cut[tid];
+                f = F[tid]; l = L[tid]; d = (D[tid] & 0xff) - 1; cut = S.cut[tid];
                 PS_CHECK(cut > f && cut < l, "ls cut: f %d l %d cut %d\n", f, l, cut);
                 atomicOr(&S.bits[cut >> 6], 1ull << (cut & 63));
                 if (cut - f > PS_THRESHOLD) { if (d > 0) aL = 1; else ps_heap_sort(E + f, E + cut); }
@@ -252,9 +455,13 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             int* Dn = S.seg(b ^ 1, 2);
             int* Kn = S.seg(b ^ 1, 3);
             if (tid < ns) {
-                if (aL) { Fn[base] = f; Ln[base] = cut; Dn[base] = d; Kn[base] = (int)ps_median_to_first(E, f, cut); }
-                if (aR) { Fn[base + aL] = cut; Ln[base + aL] = l; Dn[base + aL] = d; Kn[base + aL] = (int)ps_median_to_first(E, cut, l); }
+                // D: depth | (median position - f) << 8 (the wave tail undoes the median move)
+                int o = 0;
+                if (aL) { Fn[base] = f; Ln[base] = cut; Kn[base] = (int)ls_median_to_first(E, f, cut, &o); Dn[base] = d | (o << 8); }
+                if (aR) { Fn[base + aL] = cut; Ln[base + aL] = l; Kn[base + aL] = (int)ls_median_to_first(E, cut, l, &o); Dn[base + aL] = d | (o << 8); }
                 S.idx[tid] = (aL ? base : LS_INACT) | ((aR ? base + aL : LS_INACT) << 16);
+                const int big = max(aL ? cut - f : 0, aR ? l - cut : 0);
+                if (big) atomicMax(mx, big);
                 const int lo = aL ? f : cut, hi = aR ? l : cut;       // positions of the active children
                 if (hi > lo) {
                     const int c0 = lo >> 6, c1 = (hi - 1) >> 6;          // their chunks, a word at a time
@@ -269,10 +476,21 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         lds_barrier();
         ns = S.hdr[8 + (b ^ 1)];
         // this level's counter and active chunks reset for the level after next
-        if (tid == 0) S.hdr[8 + b] = 0;
+        if (tid == 0) { S.hdr[8 + b] = 0; S.hdr[12 + b] = 0; }
         if (tid < 32) S.act[(b ? 32 : 0) + tid] = 0ull;
         LS_TS(5);
         b ^= 1;
+        // the sparse tail: once at most one active segment per wave is left and each is short, the waves
+        // finish them independently (no workgroup barriers per level)
+        if (ns > 0 && ns <= W && S.hdr[12 + b] <= LS_TAIL) {
+            if (wid < ns) {
+                const int sf = ps_u(S.seg(b, 0)[wid]), sl = ps_u(S.seg(b, 1)[wid]), sd = ps_u(S.seg(b, 2)[wid]);
+                PS_SAME({ const unsigned long long t_ = E[sf]; E[sf] = E[sf + (sd >> 8)]; E[sf + (sd >> 8)] = t_; });   // undo the median move
+                ps_wsync<false>();
+                ws_segment(E, sf, sl, sd & 0xff, S.rs);
+            }
+            ns = 0;
+        }
     }
     LS_TS(6);
     // final insertion sort (stable, whole array): every element ranked inside its leaf (<= 16 elements
@@ -372,6 +590,59 @@ __device__ __noinline__ void ls_sort_global_lds(unsigned long long* gE, const in
 template <int NT, int CPW>
 __device__ __forceinline__ void ls_sort_global(unsigned long long* gE, const int n, unsigned long long* EL, const int cap, unsigned char* scratch) {
     ls_sort_global_lds<NT, CPW>(gE, n, (lds_u64*)EL, cap, (lds_u8*)scratch);
+}
+
+// ---- sorts over several workgroups -------------------------------------------------------------------
+// A large array is split by one workgroup (the workgroup phase of pcl_sort.hpp on global memory) until
+// every segment has <= limit elements; the segment list goes to global memory (gseg: count, then f, l,
+// depth + 1 per segment) and the segments are then sorted by other workgroups in parallel (ls_sort_list),
+// each independent of the others (introsort's recursion below a partition only sees its own range).
+constexpr int LS_SEGL = 1 + 3 * PS_GLIST;       // ints per segment list
+__host__ __device__ constexpr size_t ls_split_scratch_bytes(int NT, int limit) {
+    return 4 * (size_t)(16 + 3 * PS_GLIST) + 4 * (size_t)ps_scratch_ints(NT, limit, true);
+}
+template <int NT>
+__device__ __noinline__ void ls_split_to_list_lds(unsigned long long* gE, const int n, const int limit, int* gseg, lds_u8* scrs) {
+    int* H = (int*)(unsigned char*)scrs;
+    int* GL = H + 16;
+    int* wsc = GL + 3 * PS_GLIST;
+    const int tid = threadIdx.x;
+    if (tid < 16) { H[tid] = 0; wsc[tid] = 0; }
+    for (int i = tid; i < 3 * PS_GLIST; i += NT) GL[i] = 0;
+    int* Bf = wsc + 16 + 2 * (NT / WAVE) + 7 * (NT + 1);
+    const int D0 = n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0;
+    __syncthreads();
+    if (tid == 0) {
+        if (n > limit) { Bf[0] = 0; Bf[PS_WGSEG] = n; Bf[2 * PS_WGSEG] = D0; wsc[0] = 1; }
+        else if (n >= 2) { GL[0] = 0; GL[1] = n; GL[2] = D0 + 1; H[4] = 1; }
+    }
+    __syncthreads();
+    if (n > limit) ps_wg_split<NT, true>(gE, n, wsc, limit, &H[4], &H[5], GL, PS_GLIST);
+    __syncthreads();
+    const int ns = min(H[4], PS_GLIST);
+    for (int i = tid; i < 3 * ns; i += NT) gseg[1 + i] = GL[i];
+    if (tid == 0) gseg[0] = ns;
+}
+template <int NT>
+__device__ __forceinline__ void ls_split_to_list(unsigned long long* gE, const int n, const int limit, int* gseg, unsigned char* scratch) {
+    ls_split_to_list_lds<NT>(gE, n, limit, gseg, (lds_u8*)scratch);
+}
+// segments w, w + nw, ... of the list: each copied into EL (cap elements of LDS), sorted by ls_sort from
+// its remaining depth, copied back
+template <int NT, int CPW>
+__device__ __forceinline__ void ls_sort_list(unsigned long long* gE, const int* gseg, int w, int nw, unsigned long long* EL,
+                                             const int cap, unsigned char* scratch) {
+    const int tid = threadIdx.x;
+    const int ns = min(gseg[0], PS_GLIST);
+    for (int i = w; i < ns; i += nw) {
+        const int f = gseg[1 + 3 * i], l = gseg[2 + 3 * i], d = gseg[3 + 3 * i] - 1;
+        const int m = l - f;
+        for (int t = tid; t < m; t += NT) EL[t] = gE[f + t];
+        __syncthreads();
+        ls_sort<NT, CPW>(EL, m, d, scratch, cap);
+        for (int t = tid; t < m; t += NT) gE[f + t] = EL[t];
+        __syncthreads();
+    }
 }
 
 }  // namespace aloam

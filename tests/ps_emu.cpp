@@ -101,6 +101,11 @@ static inline int atomicMin(int* p, int v) {
     return o;
 }
 static inline unsigned long long atomicOr(unsigned long long* p, unsigned long long v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
+static inline int atomicMax(int* p, int v) {
+    int o = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+    while (v > o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {}
+    return o;
+}
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
 #define __hip_atomic_fetch_add(p, v, o, sc) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
 #define __hip_atomic_load(p, o, sc) __atomic_load_n((p), __ATOMIC_SEQ_CST)

@@ -23,9 +23,14 @@ def test_device_sort_matches_libstdcxx_under_emulation(emu):
     assert "mismatches 0" in r.stdout
 
 
-def test_ls_sort_matches_libstdcxx_under_emulation(emu):
-    # csrc/ls_sort.hpp on 2 emulated waves (n <= 128 * 16): every introsort level of every segment at once
-    r = subprocess.run([emu, "50", "13", "1"], capture_output=True, text=True, timeout=600)
+@pytest.mark.parametrize("tail", [None, 4096], ids=["default_tail", "waves_early"])
+def test_ls_sort_matches_libstdcxx_under_emulation(tmp_path, tail):
+    # csrc/ls_sort.hpp on 2 emulated waves (n <= 128 * 16): every introsort level of every segment at once,
+    # the sparse tail per wave (LS_TAIL 4096: the waves take over as soon as <= 2 segments are active)
+    exe = tmp_path / "ls_emu"
+    defs = [f"-DLS_TAIL_DEF={tail}"] if tail else []
+    subprocess.check_call(["g++", "-std=c++20", "-O1", "-pthread", "-w", *defs, "-o", str(exe), os.path.join(HERE, "ps_emu.cpp")])
+    r = subprocess.run([str(exe), "40", "13", "1"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
 
