@@ -261,6 +261,8 @@ static void allocate(Ctx& C) {
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_scan, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_lf, hipEventDisableTiming));
     HIPCHK(hipHostMalloc((void**)&C.h_meta_pin, sizeof(ScanMeta), hipHostMallocMapped));
     std::memset(C.h_meta_pin, 0, sizeof(ScanMeta));
     for (auto& e : C.ev_mdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -327,8 +329,13 @@ static float evh_ms(hipEvent_t a, hipEvent_t b) {
 // scanRegistration's counts reach the host without a sync of their own: the copy is queued behind the
 // registration kernels and read at the next sync of the stream (ensure_meta, or the odometry's result sync)
 static void queue_meta(Ctx& C) {
+    if (C.lf_pending) {                   // counts[4] comes from the per-line VoxelGrid on stream2
+        HIPCHK(hipStreamWaitEvent(C.stream, C.ev_lf, 0));
+        C.lf_pending = false;
+    }
     d2h_small(C.h_meta_pin, C.d_meta, sizeof(ScanMeta), C.stream);
     C.meta_pending = true;
+    C.meta_deferred = false;
 }
 static void apply_meta(Ctx& C) {   // the stream has been synchronised since queue_meta
     C.h_meta = *C.h_meta_pin;
@@ -341,6 +348,7 @@ static void apply_meta(Ctx& C) {   // the stream has been synchronised since que
 }
 static void ensure_meta(Ctx& C) {
     if (!C.meta_pending) return;
+    if (C.meta_deferred) queue_meta(C);
     sync(C);
     apply_meta(C);
 }
@@ -375,7 +383,9 @@ static void front_phase(Ctx& C, int k) {
     if (k == 4) used = true;
 }
 
-static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
+// defer: the odometry follows in the same call (front_issue, aloam_process_scan): the per-line VoxelGrid
+// runs on stream2 beside the odometry rounds and the counts copy is queued behind it (do_odometry_issue)
+static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags, bool defer = false) {
     if (n < 0 || (n > 0 && !xyzr)) throw ApiError{ALOAM_E_ARG, "bad input"};
     if (n > C.cap_in) throw ApiError{ALOAM_E_CAPACITY, "scan larger than max_scan_points"};
     const int L = C.P.scan_line;
@@ -389,10 +399,17 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags) {
     }
     prof_mark(C, 0);
     if (g_front_phases) front_phase(C, 0);
-    scan_registration_launch(C, in, n);
+    const bool side = defer && !C.profiling;
+    scan_registration_launch(C, in, n, side);
+    if (side) C.lf_pending = true;
     if (g_front_phases) front_phase(C, 1);
     prof_mark(C, 1);
-    queue_meta(C);
+    if (side) {
+        C.meta_pending = true;
+        C.meta_deferred = true;
+    } else {
+        queue_meta(C);
+    }
     if (C.profiling) {
         ensure_meta(C);
         C.timing.scan_registration_ms = ev_ms(C, 0, 1);
@@ -484,7 +501,9 @@ static void do_odometry_issue(Ctx& C) {
         }
         if (g_front_phases) front_phase(C, 3);
         prof_phase(C, Ctx::PM_ODOM_ROUNDS_END);
-        // pairs with build_last_grids(C, true) below; the new last-cloud counts from the device meta
+        // the less-flat cloud (stream2) and the counts copy, then the compose; pairs with
+        // build_last_grids(C, true) below; the new last-cloud counts from the device meta
+        if (C.meta_deferred) queue_meta(C);
         odom_compose(C, C.n_lsharp, C.n_lflat, pend ? C.d_meta->counts : nullptr);
         C.odom_spread_dirty = false;
     }
@@ -632,7 +651,7 @@ static void do_odometry(Ctx& C, aloam_odom_result* R) {
 
 void front_issue(Ctx& C, const float* xyzr, int n, int flags) {
     HIPCHK(hipSetDevice(C.device));
-    do_scan_registration(C, xyzr, n, flags);
+    do_scan_registration(C, xyzr, n, flags, true);
     do_odometry_issue(C);
 }
 void front_complete(Ctx& C, aloam_odom_result* R) {
@@ -1004,6 +1023,8 @@ void aloam_destroy(aloam_ctx* ctx) {
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
     if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
+    if (C->ev_scan) (void)hipEventDestroy(C->ev_scan);
+    if (C->ev_lf) (void)hipEventDestroy(C->ev_lf);
     if (C->h_meta_pin) (void)hipHostFree(C->h_meta_pin);
     for (auto e : C->ev_mdone) if (e) (void)hipEventDestroy(e);
     for (auto& m : C->mset) {
@@ -1243,7 +1264,7 @@ int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out) {
 
 int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags, aloam_odom_result* o, aloam_map_result* m) {
     API_BEGIN(ctx)
-    do_scan_registration(C, xyzr, n, flags);
+    do_scan_registration(C, xyzr, n, flags, true);
     aloam_odom_result od{};
     do_odometry(C, &od);
     if (o) *o = od;

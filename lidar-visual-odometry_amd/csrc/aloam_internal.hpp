@@ -118,6 +118,7 @@ struct Ctx {
     hipStream_t stream2 = nullptr;   // mapping: the surf half of the per-kind work runs here (fork/join)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_handoff = nullptr; // device-to-device hand-offs: the source stream waits on it
+    hipEvent_t ev_scan = nullptr, ev_lf = nullptr;   // per-line VoxelGrid on stream2: after the line kernel / done
     bool profiling = false;
     aloam_timing timing{};
     std::vector<DevBuf> bufs;
@@ -147,6 +148,8 @@ struct Ctx {
     ScanMeta h_meta{};
     ScanMeta* h_meta_pin = nullptr;  // pinned landing slot of the async meta copy
     bool meta_pending = false;       // scanRegistration's counts are in flight to h_meta_pin (no sync yet)
+    bool lf_pending = false;         // the per-line VoxelGrid runs on stream2 (stream waits on ev_lf before its results)
+    bool meta_deferred = false;      // the counts copy is queued later (queue_meta, behind the ev_lf wait)
     int last_nslots = 0;             // the previous scan's odometry factor count (LM grid hint)
     int stack_hint[2] = {0, 0};      // launch / sort sizes of the next publish's stack VoxelGrids (0: caps)
     // scanRegistration outputs (the "current" features)
@@ -319,7 +322,7 @@ struct ApiError {
 };
 
 // ---- launch entry points (defined in the k_*.hip files) ----
-void scan_registration_launch(Ctx& C, const float4* in, int n);
+void scan_registration_launch(Ctx& C, const float4* in, int n, bool side);
 void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, const int* cube_of, const unsigned char* cube_valid);
 struct GridBuild { Grid* g; const float4* pts; const int* d_n; int cap_n; const int* cube_of; const unsigned char* cube_valid; };
 constexpr int GRID_MULTI_MAX = 6;

@@ -929,7 +929,7 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
 }
 
 // the segments of the split cubes, RBV_SEGW workgroups per cube (blockIdx.x = cube slot * RBV_SEGW + w)
-constexpr int RBV_SEGW = 8;
+constexpr int RBV_SEGW = 16;
 __global__ void __launch_bounds__(RBV_T) k_rb_cubeseg(RbKinds P, const MapState* __restrict__ m) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RbKind& K = P.k[blockIdx.y];
@@ -1022,7 +1022,7 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     // tuning knobs: segment size of the split cubes' parallel sorts; cubes up to `fit` points are sorted
     // whole by their own workgroup, larger ones split
     static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
-    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_FIT")))) : RBV_CAP;
+    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_FIT")))) : 4096;
     k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit);
     k_rb_cubeseg<<<dim3(125 * RBV_SEGW, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
     k_rb_cubered<<<dim3(125, 2), RBV_T, 0, st>>>(P, C.d_map);

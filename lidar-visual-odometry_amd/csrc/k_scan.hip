@@ -696,99 +696,16 @@ __device__ __forceinline__ void line_features_body(const float4* __restrict__ cl
     }
     const int nc = s_ncand;
     LF_TS(3);
-    // ---- VoxelGrid(0.2) of the candidates (PCL 1.8 applyFilter), points summed in PCL's order ----
-    if (threadIdx.x < 6) s_bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    __syncthreads();
-    {
-        unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-        for (int t = threadIdx.x; t < nc; t += LT) {
-            int k = S[t];
-            unsigned v[3] = {f2ord(X[k]), f2ord(Y[k]), f2ord(Z[k])};
-            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
-        }
-#pragma unroll
-        for (int d = 0; d < 3; d++) {
-            mn[d] = allreduce_u32<6>(mn[d], [](unsigned a, unsigned b) { return min(a, b); });
-            mx[d] = allreduce_u32<6>(mx[d], [](unsigned a, unsigned b) { return max(a, b); });
-        }
-        if (lane_id() == 0)
-            for (int d = 0; d < 3; d++) { atomicMin(&s_bb[d], mn[d]); atomicMax(&s_bb[3 + d], mx[d]); }
-    }
-    __syncthreads();
-    const float inv = 1.0f / 0.2f;
-    float minp[3], maxp[3];
-    for (int d = 0; d < 3; d++) { minp[d] = ord2f(s_bb[d]); maxp[d] = ord2f(s_bb[3 + d]); }
-    long long ddx = (long long)((maxp[0] - minp[0]) * inv) + 1;
-    long long ddy = (long long)((maxp[1] - minp[1]) * inv) + 1;
-    long long ddz = (long long)((maxp[2] - minp[2]) * inv) + 1;
-    const bool overflow = ddx * ddy * ddz > 2147483647LL;
-    int minb[3], divb[3];
-    for (int d = 0; d < 3; d++) {
-        minb[d] = (int)floorf(minp[d] * inv);
-        int maxb = (int)floorf(maxp[d] * inv);
-        divb[d] = maxb - minb[d] + 1;
-    }
-    const int mul1 = divb[0], mul2 = divb[0] * divb[1];
-    for (int t = threadIdx.x; t < nc; t += LT) {
-        const int k = S[t];
-        unsigned idx;
-        if (overflow) idx = (unsigned)t;   // PCL copies the input through unchanged
-        else {
-            int i0 = (int)(floorf(X[k] * inv) - (float)minb[0]);
-            int i1 = (int)(floorf(Y[k] * inv) - (float)minb[1]);
-            int i2 = (int)(floorf(Z[k] * inv) - (float)minb[2]);
-            idx = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
-        }
-        keys[t] = ((unsigned long long)idx << 32) | (unsigned)t;
-    }
-    __syncthreads();
-    LF_TS(4);
-    // PCL's order of the (leaf, index) pairs: libstdc++ std::sort by leaf (pcl_sort.hpp); LDS lines keep
-    // the sort's scratch in the merge-sort buffer, big lines in their (unused) LDS arrays.
-    constexpr int LINE_CPW = LINE_LDS_CAP / LT;    // ls_sort: 64-position chunks per wave
-    static_assert((size_t)LINE_LDS_CAP * 8 >= ls_scratch_bytes(LT, LINE_LDS_CAP) && LINE_CPW * LT == LINE_LDS_CAP, "sort scratch in the sort buffer");
-    constexpr int LINE_STAGE_CPW = 10;
-    constexpr int LINE_STAGE = LT * LINE_STAGE_CPW;   // big lines: sort segments staged through the (unused) LDS arrays
-    static_assert(line_lds_bytes() - LINE_HDR >= 8 * (size_t)LINE_STAGE + ls_global_scratch_bytes(LT, LINE_STAGE), "big lines: sort staging in LDS");
-    if (!big) {
-        ls_sort<LT, LINE_CPW>(keys, nc, nc > 1 ? 2 * (31 - __builtin_clz((unsigned)nc)) : 0, (unsigned char*)sorted, LINE_LDS_CAP);
-    } else if (nc <= LT * PS_MAX_CHUNK) {
-        ls_sort_global<LT, LINE_STAGE_CPW>(keys, nc, (unsigned long long*)smem, LINE_STAGE, smem + 8 * (size_t)LINE_STAGE);
-    } else {
-        if (threadIdx.x == 0) ps_serial_std_sort(keys, nc);
-        __syncthreads();
-    }
-    LF_TS(5);
-    // run heads -> centroids; run r's head position stored in S[nc + r] region? reuse Cv as int
-    int* heads = (int*)Cv;   // curvature no longer needed
-    if (threadIdx.x == 0) s_nrun = 0;
-    __syncthreads();
-    for (int base = 0; base < nc; base += LT) {
-        const int t = base + threadIdx.x;
-        const int flag = t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32));
-        const unsigned long long mk = __ballot(flag);
-        if (lanei == 0) s_wsum[wi] = __popcll(mk);
-        __syncthreads();
-        int before = s_nrun;
-        for (int ww = 0; ww < wi; ww++) before += s_wsum[ww];
-        if (flag) heads[before + __popcll(mk & lanemask_lt64())] = t;
-        __syncthreads();
-        if (threadIdx.x == 0) { int tt = 0; for (int ww = 0; ww < LT / WAVE; ww++) tt += s_wsum[ww]; s_nrun += tt; }
-        __syncthreads();
-    }
-    const int nrun = s_nrun;
-    LF_TS(6);
-    for (int r = threadIdx.x; r < nrun; r += LT) {
-        const int h0 = heads[r], h1 = (r + 1 < nrun) ? heads[r + 1] : nc;
-        int nrs;                                          // CentroidPoint: from zero, in sorted order
-        const float4 c = ps_run_sum(keys, nc, h0, ps_key(keys[h0]), [&](int i) { return cloud[off0 + S[i]]; }, nrs);
-        const float cnt = (float)(h1 - h0);
-        line_lf[off0 + r] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+    // ---- the less-flat candidates (line-relative indices, scan order) and their count for k_line_vox,
+    // which filters them (VoxelGrid 0.2, PCL order) on its own, possibly on another stream ----
+    if constexpr (!big) {
+        int* gS = g_i + off0;
+        for (int t = threadIdx.x; t < nc; t += LT) gS[t] = S[t];
     }
     if (threadIdx.x == 0) {
-        cnt_out[0] = s_cnt[0]; cnt_out[1] = s_cnt[1]; cnt_out[2] = s_cnt[2]; cnt_out[3] = nrun;
+        cnt_out[0] = s_cnt[0]; cnt_out[1] = s_cnt[1]; cnt_out[2] = s_cnt[2]; cnt_out[3] = nc;
     }
-    LF_TS(7);
+    LF_TS(4);
 }
 
 // oversized lines (rare): not inlined, so their global-scratch body does not load the LDS path's registers
@@ -807,6 +724,161 @@ __global__ void __launch_bounds__(LT) k_line_features(const float4* __restrict__
     const int nl_ = meta->line_off[blockIdx.x + 1] - meta->line_off[blockIdx.x];
     if (nl_ > LINE_LDS_CAP) line_features_big(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, (lds_u8*)smem_raw);
     else line_features_body<false>(cloud, gcurv, meta, N_SCANS, g_xyz, g_keys, g_i, line_sharp, line_lsharp, line_flat, line_cnt, line_lf, smem_raw);
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-line VoxelGrid(0.2) of the less-flat candidates (:401-405, PCL 1.8 applyFilter), points summed in
+// PCL's order (ls_sort.hpp), one workgroup per line. Its own kernel so that it can run on the context's
+// second stream beside the odometry rounds, which do not read the less-flat cloud (it is needed from the
+// last-cloud swap on). Reads the candidates k_line_features left (line-relative indices, scan order, at
+// g_i + line offset; their count in line_cnt[4 line + 3]) and writes the leaves' centroids + their count.
+constexpr int LV_STAGE_CPW = 10;
+constexpr int LV_STAGE = LT * LV_STAGE_CPW;              // big lines: sort segments staged through LDS
+constexpr size_t LV_HDR = 256;
+constexpr size_t lv_lds_bytes() {
+    const size_t lds_line = 8 * (size_t)LINE_LDS_CAP + ls_scratch_bytes(LT, LINE_LDS_CAP) + 4 * (size_t)LINE_LDS_CAP;
+    const size_t big_line = 8 * (size_t)LV_STAGE + ls_global_scratch_bytes(LT, LV_STAGE);
+    return LV_HDR + (lds_line > big_line ? lds_line : big_line);
+}
+static_assert(lv_lds_bytes() <= 160 * 1024, "LDS");
+template <bool BIG>
+__device__ __forceinline__ void line_vox_body(const float4* __restrict__ cloud, const ScanMeta* meta, float4* g_xyz,
+                                              unsigned long long* g_keys, int* g_i, int* line_cnt, float4* line_lf,
+                                              unsigned char* smem_raw) {
+    struct VS { unsigned bb[6]; int nrun; int pad; int wsum[LT / WAVE]; };
+    static_assert(sizeof(VS) <= LV_HDR, "VS");
+    VS& SH = *(VS*)smem_raw;
+    unsigned char* smem = smem_raw + LV_HDR;
+    const int line = blockIdx.x;
+    const int off0 = meta->line_off[line];
+    int* cnt_out = line_cnt + line * 4;
+    const int nc = cnt_out[3];
+    const int* S = g_i + off0;
+    const int lanei = lane_id(), wi = threadIdx.x / WAVE;
+    __syncthreads();                      // every thread has read nc before thread 0 overwrites it
+    if (nc <= 0) { if (threadIdx.x == 0) cnt_out[3] = 0; return; }
+    unsigned long long* keys;
+    int* heads;
+    if constexpr (!BIG) {
+        keys = (unsigned long long*)smem;
+        heads = (int*)(smem + 8 * (size_t)LINE_LDS_CAP + ls_scratch_bytes(LT, LINE_LDS_CAP));
+    } else {
+        keys = g_keys + 2 * (size_t)off0;
+        heads = (int*)(g_xyz) + 3 * (size_t)meta->cloud_size + off0;
+    }
+    if (threadIdx.x < 6) SH.bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    {
+        unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+        for (int t = threadIdx.x; t < nc; t += LT) {
+            const float4 p = cloud[off0 + S[t]];
+            const unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
+            for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
+        }
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            mn[d] = allreduce_u32<6>(mn[d], [](unsigned a, unsigned b) { return min(a, b); });
+            mx[d] = allreduce_u32<6>(mx[d], [](unsigned a, unsigned b) { return max(a, b); });
+        }
+        if (lanei == 0)
+            for (int d = 0; d < 3; d++) { atomicMin(&SH.bb[d], mn[d]); atomicMax(&SH.bb[3 + d], mx[d]); }
+    }
+    __syncthreads();
+    const float inv = 1.0f / 0.2f;
+    float minp[3], maxp[3];
+    for (int d = 0; d < 3; d++) { minp[d] = ord2f(SH.bb[d]); maxp[d] = ord2f(SH.bb[3 + d]); }
+    const long long ddx = (long long)((maxp[0] - minp[0]) * inv) + 1;
+    const long long ddy = (long long)((maxp[1] - minp[1]) * inv) + 1;
+    const long long ddz = (long long)((maxp[2] - minp[2]) * inv) + 1;
+    const bool overflow = ddx * ddy * ddz > 2147483647LL;
+    int minb[3], divb[3];
+    for (int d = 0; d < 3; d++) {
+        minb[d] = (int)floorf(minp[d] * inv);
+        const int maxb = (int)floorf(maxp[d] * inv);
+        divb[d] = maxb - minb[d] + 1;
+    }
+    const int mul1 = divb[0], mul2 = divb[0] * divb[1];
+    for (int t = threadIdx.x; t < nc; t += LT) {
+        const float4 p = cloud[off0 + S[t]];
+        unsigned idx;
+        if (overflow) idx = (unsigned)t;   // PCL copies the input through unchanged
+        else {
+            const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+            const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+            const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+            idx = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+        }
+        keys[t] = ((unsigned long long)idx << 32) | (unsigned)t;
+    }
+    __syncthreads();
+    // PCL's order of the (leaf, index) pairs: libstdc++ std::sort by leaf (ls_sort.hpp)
+    constexpr int LINE_CPW = LINE_LDS_CAP / LT;
+    static_assert(LINE_CPW * LT == LINE_LDS_CAP, "LDS lines: whole chunks per wave");
+    if (!BIG) {
+        ls_sort<LT, LINE_CPW>(keys, nc, nc > 1 ? 2 * (31 - __builtin_clz((unsigned)nc)) : 0, smem + 8 * (size_t)LINE_LDS_CAP, LINE_LDS_CAP);
+    } else if (nc <= LT * PS_MAX_CHUNK) {
+        ls_sort_global<LT, LV_STAGE_CPW>(keys, nc, (unsigned long long*)smem, LV_STAGE, smem + 8 * (size_t)LV_STAGE);
+    } else {
+        if (threadIdx.x == 0) ps_serial_std_sort(keys, nc);
+        __syncthreads();
+    }
+    // run heads -> centroids (CentroidPoint: from zero, in sorted order)
+    if (threadIdx.x == 0) SH.nrun = 0;
+    __syncthreads();
+    for (int base = 0; base < nc; base += LT) {
+        const int t = base + threadIdx.x;
+        const int flag = t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32));
+        const unsigned long long mk = __ballot(flag);
+        if (lanei == 0) SH.wsum[wi] = __popcll(mk);
+        __syncthreads();
+        int before = SH.nrun;
+        for (int ww = 0; ww < wi; ww++) before += SH.wsum[ww];
+        if (flag) heads[before + __popcll(mk & lanemask_lt64())] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) { int tt = 0; for (int ww = 0; ww < LT / WAVE; ww++) tt += SH.wsum[ww]; SH.nrun += tt; }
+        __syncthreads();
+    }
+    const int nrun = SH.nrun;
+    for (int r = threadIdx.x; r < nrun; r += LT) {
+        const int h0 = heads[r], h1 = (r + 1 < nrun) ? heads[r + 1] : nc;
+        int nrs;
+        const float4 c = ps_run_sum(keys, nc, h0, ps_key(keys[h0]), [&](int i) { return cloud[off0 + S[i]]; }, nrs);
+        const float cnt = (float)(h1 - h0);
+        line_lf[off0 + r] = make_float4(c.x / cnt, c.y / cnt, c.z / cnt, c.w / cnt);
+    }
+    if (threadIdx.x == 0) cnt_out[3] = nrun;
+}
+__device__ __noinline__ void line_vox_big(const float4* __restrict__ cloud, const ScanMeta* meta, float4* g_xyz,
+                                          unsigned long long* g_keys, int* g_i, int* line_cnt, float4* line_lf, lds_u8* smem) {
+    line_vox_body<true>(cloud, meta, g_xyz, g_keys, g_i, line_cnt, line_lf, (unsigned char*)smem);
+}
+__global__ void __launch_bounds__(LT) k_line_vox(const float4* __restrict__ cloud, const ScanMeta* meta, float4* g_xyz,
+                                                 unsigned long long* g_keys, int* g_i, int* line_cnt, float4* line_lf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int nc = line_cnt[blockIdx.x * 4 + 3];
+    if (nc > LINE_LDS_CAP) line_vox_big(cloud, meta, g_xyz, g_keys, g_i, line_cnt, line_lf, (lds_u8*)smem_raw);
+    else line_vox_body<false>(cloud, meta, g_xyz, g_keys, g_i, line_cnt, line_lf, smem_raw);
+}
+
+// the less-flat cloud in line order and its count (the other kinds: k_concat)
+__global__ void k_concat_lf(const int* line_cnt, const float4* line_lf, int N_SCANS, ScanMeta* meta, float4* lflat) {
+    const int line = blockIdx.x;
+    __shared__ int sh_o, sh_tot;
+    if (threadIdx.x == 0) { sh_o = 0; sh_tot = 0; }
+    __syncthreads();
+    {
+        const int l = threadIdx.x;
+        const int v = l < N_SCANS ? line_cnt[l * 4 + 3] : 0;
+        if (threadIdx.x < WAVE * ((N_SCANS + WAVE - 1) / WAVE)) {
+            const int a = wave_sum_i(l < line ? v : 0), b = wave_sum_i(v);
+            if (lane_id() == 0) { if (a) atomicAdd(&sh_o, a); if (b) atomicAdd(&sh_tot, b); }
+        }
+    }
+    __syncthreads();
+    const int o = sh_o, n = line_cnt[line * 4 + 3];
+    const int off0 = meta->line_off[line];
+    for (int t = threadIdx.x; t < n; t += blockDim.x) lflat[o + t] = line_lf[off0 + t];
+    if (line == 0 && threadIdx.x == 0) meta->counts[4] = sh_tot;
 }
 
 // concatenate per-line outputs in line order (:304-310,356,407)
@@ -848,11 +920,9 @@ __global__ void k_concat(const float4* __restrict__ cloud, const int* line_sharp
         int i = line_flat[line * LINE_FLAT_CAP + t];
         flat[o[2] + t] = cloud[i]; flat_idx[o[2] + t] = i;
     }
-    const int off0 = meta->line_off[line];
-    for (int t = threadIdx.x; t < lc[3]; t += blockDim.x) lflat[o[3] + t] = line_lf[off0 + t];
     if (line == 0 && threadIdx.x == 0) {
         meta->counts[0] = meta->cloud_size;
-        meta->counts[1] = tot[0]; meta->counts[2] = tot[1]; meta->counts[3] = tot[2]; meta->counts[4] = tot[3];
+        meta->counts[1] = tot[0]; meta->counts[2] = tot[1]; meta->counts[3] = tot[2];
         odom_nq[0] = tot[0]; odom_nq[1] = tot[2];   // the odometry's query counts (sharp, flat), no host round trip
     }
 }
@@ -866,7 +936,8 @@ __global__ void k_meta_init(ScanMeta* m, int n_in, int* odom_nq) {
 }
 
 // ------------------------------------------------------------------------------------------
-void scan_registration_launch(Ctx& C, const float4* in, int n) {
+// side: the per-line VoxelGrid (k_line_vox, k_concat_lf) on stream2 behind an event (ev_lf marks it done)
+void scan_registration_launch(Ctx& C, const float4* in, int n, bool side) {
     const aloam_params& P = C.P;
     const int N_SCANS = P.scan_line;
     hipStream_t st = C.stream;
@@ -891,6 +962,21 @@ void scan_registration_launch(Ctx& C, const float4* in, int n) {
         k_concat<<<N_SCANS, 256, 0, st>>>(C.d_cloud, C.d_line_sharp, C.d_line_lsharp, C.d_line_flat, C.d_line_cnt,
                                           C.d_line_lf, N_SCANS, C.d_meta, C.d_sharp, C.d_sharp_idx, C.d_lsharp,
                                           C.d_lsharp_idx, C.d_flat, C.d_flat_idx, C.d_lflat, C.d_odom_nq);
+        hipStream_t sv = st;
+        if (side) {
+            HIPCHK(hipEventRecord(C.ev_scan, st));
+            HIPCHK(hipStreamWaitEvent(C.stream2, C.ev_scan, 0));
+            sv = C.stream2;
+        }
+        static bool lv_attr = false;
+        if (!lv_attr) {
+            HIPCHK(hipFuncSetAttribute((const void*)k_line_vox, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv_lds_bytes()));
+            lv_attr = true;
+        }
+        k_line_vox<<<N_SCANS, LT, lv_lds_bytes(), sv>>>(C.d_cloud, C.d_meta, C.d_scratch_xyz, C.d_scratch_keys, C.d_scratch_i,
+                                                      C.d_line_cnt, C.d_line_lf);
+        k_concat_lf<<<N_SCANS, 256, 0, sv>>>(C.d_line_cnt, C.d_line_lf, N_SCANS, C.d_meta, C.d_lflat);
+        if (side) HIPCHK(hipEventRecord(C.ev_lf, sv));
     } else {
         prof_phase(C, Ctx::PM_SCAN_PREP);
         prof_phase(C, Ctx::PM_SCAN_CURV);

@@ -56,6 +56,8 @@ struct VoxJobs { VoxJob j[2]; };
 // sums the leaves.
 constexpr int VX_SEGW = 16;
 static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : 4096;   // tuning knob
+// tuning knob: clouds up to this size are sorted whole by their own workgroup, larger ones split
+static const int g_vox_fit = getenv("ALOAM_VOX_FIT") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_FIT")))) : VX_LDS_N;
 static_assert(ls_split_scratch_bytes(VX_T, VX_LDS_N) <= ls_global_scratch_bytes(VX_T, VX_LDS_N), "split scratch");
 
 // runs of equal leaves in sorted E -> centroids in leaf order; each run summed in sorted order by its head
@@ -80,7 +82,7 @@ __device__ void vox_reduce(const VoxJob& J, int n, const unsigned long long* E, 
     if (tid == 0) *J.d_nout = tot;
 }
 
-__global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit) {
+__global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int fit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const VoxJob& J = P.j[blockIdx.x];
     unsigned* bb = (unsigned*)smem;
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit) {
     const int tid = threadIdx.x;
     // a hinted launch never reads past its launch size (the exact-size redo replaces the result)
     const int n = min(*J.d_n, J.cap);
-    if (n <= VX_LDS_N || n > VX_NMAX) { if (tid == 0) J.gseg[0] = 0; }   // done here (the others: split)
+    if (n <= fit || n > VX_NMAX) { if (tid == 0) J.gseg[0] = 0; }   // done here (the others: split)
     if (n <= 0) { if (tid == 0) *J.d_nout = 0; return; }
     if (tid < 6) bb[tid] = tid < 3 ? 0xffffffffu : 0u;
     __syncthreads();
@@ -117,7 +119,7 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit) {
         return;
     }
     const float inv = 1.0f / J.leaf;
-    if (n <= VX_LDS_N) {
+    if (n <= fit) {
         for (int t = tid; t < n; t += VX_T) EL[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
         lds_barrier();
         ls_sort<VX_T, VX_CPW>(EL, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, VX_LDS_N);
@@ -203,8 +205,8 @@ void voxel_grid_pair_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* pt
     VoxJobs P;
     P.j[0] = vox_job(C, K, 0, ptsA, d_nA, std::max(capA, 0), leafA, outA, d_noutA);
     P.j[1] = vox_job(C, K, 1, ptsB, d_nB, std::max(capB, 0), leafB, outB, d_noutB);
-    k_vox_pcl<<<2, VX_T, VX_LDS, st>>>(P, g_vox_seg);
-    if (std::max(capA, capB) > VX_LDS_N) {
+    k_vox_pcl<<<2, VX_T, VX_LDS, st>>>(P, g_vox_seg, g_vox_fit);
+    if (std::max(capA, capB) > g_vox_fit) {
         k_vox_seg<<<dim3(VX_SEGW, 2), VX_T, VX_LDS, st>>>(P);
         k_vox_reduce<<<dim3(VX_REDW, 2), VX_T, 0, st>>>(P);
     }
@@ -218,8 +220,8 @@ void voxel_grid_sorted_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* 
     VoxJobs P;
     P.j[0] = vox_job(C, K, 0, pts, d_n, std::max(cap_n, 0), leaf, out, d_nout);
     P.j[1] = P.j[0];
-    k_vox_pcl<<<1, VX_T, VX_LDS, st>>>(P, g_vox_seg);
-    if (cap_n > VX_LDS_N) {
+    k_vox_pcl<<<1, VX_T, VX_LDS, st>>>(P, g_vox_seg, g_vox_fit);
+    if (cap_n > g_vox_fit) {
         k_vox_seg<<<dim3(VX_SEGW, 1), VX_T, VX_LDS, st>>>(P);
         k_vox_reduce<<<dim3(VX_REDW, 1), VX_T, 0, st>>>(P);
     }

@@ -627,21 +627,29 @@ template <int NT>
 __device__ __forceinline__ void ls_split_to_list(unsigned long long* gE, const int n, const int limit, int* gseg, unsigned char* scratch) {
     ls_split_to_list_lds<NT>(gE, n, limit, gseg, (lds_u8*)scratch);
 }
-// segments w, w + nw, ... of the list: each copied into EL (cap elements of LDS), sorted by ls_sort from
-// its remaining depth, copied back
+// Workgroup w of nw: the list's segments of > 64 elements w, w + nw, ... (in list order, counting only
+// those), each copied into EL (cap elements of LDS), sorted by ls_sort from its remaining depth, copied
+// back; the <= 64-element ones one per wave (all waves of all nw workgroups), in registers in place.
 template <int NT, int CPW>
 __device__ __forceinline__ void ls_sort_list(unsigned long long* gE, const int* gseg, int w, int nw, unsigned long long* EL,
                                              const int cap, unsigned char* scratch) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wid = tid / WAVE;
     const int ns = min(gseg[0], PS_GLIST);
-    for (int i = w; i < ns; i += nw) {
+    int big = 0, small = 0;
+    for (int i = 0; i < ns; i++) {
         const int f = gseg[1 + 3 * i], l = gseg[2 + 3 * i], d = gseg[3 + 3 * i] - 1;
         const int m = l - f;
-        for (int t = tid; t < m; t += NT) EL[t] = gE[f + t];
-        __syncthreads();
-        ls_sort<NT, CPW>(EL, m, d, scratch, cap);
-        for (int t = tid; t < m; t += NT) gE[f + t] = EL[t];
-        __syncthreads();
+        if (m > WAVE) {
+            if (big++ % nw != w) continue;
+            for (int t = tid; t < m; t += NT) EL[t] = gE[f + t];
+            __syncthreads();
+            ls_sort<NT, CPW>(EL, m, d, scratch, cap);
+            for (int t = tid; t < m; t += NT) gE[f + t] = EL[t];
+            __syncthreads();
+        } else if (m >= 2) {
+            if (small++ % (nw * (NT / WAVE)) != w * (NT / WAVE) + wid) continue;
+            ws_small(gE, f, m, d);
+        }
     }
 }
 

@@ -1,19 +1,18 @@
-// pcl_sort.hpp — PCL VoxelGrid's point order on gfx950: libstdc++ std::sort, replayed in parallel.
+// pcl_sort.hpp — PCL VoxelGrid's point order on gfx950: libstdc++ std::sort building blocks.
 //
 // pcl::VoxelGrid<PointXYZI>::applyFilter (PCL 1.8.0, voxel_grid.hpp) pushes one (leaf index, point
 // index) pair per point, std::sort's them by leaf index (an UNSTABLE introsort: the pairs of one leaf
 // end up in an order that depends on the whole array) and sums every leaf's points in that order. The
 // reference calls it at src/scanRegistration.cpp:401-405 (per scan line, leaf 0.2) and
 // src/laserMapping.cpp:542-550 (the stacks), :788-801 (every surrounding map cube). fp32 sums depend on
-// the order, so the device reproduces it exactly:
-//
-//   pcl_std_sort<NT, BIG>(E, n, scratch, nmax)             E in LDS
-//   pcl_std_sort_global<NT>(gE, n, EL, cap, scratch)       E in global memory, staged through LDS
-//
-// leave E[0, n) (u64 = key << 32 | payload, compared by key only) in exactly the order
-// std::sort(E, E + n, key-less) of libstdc++ produces. libstdc++'s sort is introsort_loop (median of
-// first+1 / mid / last-1 moved to first, unguarded Hoare partition, recurse right, loop left, 16-element
-// threshold, heap sort at depth 2 floor(log2 n)) followed by one insertion sort over the whole array.
+// the order, so the device reproduces it exactly (ls_sort.hpp). libstdc++'s sort is introsort_loop
+// (median of first+1 / mid / last-1 moved to first, unguarded Hoare partition, recurse right, loop left,
+// 16-element threshold, heap sort at depth 2 floor(log2 n)) followed by one insertion sort over the whole
+// array. This file holds the pieces shared by ls_sort.hpp: keys (u64 = key << 32 | payload, compared by
+// key only), the median move, heap sort, insertion sort, the one-thread whole sort (arrays beyond the
+// parallel paths), block scans, the leaf sums, and the workgroup split of an array in global memory
+// (ps_wg_split: segments above a limit partitioned level by level by the whole workgroup, each thread a
+// chunk of <= 64 positions; children at or below the limit pushed to a sink list).
 //
 // The partition of a segment [f, l) with pivot key K at f is computed, not simulated: with LS = the
 // positions p in (f, l) with key >= K in ascending order ("left stops") and RS = the positions in
@@ -22,22 +21,12 @@
 // iff more than j right stops lie after LS[j]) and return cut = min(LS[k], RS[k-1]) (LS[k] when k = 0,
 // RS[k-1] when LS runs out): every element a scan passes before a swap is untouched, and the first
 // swapped element a scan meets stops it. The final insertion sort is stable and the partition property
-// keeps every element inside its <= 16-element leaf, so each leaf is sorted (stable rank, lane-parallel)
-// as soon as it forms. Depth-exhausted segments are heap-sorted by one lane, exactly as
-// std::__partial_sort(first, last, last).
-//
-// Every step is element-parallel: a wave partitions a segment of <= PS_WMAX positions in 64-position
-// chunks (chunk u = positions f + 64u + lane): one pass of ballots gives the stop masks, a DPP scan the
-// per-chunk prefixes, and a second pass decides each left stop's swap from its own rank and its partner
-// from the chunk prefixes held in the lanes (readlane), so no lane walks a mask bit by bit. Waves take
-// segments from an LDS queue, push every right child for another wave and keep the left one
-// (introsort's own recursion shape). Larger segments are first split level by level by the whole
-// workgroup (per-thread chunks of <= 64 positions). Arrays in global memory are split by the workgroup
-// until every segment fits the LDS buffer, then each segment is sorted there.
+// keeps every element inside its <= 16-element leaf, so each leaf is sorted (stable rank) once it forms.
+// Depth-exhausted segments are heap-sorted by one lane, exactly as std::__partial_sort(first, last, last).
 //
 // The characterisation is checked against libstdc++ on the host (oracle/aloam_oracle.cpp
-// oracle_pcl_replay_check, tests/test_oracle_pins.py), this file's code on the host by a per-lane
-// thread emulation (tests/ps_emu.cpp, tests/test_pcl_sort_emu.py) and on the device by the VoxelGrid /
+// oracle_pcl_replay_check, tests/test_oracle_pins.py), the device code on the host by a per-lane thread
+// emulation (tests/ps_emu.cpp, tests/test_pcl_sort_emu.py) and on the device by the VoxelGrid /
 // scanRegistration / mapping parity tests against the oracle's PCL order.
 #pragma once
 #ifndef PS_HOST_EMU                          // tests/ps_emu.cpp compiles this file on the host
@@ -68,16 +57,14 @@
 namespace aloam {
 
 constexpr int PS_THRESHOLD = 16;    // libstdc++ _S_threshold
-constexpr int PS_WMAX = 4096;       // segments one wave partitions (64 chunks of 64 positions)
 constexpr int PS_MAX_CHUNK = 64;    // workgroup phase: positions per thread (u64 stop masks)
 constexpr int PS_WGSEG = 32;        // workgroup phase: segments split at once (n <= NT * 64)
 constexpr int PS_GLIST = 320;       // global sorts: segments staged through LDS (<= 2 per split x depth)
-constexpr int PS_LANE_MAX = 64;     // segments of <= this many elements: one lane each (ps_lane_sort)
 
 // Scratch (ints, LDS, 8-byte aligned): header | exscan words | workgroup phase arrays (BIG) | segment
 // queue (3 ints per queued segment) [| staged-segment list (global sorts)]
 __host__ __device__ constexpr int ps_wg_ints(int NT) { return 7 * (NT + 1) + 8 * PS_WGSEG; }
-__host__ __device__ constexpr int ps_qcap(int n) { return n / (PS_THRESHOLD + 1) + 64; }   // (overflow: ps_wave_phase)
+__host__ __device__ constexpr int ps_qcap(int n) { return n / (PS_THRESHOLD + 1) + 64; }
 __host__ __device__ constexpr int ps_scratch_ints(int NT, int nmax, bool big) {
     return 16 + 2 * (NT / 64) + (big ? ps_wg_ints(NT) : 0) + 3 * ps_qcap(nmax);
 }
@@ -96,17 +83,6 @@ __device__ __forceinline__ unsigned long long ps_rl64(unsigned long long v, int 
     return ((unsigned long long)(unsigned)readlane_i((int)(v >> 32), lane) << 32) | (unsigned)readlane_i((int)v, lane);
 }
 __device__ __forceinline__ int ps_msb(unsigned long long m) { return 63 - __builtin_clzll(m); }   // m != 0
-// Single-writer updates inside the wave phase are done by the WHOLE wave, branch-free: an `if (lane ==
-// 0)` block at a loop boundary was merged into the loop's exit mask by the compiler (lane 0 left the
-// loop, lanes 1-63 kept iterating). Atomics: every lane adds, only lane 0 a non-zero amount, lane 0's
-// old value broadcast; stores: every lane writes the same value.
-__device__ __forceinline__ int ps_wave_add(int* p, int v, int order = __ATOMIC_RELAXED) {
-    const int r = order == __ATOMIC_RELEASE
-                      ? __hip_atomic_fetch_add(p, lane_id() == 0 ? v : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP)
-                      : __hip_atomic_fetch_add(p, lane_id() == 0 ? v : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return ps_u(r);
-}
-
 template <bool G>
 __device__ __forceinline__ void ps_bar() {
     if (G) __syncthreads();
@@ -240,168 +216,10 @@ __device__ __forceinline__ unsigned ps_median_to_first(unsigned long long* E, in
     return ps_key(ep);
 }
 
-// One lane's whole std::sort of E[f0, l0) (l0 - f0 <= PS_LANE_MAX) from depth d: introsort_loop (right
-// parts > 16 on a 3-entry register stack: they are disjoint, so at most 3 wait at once), then the final
-// stable insertion sort over the segment (== sorting its <= 16-element leaves). No wave operations
-// inside: the lanes of a wave run it on 64 different segments at once.
-__device__ __forceinline__ void ps_lane_sort(unsigned long long* E, const int f0, const int l0, int d) {
-    int f = f0, l = l0, sp = 0;
-    int af = 0, al = 0, ad = 0, bf = 0, bl = 0, bd = 0, cf = 0, cl = 0, cd = 0;
-    for (;;) {
-        while (l - f > PS_THRESHOLD) {
-            if (d == 0) { ps_heap_sort(E + f, E + l); break; }
-            d--;
-            const unsigned kp = ps_median_to_first(E, f, l);
-            int lo = f + 1, hi = l;
-            while (true) {
-                while (ps_key(E[lo]) < kp) ++lo;
-                --hi;
-                while (kp < ps_key(E[hi])) --hi;
-                if (!(lo < hi)) break;
-                const unsigned long long t = E[lo]; E[lo] = E[hi]; E[hi] = t;
-                ++lo;
-            }
-            if (l - lo > PS_THRESHOLD) {
-                if (sp == 0) { af = lo; al = l; ad = d; }
-                else if (sp == 1) { bf = lo; bl = l; bd = d; }
-                else { cf = lo; cl = l; cd = d; }
-                sp++;
-            }
-            l = lo;
-        }
-        if (sp == 0) break;
-        sp--;
-        if (sp == 0) { f = af; l = al; d = ad; }
-        else if (sp == 1) { f = bf; l = bl; d = bd; }
-        else { f = cf; l = cl; d = cd; }
-    }
-    ps_insertion_sort(E, f0, l0);
-}
-
-// ---- one wave ---------------------------------------------------------------------------------
-// Leaf (m <= 16 elements): stable rank of every element by lane, then the scatter.
-template <bool G>
-__device__ __forceinline__ void ps_wave_leaf(unsigned long long* E, int f, int l) {
-    const int m = l - f;
-    if (m < 2) return;
-    const int lane = lane_id();
-    const bool act = lane < m;
-    const unsigned long long v = act ? E[f + lane] : ~0ull;
-    const unsigned kv = ps_key(v);
-    int rank = 0;
-#pragma unroll
-    for (int i = 0; i < PS_THRESHOLD; i++) {
-        const unsigned ki = (unsigned)__shfl((int)kv, i, WAVE);
-        rank += (i < m) && (ki < kv || (ki == kv && i < lane));
-    }
-    ps_wsync<G>();
-    if (act) E[f + rank] = v;
-    ps_wsync<G>();
-}
-
-// Partition of E[f, l) (17 <= l - f <= PS_WMAX) by one wave; returns the cut. Chunk u = positions
-// f + 64u + lane; lane u keeps chunk u's stop masks (myL, myR) and exclusive stop prefixes (pL, pR).
-template <bool G>
-__device__ int ps_wave_partition(unsigned long long* E, const int f, const int l) {
-    const int lane = lane_id();
-    int k0 = 0;
-    PS_SAME(k0 = (int)ps_median_to_first(E, f, l));
-    const unsigned K = (unsigned)ps_u(k0);
-    ps_wsync<G>();
-    const int nch = ps_u((l - f + 63) >> 6);
-    unsigned long long myL = 0, myR = 0;
-    for (int c0 = 0; c0 < nch; c0 += 4) {
-        unsigned kk[4];
-        bool in[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int p = f + ((c0 + u) << 6) + lane;
-            in[u] = c0 + u < nch && p < l;
-            kk[u] = in[u] ? ps_keyat(E, p) : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int p = f + ((c0 + u) << 6) + lane;
-            const unsigned long long bl = __ballot(in[u] && p > f && kk[u] >= K);
-            const unsigned long long br = __ballot(in[u] && kk[u] <= K);
-            myL = lane == c0 + u ? bl : myL;
-            myR = lane == c0 + u ? br : myR;
-        }
-    }
-    const int cl = __popcll(myL), cr = __popcll(myR);
-    const int iL = wave_incl_scan(cl), iR = wave_incl_scan(cr);
-    const int pL = iL - cl, pR = iR - cr;
-    const int nL = ps_u(readlane_i(iL, WAVE - 1)), nR = ps_u(readlane_i(iR, WAVE - 1));
-    const bool valid = lane < nch;
-    const unsigned long long lt = (1ull << lane) - 1ull, le = lt | (1ull << lane);
-    // the swaps: left stop of rank j swaps with RS[j] iff more than j right stops lie after it; the
-    // swapped ones are a prefix of the left stops, so the chunk loop ends at the first refusal
-    int k = 0;
-    for (int u = 0; u < nch; u++) {
-        const unsigned long long bL = ps_rl64(myL, u);
-        if (bL == 0ull) continue;
-        const unsigned long long bR = ps_rl64(myR, u);
-        const int pLu = ps_u(readlane_i(pL, u)), pRu = ps_u(readlane_i(pR, u));
-        const int j = pLu + __popcll(bL & lt);
-        const int after = nR - pRu - __popcll(bR & le);
-        const bool sw = ((bL >> lane) & 1ull) && j < after;
-        const unsigned long long bs = __ballot(sw);
-        const int nsw = __popcll(bs);
-        if (nsw > 0) {
-            // partners: RS[j] = the right stop of ascending rank a = nR - 1 - j; this chunk's swaps
-            // take ranks [aLo, aHi], found in chunks cLo..cHi (last chunk whose prefix is <= the rank)
-            const int aHi = nR - 1 - pLu, aLo = aHi - nsw + 1;
-            const int cHi = ps_msb(__ballot(valid && pR <= aHi)), cLo = ps_msb(__ballot(valid && pR <= aLo));
-            const int a = nR - 1 - j;
-            int q = -1;
-            for (int c = cHi; c >= cLo; c--) {
-                const int pRc = ps_u(readlane_i(pR, c));
-                const unsigned long long mRc = ps_rl64(myR, c);
-                if (sw && q < 0 && a >= pRc) q = f + (c << 6) + ps_select_bit(mRc, a - pRc);
-            }
-            if (sw) {
-                const int p = f + (u << 6) + lane;
-                PS_CHECK(p > f && p < l && q >= f && q < l && p < q, "ps swap: f %d l %d p %d q %d j %d nL %d nR %d\n", f, l, p, q, j, nL, nR);
-                const unsigned long long ep = E[p], eq = E[q];
-                E[p] = eq;
-                E[q] = ep;
-            }
-        }
-        k += nsw;
-        if (nsw < __popcll(bL)) break;
-    }
-    k = ps_u(k);
-    ps_wsync<G>();
-    // the cut: LS[k] (k < nL) and RS[k-1] (k >= 1)
-    int cut = 0x7fffffff;
-    if (k < nL) {
-        const int c = ps_msb(__ballot(valid && pL <= k));
-        cut = f + (c << 6) + ps_select_bit(ps_rl64(myL, c), k - ps_u(readlane_i(pL, c)));
-    }
-    if (k >= 1) {
-        const int a = nR - k;
-        const int c = ps_msb(__ballot(valid && pR <= a));
-        cut = min(cut, f + (c << 6) + ps_select_bit(ps_rl64(myR, c), a - ps_u(readlane_i(pR, c))));
-    }
-    cut = ps_u(cut);
-    PS_CHECK(cut > f && cut < l, "ps cut: f %d l %d cut %d k %d nL %d nR %d\n", f, l, cut, k, nL, nR);
-    return cut;
-}
-
 // Work queue of segments (f, l, depth + 1 as the ready mark). hdr: [1] head, [2] tail, [3] pending
 // (queued or in progress). ps_push: ONE lane (the workgroup phase's thread 0); ps_push_wave: a whole
 // wave, uniform arguments. False when the queue is full (the slot claimed past qcap is never filled: a
 // wave waiting on it leaves when pending reaches zero).
-__device__ __forceinline__ bool ps_push_wave(int* hdr, int* Q, int qcap, int f, int l, int d) {
-    const int s = ps_wave_add(&hdr[2], 1);
-    if (s >= qcap) return false;
-    PS_CHECK(f >= 0 && l > f + PS_LANE_MAX, "ps push: f %d l %d d %d s %d qcap %d\n", f, l, d, s, qcap);
-    ps_wave_add(&hdr[3], 1);
-    Q[3 * s] = f;
-    Q[3 * s + 1] = l;
-    __hip_atomic_store(&Q[3 * s + 2], d + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return true;
-}
 __device__ __forceinline__ bool ps_push(int* tail, int* pend, int* Q, int qcap, int f, int l, int d) {
     const int s = __hip_atomic_fetch_add(tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (s >= qcap) return false;
@@ -411,85 +229,6 @@ __device__ __forceinline__ bool ps_push(int* tail, int* pend, int* Q, int qcap, 
     Q[3 * s + 1] = l;
     __hip_atomic_store(&Q[3 * s + 2], d + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return true;
-}
-
-// every wave: take segments until no segment is queued or in progress. Every branch below is on a
-// wave-uniform scalar (ps_u), so the wave runs it with its full exec mask. Segments of <= PS_LANE_MAX
-// elements are collected, one per lane (lane i holds entry i), and sorted 64 at a time by ps_lane_sort.
-template <bool G>
-__device__ void ps_wave_phase(unsigned long long* E, int* hdr, int* Q, int qcap) {
-    const int lane = lane_id();
-    int lf = 0, ll = 0, ld = 0, ln = 0;                            // the collected small segments
-    auto flush = [&]() {
-        ps_wsync<G>();
-        const unsigned long long tl = PS_CLK();
-        if (lane < ln) ps_lane_sort(E, lf, ll, ld);
-        ps_wsync<G>();
-        PS_WSTAT(4, PS_CLK() - tl);
-        PS_WSTAT(5, 1);
-        ln = 0;
-    };
-    auto collect = [&](int f, int l, int d) {                      // uniform arguments
-        if (ln == WAVE) flush();
-        lf = lane == ln ? f : lf;
-        ll = lane == ln ? l : ll;
-        ld = lane == ln ? d : ld;
-        ln = ps_u(ln + 1);
-    };
-    for (;;) {
-        const int s = ps_wave_add(&hdr[1], 1);
-        int mark = 0, quit = 0;
-        const unsigned long long tw = PS_CLK();
-        for (;;) {
-            const int rdy = ps_u(s < qcap ? __hip_atomic_load(&Q[3 * min(s, qcap - 1) + 2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 0);
-            const int pend = ps_u(__hip_atomic_load(&hdr[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (rdy != 0) { mark = rdy; break; }
-            if (pend == 0) { quit = 1; break; }                    // nothing queued, nothing running
-            __builtin_amdgcn_s_sleep(1);
-        }
-        PS_WSTAT(0, PS_CLK() - tw);
-        if (ps_u(quit)) break;
-        int f = ps_u(Q[3 * s]), l = ps_u(Q[3 * s + 1]);
-        int d = ps_u(mark - 1);
-        // right children the full queue refused stay with this wave: a stack held one entry per lane
-        // (at most one per recursion level, <= 2 log2 n <= 32)
-        int sp = 0, stf = 0, stl = 0, std_ = 0;
-        for (;;) {
-            for (;;) {                                             // introsort_loop on [f, l)
-                if (l - f <= PS_LANE_MAX) {
-                    if (l - f >= 2) collect(f, l, d);
-                    break;
-                }
-                if (d == 0) {
-                    PS_SAME(ps_heap_sort(E + f, E + l));           // (rare)
-                    ps_wsync<G>();
-                    break;
-                }
-                d = ps_u(d - 1);
-                const unsigned long long tp = PS_CLK();
-                const int cut = ps_wave_partition<G>(E, f, l);
-                PS_WSTAT(1, PS_CLK() - tp);
-                PS_WSTAT(2, 1);
-                PS_WSTAT(3, l - f);
-                if (l - cut > PS_LANE_MAX) {
-                    if (!ps_push_wave(hdr, Q, qcap, cut, l, d)) {
-                        stf = lane == sp ? cut : stf;
-                        stl = lane == sp ? l : stl;
-                        std_ = lane == sp ? d : std_;
-                        sp = ps_u(sp + 1);
-                    }
-                } else if (l - cut >= 2) {
-                    collect(cut, l, d);
-                }
-                l = ps_u(cut);
-            }
-            if (sp == 0) break;
-            sp = ps_u(sp - 1);
-            f = ps_u(readlane_i(stf, sp)); l = ps_u(readlane_i(stl, sp)); d = ps_u(readlane_i(std_, sp));
-        }
-        ps_wave_add(&hdr[3], -1, __ATOMIC_RELEASE);
-    }
-    if (ln > 0) flush();
 }
 
 // ---- the workgroup phase (segments > limit) ----------------------------------------------------
@@ -712,77 +451,6 @@ __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const i
         }
         ps_bar<G>();
         PS_TS(lvl, 4);
-    }
-}
-
-// The sort of E[0, n) in LDS from depth d0 (the caller's segment of a larger sort: its remaining
-// introsort depth). sc: ps_scratch_ints(NT, nmax, BIG) ints of LDS (8-byte aligned), nmax >= n. BIG =
-// false: the caller guarantees n <= PS_WMAX. n <= NT * PS_MAX_CHUNK. All NT threads call it with the
-// same arguments. Ends with a barrier.
-template <int NT, bool BIG>
-__device__ void ps_sort_lds(unsigned long long* E, const int n, const int d0, int* sc, const int nmax) {
-    const int tid = threadIdx.x;
-    int* hdr = sc;
-    int* Q = sc + 16 + 2 * (NT / WAVE) + (BIG ? ps_wg_ints(NT) : 0);
-    const int qcap = ps_qcap(nmax);
-    for (int i = tid; i < 3 * qcap; i += NT) Q[i] = 0;
-    if (tid < 16) hdr[tid] = 0;
-    lds_barrier();
-    if (!BIG || n <= PS_WMAX) {
-        if (tid == 0) {
-            if (n <= PS_THRESHOLD) ps_insertion_sort(E, 0, n);
-            else if (d0 == 0) ps_heap_sort(E, E + n);
-            else ps_push(&hdr[2], &hdr[3], Q, qcap, 0, n, d0);
-        }
-    } else {
-        int* Bf = sc + 16 + 2 * (NT / WAVE) + 7 * (NT + 1);
-        if (tid == 0) { Bf[0] = 0; Bf[PS_WGSEG] = n; Bf[2 * PS_WGSEG] = d0; hdr[0] = 1; }
-        lds_barrier();
-        ps_wg_split<NT, false>(E, n, sc, PS_WMAX, &hdr[2], &hdr[3], Q, qcap);
-    }
-    lds_barrier();
-    PS_TS(60, 0);
-    ps_wave_phase<false>(E, hdr, Q, qcap);
-    lds_barrier();
-    PS_TS(60, 1);
-}
-
-template <int NT, bool BIG>
-__device__ void pcl_std_sort(unsigned long long* E, const int n, int* sc, const int nmax) {
-    if (n <= 1) return;
-    ps_sort_lds<NT, BIG>(E, n, 2 * (31 - __builtin_clz((unsigned)n)), sc, nmax);
-}
-
-// The sort of gE[0, n) in global memory (n <= NT * PS_MAX_CHUNK): the workgroup splits it until every
-// segment fits EL (cap elements of LDS), then each segment is copied into EL, sorted there from its
-// remaining depth and copied back. sc: ps_scratch_ints_global(NT, cap) ints of LDS. Ends with a barrier.
-template <int NT>
-__device__ void pcl_std_sort_global(unsigned long long* gE, const int n, unsigned long long* EL, const int cap, int* sc) {
-    const int tid = threadIdx.x;
-    if (n <= 1) return;
-    int* hdr = sc;
-    int* GL = sc + ps_scratch_ints(NT, cap, true);
-    if (tid < 16) hdr[tid] = 0;
-    for (int i = tid; i < 3 * PS_GLIST; i += NT) GL[i] = 0;
-    int* Bf = sc + 16 + 2 * (NT / WAVE) + 7 * (NT + 1);
-    const int D0 = 2 * (31 - __builtin_clz((unsigned)n));
-    __syncthreads();
-    if (tid == 0) {
-        if (n > cap) { Bf[0] = 0; Bf[PS_WGSEG] = n; Bf[2 * PS_WGSEG] = D0; hdr[0] = 1; }
-        else { GL[0] = 0; GL[1] = n; GL[2] = D0 + 1; hdr[4] = 1; }     // fits: one staged segment
-    }
-    __syncthreads();
-    if (n > cap) ps_wg_split<NT, true>(gE, n, sc, cap, &hdr[4], &hdr[5], GL, PS_GLIST);
-    __syncthreads();
-    const int ns = min(ps_u(hdr[4]), PS_GLIST);
-    for (int i = 0; i < ns; i++) {
-        const int f = GL[3 * i], l = GL[3 * i + 1], d = GL[3 * i + 2] - 1;
-        const int m = l - f;
-        for (int t = tid; t < m; t += NT) EL[t] = gE[f + t];
-        __syncthreads();
-        ps_sort_lds<NT, true>(EL, m, d, sc, cap);
-        for (int t = tid; t < m; t += NT) gE[f + t] = EL[t];
-        __syncthreads();
     }
 }
 

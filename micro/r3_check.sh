@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-3 check on the box: GPU suite, bench line, kernel-trace profile (each step time-limited, stop at the first failure)
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r3_gpu_tests.log 2>&1; rc=$?
+tail -2 gpurun_out/r3_gpu_tests.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py > gpurun_out/r3_bench.log 2>&1 || exit 1
+grep -o '"value": [0-9.]*' gpurun_out/r3_bench.log | head -1
+bash profiles/prof.sh prof_r3 --steps 30 --no-traffic
+for cfg in "ALOAM_CUBE_FIT=4096" "ALOAM_CUBE_FIT=4096 ALOAM_VOX_FIT=4096" "ALOAM_CUBE_FIT=4096 ALOAM_VOX_FIT=2048 ALOAM_VOX_SEG=2048"; do
+  env $cfg timeout -k 10 150 python bench.py --no-cpu --c4-launches 0 --c4-reg-steps 0 > gpurun_out/sw.log 2>&1 || exit 1
+  echo "$cfg $(grep -o '"value": [0-9.]*' gpurun_out/sw.log | head -1)"
+done

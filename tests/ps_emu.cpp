@@ -1,4 +1,4 @@
-// tests/ps_emu.cpp — host emulation of one HIP workgroup running csrc/pcl_sort.hpp.
+// tests/ps_emu.cpp — host emulation of HIP workgroups running csrc/ls_sort.hpp (+ pcl_sort.hpp's pieces).
 //
 // Every lane is a std::thread; the wave collectives the sort uses (ballot, shfl, readlane /
 // readfirstlane, DPP scans, all-reduces, the wave barrier) are a wave-wide std::barrier around a shared
@@ -139,6 +139,33 @@ static void run_ls(std::vector<unsigned long long>& E) {
         });
     for (auto& x : th) x.join();
 }
+// csrc/ls_sort.hpp's split-to-list + ls_sort_list: one emulated workgroup splits, then nw = 2 workgroups
+// (run one after the other) sort their share of the segments
+template <int NT, int CPW>
+static void run_ls_list(std::vector<unsigned long long>& E, int limit) {
+    const int n = (int)E.size(), cap = NT * CPW;
+    std::vector<unsigned long long> scr((aloam::ls_global_scratch_bytes(NT, cap) + 7) / 8), EL(cap);
+    std::vector<int> gseg(aloam::LS_SEGL);
+    for (int phase = 0; phase < 3; phase++) {
+        g_waves.clear();
+        for (int w = 0; w < NT / WAVE; w++) {
+            auto c = std::make_unique<WaveCtx>();
+            c->bar = std::make_unique<std::barrier<>>(WAVE);
+            g_waves.push_back(std::move(c));
+        }
+        g_block = std::make_unique<std::barrier<>>(NT);
+        std::vector<std::thread> th;
+        for (int t = 0; t < NT; t++)
+            th.emplace_back([&, t] {
+                threadIdx.x = t;
+                t_lane = t % WAVE;
+                t_wave = t / WAVE;
+                if (phase == 0) aloam::ls_split_to_list<NT>(E.data(), n, limit, gseg.data(), (unsigned char*)scr.data());
+                else aloam::ls_sort_list<NT, CPW>(E.data(), gseg.data(), phase - 1, 2, EL.data(), cap, (unsigned char*)scr.data());
+            });
+        for (auto& x : th) x.join();
+    }
+}
 // csrc/ls_sort.hpp's global sort: split in "global" memory by the workgroup phase of pcl_sort.hpp, segments
 // staged through an LDS buffer of `cap` elements and sorted there by ls_sort
 template <int NT, int CPW>
@@ -163,40 +190,13 @@ static void run_ls_global(std::vector<unsigned long long>& E, int cap) {
     for (auto& x : th) x.join();
 }
 
-// mode 0: LDS sort (BIG = n may exceed one wave segment); mode 1: global sort staged through an LDS
-// buffer of `cap` elements
-template <int NT, bool BIG>
-static bool run_case(std::vector<unsigned long long>& E, int nmax, int mode, int cap) {
-    std::vector<int> sc(mode ? aloam::ps_scratch_ints_global(NT, cap) : aloam::ps_scratch_ints(NT, nmax, BIG));
-    std::vector<unsigned long long> EL(mode ? cap : 0);
-    g_waves.clear();
-    for (int w = 0; w < NT / WAVE; w++) {
-        auto c = std::make_unique<WaveCtx>();
-        c->bar = std::make_unique<std::barrier<>>(WAVE);
-        g_waves.push_back(std::move(c));
-    }
-    g_block = std::make_unique<std::barrier<>>(NT);
-    const int n = (int)E.size();
-    std::vector<std::thread> th;
-    for (int t = 0; t < NT; t++)
-        th.emplace_back([&, t] {
-            threadIdx.x = t;
-            t_lane = t % WAVE;
-            t_wave = t / WAVE;
-            if (mode) aloam::pcl_std_sort_global<NT>(E.data(), n, EL.data(), cap, sc.data());
-            else aloam::pcl_std_sort<NT, BIG>(E.data(), n, sc.data(), nmax);
-        });
-    for (auto& x : th) x.join();
-    return true;
-}
-
 #ifndef NTHREADS
 #define NTHREADS 128
 #endif
 int main(int argc, char** argv) {
     const int trials = argc > 1 ? atoi(argv[1]) : 40;
     std::mt19937_64 rng(argc > 2 ? strtoull(argv[2], nullptr, 10) : 5);
-    const int lsm = argc > 3 ? atoi(argv[3]) : 0;        // 1: csrc/ls_sort.hpp (n <= 128 * 16); 2: its global sort
+    const int lsm = argc > 3 ? atoi(argv[3]) : 1;        // 1: csrc/ls_sort.hpp (n <= 128 * 16); 2: its global sort; 3: split + list sort
     const bool ls = lsm == 1;
     int bad = 0;
     for (int t = 0; t < trials; t++) {
@@ -218,23 +218,14 @@ int main(int argc, char** argv) {
         }
         std::vector<unsigned long long> A = E;
         std::sort(A.begin(), A.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
-        // every third big case: the global sort, staged through a buffer of a fraction of n
-        const int mode = big && t % 3 == 0;
-        const int cap = mode ? 600 + (int)(rng() % 2000) : 0;
         if (lsm == 2) run_ls_global<128, 16>(E, 300 + (int)(rng() % 1748));
-        else if (ls) run_ls<128, 16>(E);
-        else if (NTHREADS == 1024) {                  // the device's workgroup size (16 waves)
-            if (big) run_case<1024, true>(E, n, mode, cap);
-            else run_case<1024, false>(E, n, 0, 0);
-        } else {
-            if (big) run_case<128, true>(E, n, mode, cap);  // 2 waves: the work queue; n > 4096: the workgroup phase
-            else run_case<128, false>(E, n, 0, 0);
-        }
+        else if (lsm == 3) run_ls_list<128, 16>(E, 100 + (int)(rng() % 1948));
+        else run_ls<128, 16>(E);
         if (A != E) {
             bad++;
             int first = 0;
             while (first < n && A[first] == E[first]) first++;
-            std::printf("mismatch trial %d n %d kinds %u big %d mode %d cap %d first diff at %d\n", t, n, kinds, (int)big, mode, cap, first);
+            std::printf("mismatch trial %d n %d kinds %u mode %d first diff at %d\n", t, n, kinds, lsm, first);
         }
     }
     std::printf("trials %d mismatches %d\n", trials, bad);
