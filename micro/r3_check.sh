@@ -4,10 +4,7 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r3_gpu_tests.log 2>&1; rc=$?
 tail -2 gpurun_out/r3_gpu_tests.log
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python bench.py > gpurun_out/r3_bench.log 2>&1 || exit 1
+timeout -k 10 400 python bench.py > gpurun_out/r3_bench.log 2>&1 || exit 1
 grep -o '"value": [0-9.]*' gpurun_out/r3_bench.log | head -1
-bash profiles/prof.sh prof_r3 --steps 30 --no-traffic
-for cfg in "ALOAM_CUBE_FIT=4096" "ALOAM_CUBE_FIT=4096 ALOAM_VOX_FIT=4096" "ALOAM_CUBE_FIT=4096 ALOAM_VOX_FIT=2048 ALOAM_VOX_SEG=2048"; do
-  env $cfg timeout -k 10 150 python bench.py --no-cpu --c4-launches 0 --c4-reg-steps 0 > gpurun_out/sw.log 2>&1 || exit 1
-  echo "$cfg $(grep -o '"value": [0-9.]*' gpurun_out/sw.log | head -1)"
-done
+bash profiles/prof.sh prof_r3 --steps 30 --no-traffic || exit 1
+python profiles/stats.py gpurun_out/prof_r3 > gpurun_out/prof_r3_stats.txt 2>&1 || true
