@@ -460,8 +460,11 @@ __global__ void __launch_bounds__(256) k_s2m_fit(const float4* __restrict__ csta
 void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
                       const Grid* gcf, const Grid* gsf, aloam_factor* out) {
     if (s1 <= s0) return;
-    const char* bm = getenv("ALOAM_S2M_BATCH_MIN");                 // regime threshold (tests force either path)
-    const int batch_min = bm ? atoi(bm) : 65536;
+    // regime threshold (tests force either path). Default 1: the split 5-NN / fit kernels at any slot count —
+    // a rank's share at world 4 / 8 (65k / 33k slots) runs 4.65 / 13.55 ms per group registration on one GPU
+    // with them against 5.56 / 16.74 ms with the fused latency kernel (micro/s2m_share.py)
+    const char* bm = getenv("ALOAM_S2M_BATCH_MIN");
+    const int batch_min = bm ? atoi(bm) : 1;
     const bool fine = gcf && gsf;
     const KindGrids cc{gc.desc, gc.cell_start, gc.pts, gc.idx}, cs{gs.desc, gs.cell_start, gs.pts, gs.idx};
     const KindGrids fc = fine ? KindGrids{gcf->desc, gcf->cell_start, gcf->pts, gcf->idx} : cc;
@@ -941,6 +944,23 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubeseg(RbKinds P, const MapState*
     unsigned long long* EL = (unsigned long long*)(smem + RBV_HDR);
     ls_sort_list<RBV_T, RBV_CPW>(K.gscr + 4 * (size_t)p0, segl, w, RBV_SEGW, EL, RBV_CAP, (unsigned char*)(EL + RBV_CAP));
 }
+// The same for segments of <= RBQ_CAP elements (seg_limit <= RBQ_CAP): 256 threads and ~28 KB of LDS, so
+// several workgroups share a CU. One segment's sort is bound by its levels' barriers and dependent LDS
+// round trips, not by the CU's lanes, so occupancy is what raises the throughput over many segments.
+constexpr int RBQ_T = 256, RBQ_CPW = 8, RBQ_CAP = RBQ_T * RBQ_CPW;
+constexpr size_t RBQ_LDS = 8 * (size_t)RBQ_CAP + ls_scratch_bytes(RBQ_T, RBQ_CAP);
+constexpr int RBQ_SEGW = 32;
+__global__ void __launch_bounds__(RBQ_T) k_rb_cubeseg_s(RbKinds P, const MapState* __restrict__ m) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RbKind& K = P.k[blockIdx.y];
+    const int r = blockIdx.x / RBQ_SEGW, w = blockIdx.x % RBQ_SEGW;
+    if (r >= m->valid_num) return;
+    const int* segl = K.segl + (size_t)r * LS_SEGL;
+    if (segl[0] == 0) return;
+    const int p0 = K.a.off[m->valid_ind[r]];
+    unsigned long long* EL = (unsigned long long*)smem;
+    ls_sort_list<RBQ_T, RBQ_CPW>(K.gscr + 4 * (size_t)p0, segl, w, RBQ_SEGW, EL, RBQ_CAP, (unsigned char*)(EL + RBQ_CAP));
+}
 __global__ void __launch_bounds__(RBV_T) k_rb_cubered(RbKinds P, const MapState* __restrict__ m) {
     __shared__ int sc[16 + 2 * (RBV_T / WAVE) + 2];
     const RbKind& K = P.k[blockIdx.y];
@@ -1024,7 +1044,8 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
     static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_FIT")))) : 4096;
     k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit);
-    k_rb_cubeseg<<<dim3(125 * RBV_SEGW, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
+    if (seg_limit <= RBQ_CAP) k_rb_cubeseg_s<<<dim3(125 * RBQ_SEGW, 2), RBQ_T, RBQ_LDS, st>>>(P, C.d_map);
+    else k_rb_cubeseg<<<dim3(125 * RBV_SEGW, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
     k_rb_cubered<<<dim3(125, 2), RBV_T, 0, st>>>(P, C.d_map);
     k_rb_final_scan<<<2, 1024, 0, st>>>(P, C.d_cube_valid);
     k_rb_final<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P, C.d_cube_valid);
@@ -1038,6 +1059,7 @@ void rebuild_init(Ctx& C) {
     if (!attr) {
         HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubevox, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBV_LDS));
         HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubeseg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBV_LDS));
+        HIPCHK(hipFuncSetAttribute((const void*)k_rb_cubeseg_s, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBQ_LDS));
         HIPCHK(hipFuncSetAttribute((const void*)k_rb_sort_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RBS_LDS));
         attr = true;
     }

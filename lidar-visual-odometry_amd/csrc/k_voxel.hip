@@ -145,6 +145,21 @@ __global__ void __launch_bounds__(VX_T) k_vox_seg(VoxJobs P) {
     unsigned long long* EL = (unsigned long long*)(smem + VX_HDR);
     ls_sort_list<VX_T, VX_CPW>(J.gE, J.gseg, blockIdx.x, gridDim.x, EL, VX_LDS_N, (unsigned char*)(EL + VX_LDS_N));
 }
+// segments of <= VQ_CAP elements (g_vox_seg <= VQ_CAP): 256 threads, ~28 KB of LDS, several workgroups per CU
+// (k_map.hip's k_rb_cubeseg_s, same reasoning)
+constexpr int VQ_T = 256, VQ_CPW = 8, VQ_CAP = VQ_T * VQ_CPW, VQ_SEGW = 32;
+constexpr size_t VQ_LDS = 8 * (size_t)VQ_CAP + ls_scratch_bytes(VQ_T, VQ_CAP);
+__global__ void __launch_bounds__(VQ_T) k_vox_seg_s(VoxJobs P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const VoxJob& J = P.j[blockIdx.y];
+    if (J.gseg[0] == 0) return;
+    unsigned long long* EL = (unsigned long long*)smem;
+    ls_sort_list<VQ_T, VQ_CPW>(J.gE, J.gseg, blockIdx.x, gridDim.x, EL, VQ_CAP, (unsigned char*)(EL + VQ_CAP));
+}
+static void vox_seg_launch(const VoxJobs& P, int nk, hipStream_t st) {
+    if (g_vox_seg <= VQ_CAP) k_vox_seg_s<<<dim3(VQ_SEGW, nk), VQ_T, VQ_LDS, st>>>(P);
+    else k_vox_seg<<<dim3(VX_SEGW, nk), VX_T, VX_LDS, st>>>(P);
+}
 
 // the leaves of a split cloud, VX_REDW workgroups per cloud: workgroup w owns sorted positions [w R, (w+1) R)
 // and counts the run heads before them itself (a pass over the keys) for its output offset
@@ -183,6 +198,7 @@ static void vox_attr() {
     if (!done) {
         HIPCHK(hipFuncSetAttribute((const void*)k_vox_pcl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)VX_LDS));
         HIPCHK(hipFuncSetAttribute((const void*)k_vox_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)VX_LDS));
+        HIPCHK(hipFuncSetAttribute((const void*)k_vox_seg_s, hipFuncAttributeMaxDynamicSharedMemorySize, (int)VQ_LDS));
         done = true;
     }
 }
@@ -207,7 +223,7 @@ void voxel_grid_pair_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* pt
     P.j[1] = vox_job(C, K, 1, ptsB, d_nB, std::max(capB, 0), leafB, outB, d_noutB);
     k_vox_pcl<<<2, VX_T, VX_LDS, st>>>(P, g_vox_seg, g_vox_fit);
     if (std::max(capA, capB) > g_vox_fit) {
-        k_vox_seg<<<dim3(VX_SEGW, 2), VX_T, VX_LDS, st>>>(P);
+        vox_seg_launch(P, 2, st);
         k_vox_reduce<<<dim3(VX_REDW, 2), VX_T, 0, st>>>(P);
     }
     HIPCHK(hipGetLastError());
@@ -222,7 +238,7 @@ void voxel_grid_sorted_on(Ctx& C, hipStream_t st, KindScratch& K, const float4* 
     P.j[1] = P.j[0];
     k_vox_pcl<<<1, VX_T, VX_LDS, st>>>(P, g_vox_seg, g_vox_fit);
     if (cap_n > g_vox_fit) {
-        k_vox_seg<<<dim3(VX_SEGW, 1), VX_T, VX_LDS, st>>>(P);
+        vox_seg_launch(P, 1, st);
         k_vox_reduce<<<dim3(VX_REDW, 1), VX_T, 0, st>>>(P);
     }
     HIPCHK(hipGetLastError());

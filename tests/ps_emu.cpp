@@ -198,6 +198,9 @@ int main(int argc, char** argv) {
     std::mt19937_64 rng(argc > 2 ? strtoull(argv[2], nullptr, 10) : 5);
     const int lsm = argc > 3 ? atoi(argv[3]) : 1;        // 1: csrc/ls_sort.hpp (n <= 128 * 16); 2: its global sort; 3: split + list sort
     const bool ls = lsm == 1;
+    // 1: every trial a sorted prefix of distinct keys + a short unsorted tail of keys next to them (a map
+    // cube's old points + the appended ones): introsort exhausts its depth on much of it (heap sorts)
+    const bool cube_pattern = argc > 4 && atoi(argv[4]) == 1;
     int bad = 0;
     for (int t = 0; t < trials; t++) {
         const bool big = t % 2 == 1;
@@ -215,6 +218,16 @@ int main(int argc, char** argv) {
                 default: k = i < n / 2 ? (unsigned)(i / 8) : (unsigned)(rng() % kinds);
             }
             E[i] = ((unsigned long long)k << 32) | (unsigned)i;
+        }
+        if (cube_pattern) {
+            const int tail = std::min(n - 1, 1 + (int)(rng() % (unsigned)(n / 20 + 1)));
+            const int m = n - tail;
+            unsigned k = 0;
+            for (int i = 0; i < m; i++) { k += 1 + (unsigned)(rng() % 3); E[i] = ((unsigned long long)k << 32) | (unsigned)i; }
+            for (int i = m; i < n; i++) {
+                const unsigned kk = (unsigned)(E[rng() % (unsigned)m] >> 32) + (unsigned)(rng() % 3) - 1u;
+                E[i] = ((unsigned long long)kk << 32) | (unsigned)i;
+            }
         }
         std::vector<unsigned long long> A = E;
         std::sort(A.begin(), A.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
