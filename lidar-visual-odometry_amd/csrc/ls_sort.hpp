@@ -40,9 +40,6 @@ constexpr int LS_INACT = 0xffff;
 #define LS_TAIL_DEF 256                   // (tests vary it)
 #endif
 constexpr int LS_TAIL = LS_TAIL_DEF;     // the waves take over when every active segment has <= this many elements
-#ifndef LS_WQ
-#define LS_WQ 0                           // 1: ... whatever their number (round-robin over the waves)
-#endif
 
 // LDS scratch (bytes, 8-byte aligned sections) for n <= nmax elements sorted by NT threads
 __host__ __device__ constexpr int ls_nc(int nmax) { return (nmax + 63) / 64; }
@@ -277,7 +274,8 @@ __device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, 
                 break;
             }
             if (d == 0) {
-                ws_heap_sort<false>(E + f, l - f);
+                PS_SAME(ps_heap_sort(E + f, E + l));
+                ps_wsync<false>();
                 break;
             }
             d = ps_u(d - 1);
@@ -324,7 +322,7 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             S.seg(0, 2)[0] = d0 | (o << 8);
         }
     } else if (n > PS_THRESHOLD) {
-        if (wid == 0) ws_heap_sort<false>(E, n);
+        if (tid == 0) ps_heap_sort(E, E + n);
     }
     lds_barrier();
     int b = 0;
@@ -444,16 +442,8 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
                 f = F[tid]; l = L[tid]; d = (D[tid] & 0xff) - 1; cut = S.cut[tid];
                 PS_CHECK(cut > f && cut < l, "ls cut: f %d l %d cut %d\n", f, l, cut);
                 atomicOr(&S.bits[cut >> 6], 1ull << (cut & 63));
-                // depth-exhausted children: heap-sort jobs (f, l as u16 pairs in RS_pos, free until the next
-                // level's stage C), one wave each after the barrier
-                if (cut - f > PS_THRESHOLD) {
-                    if (d > 0) aL = 1;
-                    else { const int j = atomicAdd(&S.hdr[4], 1); S.rs[2 * j] = (unsigned short)f; S.rs[2 * j + 1] = (unsigned short)cut; }
-                }
-                if (l - cut > PS_THRESHOLD) {
-                    if (d > 0) aR = 1;
-                    else { const int j = atomicAdd(&S.hdr[4], 1); S.rs[2 * j] = (unsigned short)cut; S.rs[2 * j + 1] = (unsigned short)l; }
-                }
+                if (cut - f > PS_THRESHOLD) { if (d > 0) aL = 1; else ps_heap_sort(E + f, E + cut); }
+                if (l - cut > PS_THRESHOLD) { if (d > 0) aR = 1; else ps_heap_sort(E + cut, E + l); }
             }
             const int mine = aL + aR;
             const int incl = wave_incl_scan(mine);
@@ -485,11 +475,6 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         }
         lds_barrier();
         ns = S.hdr[8 + (b ^ 1)];
-        if (const int nh = S.hdr[4]) {
-            for (int j = wid; j < nh; j += W) ws_heap_sort<false>(E + S.rs[2 * j], (int)S.rs[2 * j + 1] - (int)S.rs[2 * j]);
-            lds_barrier();
-            if (tid == 0) S.hdr[4] = 0;
-        }
         // this level's counter and active chunks reset for the level after next
         if (tid == 0) { S.hdr[8 + b] = 0; S.hdr[12 + b] = 0; }
         if (tid < 32) S.act[(b ? 32 : 0) + tid] = 0ull;
@@ -497,11 +482,9 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         b ^= 1;
         // the sparse tail: once at most one active segment per wave is left and each is short, the waves
         // finish them independently (no workgroup barriers per level)
-        // (LS_WQ: also with more short segments than waves — wave w takes segments w, w + W, ...; segments
-        // are disjoint ranges of E and of RS, so the order they are finished in changes nothing)
-        if (ns > 0 && (LS_WQ || ns <= W) && S.hdr[12 + b] <= LS_TAIL) {
-            for (int s = wid; s < ns; s += W) {
-                const int sf = ps_u(S.seg(b, 0)[s]), sl = ps_u(S.seg(b, 1)[s]), sd = ps_u(S.seg(b, 2)[s]);
+        if (ns > 0 && ns <= W && S.hdr[12 + b] <= LS_TAIL) {
+            if (wid < ns) {
+                const int sf = ps_u(S.seg(b, 0)[wid]), sl = ps_u(S.seg(b, 1)[wid]), sd = ps_u(S.seg(b, 2)[wid]);
                 PS_SAME({ const unsigned long long t_ = E[sf]; E[sf] = E[sf + (sd >> 8)]; E[sf + (sd >> 8)] = t_; });   // undo the median move
                 ps_wsync<false>();
                 ws_segment(E, sf, sl, sd & 0xff, S.rs);

@@ -169,88 +169,6 @@ __device__ inline void ps_heap_sort(unsigned long long* first, unsigned long lon
         ps_adjust_heap(first, 0, (int)(last - first), v);
     }
 }
-// ps_adjust_heap by one wave (all lanes, same arguments; E in LDS, or global with G). Introsort falls back
-// to heap sort on a cube's old points (sorted, one per leaf) + a short appended tail — a pattern that
-// exhausts the depth of median-of-3 partitions on large parts of the array — so this is a hot path there.
-// The sift-down path is resolved 6 levels per step: lane u < 63 is node u of the hole's 6-level subtree
-// (heap-indexed; global node ((hole + 1) << L) - 1 + u - (2^L - 1) at subtree level L) and loads both
-// children at once, picking the right one unless right < left (libstdc++'s tie rule); the path follows the
-// decisions by shuffles and every node on it takes its chosen child by one parallel store. The push-up
-// reads the hole's ancestors (ancestor i of h = ((h + 1) >> i) - 1) at once and climbs over the leading run
-// of ancestors whose key is below the value's.
-__device__ __forceinline__ unsigned long long ps_shfl64(unsigned long long v, int src) {
-    return ((unsigned long long)(unsigned)__shfl((int)(v >> 32), src, WAVE) << 32) | (unsigned)__shfl((int)v, src, WAVE);
-}
-template <bool G>
-__device__ __forceinline__ void ws_adjust_heap(unsigned long long* first, int hole, const int len, const unsigned long long value) {
-    const int lane = lane_id();
-    const int top = hole, lim = (len - 1) / 2;
-    const int L = 31 - __builtin_clz((unsigned)(lane + 1));
-    while (hole < lim) {
-        const long long g = ((long long)(hole + 1) << L) - 1 + (lane - ((1 << L) - 1));
-        const bool can = lane < 63 && g < lim;
-        int c = 0, nu = -1;
-        unsigned long long ec = 0ull;
-        if (can) {
-            c = 2 * (int)g + 2;
-            const unsigned long long er = first[c], el = first[c - 1];
-            if (ps_key(er) < ps_key(el)) { c--; ec = el; nu = 2 * lane + 1; }
-            else { ec = er; nu = 2 * lane + 2; }
-        }
-        unsigned long long onpath = 0ull;
-        int u = 0;
-        for (int s = 0; s < 6; s++) {                // u stays < 63: levels 0-5 of the subtree
-            const int nx = ps_u(__shfl(nu, u, WAVE));
-            if (nx < 0) break;
-            onpath |= 1ull << u;
-            hole = ps_u(__shfl(c, u, WAVE));
-            u = nx;
-        }
-        ps_wsync<G>();                                 // every load of this step before its stores
-        if ((onpath >> lane) & 1ull) first[g] = ec;
-        // a path that stopped inside the subtree left hole >= lim: the loop ends (libstdc++'s condition)
-    }
-    if ((len & 1) == 0 && hole == (len - 2) / 2) {
-        ps_wsync<G>();
-        const unsigned long long e = first[2 * hole + 1];
-        ps_wsync<G>();
-        PS_SAME(first[hole] = e);
-        hole = 2 * hole + 1;
-    }
-    ps_wsync<G>();
-    // push-up: lane i climbs from n_i = ancestor i of the hole to its parent while n_i > top and the parent's
-    // key is below the value's, for every i before it too
-    const unsigned kv = ps_key(value);
-    const int ni = ((hole + 1) >> lane) - 1, pi = ((hole + 1) >> (lane + 1)) - 1;
-    const bool okc = lane < 31 && ni > top;
-    unsigned long long ep = 0ull;
-    if (okc) ep = first[pi];
-    const unsigned long long ok = __ballot(okc && ps_key(ep) < kv);
-    const int s = __builtin_ctzll(~ok);
-    ps_wsync<G>();
-    if (lane < s) first[ni] = ep;
-    if (lane == s) first[ni] = value;
-    ps_wsync<G>();
-}
-// ps_heap_sort (std::__partial_sort(first, last, last)) by one wave
-template <bool G>
-__device__ __forceinline__ void ws_heap_sort(unsigned long long* first, int len) {
-    if (len >= 2) {
-        for (int parent = (len - 2) / 2; parent >= 0; parent--) {
-            const unsigned long long v = first[parent];
-            ws_adjust_heap<G>(first, parent, len, v);
-        }
-    }
-    while (len > 1) {
-        --len;
-        const unsigned long long v = first[len], f0 = first[0];
-        ps_wsync<G>();
-        PS_SAME(first[len] = f0);
-        ps_wsync<G>();
-        ws_adjust_heap<G>(first, 0, len, v);
-    }
-}
-
 // The whole std::sort by one thread (arrays beyond NT * PS_MAX_CHUNK elements): introsort_loop with an
 // explicit stack (the right part is pushed, the left continued — disjoint ranges, same result), then
 // __final_insertion_sort.
@@ -385,8 +303,8 @@ __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const i
         PS_TS(lvl, 0);
         if (nbig == 0) break;
         // depth-exhausted segments: heap sort (rare), emptied from the list below
-        for (int s = tid / WAVE; s < nbig; s += NT / WAVE)
-            if (Bd[s] == 0) ws_heap_sort<G>(E + Bf[s], Bl[s] - Bf[s]);
+        for (int s = tid; s < nbig; s += NT)
+            if (Bd[s] == 0) ps_heap_sort(E + Bf[s], E + Bl[s]);
         if (tid < nbig && Bd[tid] > 0) { Bk[tid] = ps_median_to_first(E, Bf[tid], Bl[tid]); Bkk[tid] = 0; }
         ps_bar<G>();
         int cl = 0, cr = 0;

@@ -17,14 +17,12 @@ def emu(tmp_path_factory):
     return str(exe)
 
 
-@pytest.mark.parametrize("tail,wq", [(None, 0), (4096, 0), (None, 1), (1024, 1)],
-                         ids=["default_tail", "waves_early", "wave_queue", "wave_queue_1024"])
-def test_ls_sort_matches_libstdcxx_under_emulation(tmp_path, tail, wq):
+@pytest.mark.parametrize("tail", [None, 4096], ids=["default_tail", "waves_early"])
+def test_ls_sort_matches_libstdcxx_under_emulation(tmp_path, tail):
     # csrc/ls_sort.hpp on 2 emulated waves (n <= 128 * 16): every introsort level of every segment at once,
-    # the sparse tail per wave (LS_TAIL 4096: the waves take over as soon as <= 2 segments are active; LS_WQ:
-    # as soon as every active segment is short, whatever their number, round-robin over the waves)
+    # the sparse tail per wave (LS_TAIL 4096: the waves take over as soon as <= 2 segments are active)
     exe = tmp_path / "ls_emu"
-    defs = ([f"-DLS_TAIL_DEF={tail}"] if tail else []) + [f"-DLS_WQ={wq}"]
+    defs = [f"-DLS_TAIL_DEF={tail}"] if tail else []
     subprocess.check_call(["g++", "-std=c++20", "-O1", "-pthread", "-w", *defs, "-o", str(exe), os.path.join(HERE, "ps_emu.cpp")])
     r = subprocess.run([str(exe), "40", "13", "1"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -49,9 +47,8 @@ def test_ls_split_list_sort_matches_libstdcxx_under_emulation(emu):
 @pytest.mark.parametrize("mode", [1, 2, 3], ids=["lds", "global", "split_list"])
 def test_heap_sort_fallbacks_match_libstdcxx_under_emulation(emu, mode):
     # sorted prefix + short tail (a map cube's old points + the appended stack points): median-of-3 introsort
-    # exhausts its depth on most of such an array, so the wave heap sort (pcl_sort.hpp ws_heap_sort: 6-level
-    # sift-down steps, one-ballot push-up) carries the result in every path (stage E jobs, wave tail, the
-    # global split)
+    # exhausts its depth on much of such an array, so the heap sorts (std::__partial_sort) of the LDS levels,
+    # the wave tail and the global split carry the result (a flipped tie rule in them fails these trials)
     r = subprocess.run([emu, "5", str(20 + mode), str(mode), "1"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
