@@ -483,6 +483,9 @@ def main():
             # the oracle's VoxelGrids sum every leaf in PCL 1.8's order (libstdc++ std::sort of the (leaf,
             # index) pairs), the order the device reproduces (csrc/pcl_sort.hpp)
             result["ate_delta_vs_pcl_order_m"] = ate
+            # worst single frame of the free-running sequence (mapping position, device vs PCL-order oracle)
+            result["max_frame_delta_vs_pcl_order_m"] = float(np.max(np.linalg.norm(
+                np.array(traj[:m]) - np.array(otraj[:m]), axis=1))) if m else None
             result["ate_frames"] = m
             result["gpu_vs_cpu"] = round(value / world / cpu_value, 2) if cpu_value else None
             result["gpu_vs_cpu_box"] = round(value / world / cb["box"]["scans_per_s"], 2)
