@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ALOAM_ABI_VERSION 3
+#define ALOAM_ABI_VERSION 4
 
 /* error codes */
 #define ALOAM_OK             0
@@ -121,6 +121,13 @@ typedef struct aloam_map_result {
     int    surf_num[ALOAM_MAX_ROUNDS];
     aloam_lm_summary lm[ALOAM_MAX_ROUNDS];
     int    map_total_points;    /* all cubes, corner + surf                            */
+    /* the odometry -> map correction after this frame's transformUpdate (laserMapping.cpp:148-152),
+     * which /aft_mapped_to_init_high_frec applies to every later odometry pose (:197-229) */
+    double q_wmap_wodom[4];
+    double t_wmap_wodom[3];
+    int    frame_count;         /* frameCount of this frame: mapping frames processed before it      */
+    int    pub_surround;        /* frameCount % 5 == 0: /laser_cloud_surround is published (:806)     */
+    int    pub_map;             /* frameCount % 20 == 0: /laser_cloud_map is published (:823)         */
 } aloam_map_result;
 
 /* One residual block of lidarFactor.hpp, flattened.
@@ -185,6 +192,14 @@ int aloam_set_mapping_input(aloam_ctx* ctx, const float* corner_last, int n_corn
 int aloam_get_map_cloud(aloam_ctx* ctx, int which, aloam_cloud* out);
 /* /velodyne_cloud_registered (laserMapping.cpp:838-848): last full cloud in the map frame. */
 int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out);
+/* /aft_mapped_to_init_high_frec (laserOdometryHandler, laserMapping.cpp:197-229): an odometry pose
+ * (/laser_odom_to_init) through the correction of the latest completed mapping frame,
+ * q_out = q_wmap_wodom * q_wodom, t_out = q_wmap_wodom * t_wodom + t_wmap_wodom (Eigen's double
+ * quaternion product and _transformVector; identity before the first mapping frame). Host
+ * arithmetic only: callable from any thread (the reference calls it from the ROS spin thread while
+ * process() runs), also while a pipeline worker runs the context's mapping. */
+int aloam_map_high_freq_pose(aloam_ctx* ctx, const double q_wodom[4], const double t_wodom[3], double q_out[4],
+                             double t_out[3]);
 
 /* ---- whole per-scan pipeline: scanRegistration -> laserOdometry -> laserMapping ----- */
 /* map_out may be NULL. With ALOAM_NO_MAPPING in flags the call stops after laserOdometry and

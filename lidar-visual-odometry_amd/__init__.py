@@ -49,6 +49,8 @@ def _declare(L):
     L.aloam_set_mapping_input.argtypes = [vp, F, C.c_int, F, C.c_int, D, D]
     L.aloam_get_map_cloud.argtypes = [vp, C.c_int, C.POINTER(abi.Cloud)]
     L.aloam_get_registered_cloud.argtypes = [vp, C.POINTER(abi.Cloud)]
+    L.aloam_map_high_freq_pose.argtypes = [vp, D, D, D, D]
+    L.aloam_map_high_freq_pose.restype = C.c_int
     L.aloam_process_scan.argtypes = [vp, C.c_void_p, C.c_int, C.c_int, C.POINTER(abi.OdomResult), C.POINTER(abi.MapResult)]
     L.aloam_eval_factors.argtypes = [vp, C.c_void_p, C.c_int, D, C.c_int, D, D, D]
     L.aloam_lm_solve.argtypes = [vp, C.c_void_p, C.c_int, D, C.POINTER(abi.LMSummary)]
@@ -126,6 +128,7 @@ EXPORTED_SYMBOLS = [
     "aloam_scan_registration_pc2", "aloam_set_cu_mask",
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
+    "aloam_map_high_freq_pose",
 ]
 
 
@@ -248,6 +251,13 @@ class Context:
         c, b = abi.make_cloud(cap)
         self._check(lib().aloam_get_registered_cloud(self.h, C.byref(c)))
         return b[:min(c.n, cap)].copy()
+
+    def high_freq_pose(self, q_wodom, t_wodom):
+        """/aft_mapped_to_init_high_frec of an odometry pose (laserMapping.cpp:197-229): (q, t)."""
+        q, t = np.ascontiguousarray(q_wodom, np.float64), np.ascontiguousarray(t_wodom, np.float64)
+        qo, to = np.zeros(4), np.zeros(3)
+        self._check(lib().aloam_map_high_freq_pose(self.h, abi.dptr(q), abi.dptr(t), abi.dptr(qo), abi.dptr(to)))
+        return qo, to
 
     # ---- whole pipeline ----
     def process_scan(self, pts=None, device_ptr=None, n=None, mapping=True):

@@ -98,6 +98,8 @@ class MapResult(C.Structure):
         ("corner_num", C.c_int * ALOAM_MAX_ROUNDS), ("surf_num", C.c_int * ALOAM_MAX_ROUNDS),
         ("lm", LMSummary * ALOAM_MAX_ROUNDS),
         ("map_total_points", C.c_int),
+        ("q_wmap_wodom", C.c_double * 4), ("t_wmap_wodom", C.c_double * 3),
+        ("frame_count", C.c_int), ("pub_surround", C.c_int), ("pub_map", C.c_int),
     ]
 
 
@@ -221,6 +223,8 @@ def map_to_dict(r):
         "lm": [(r.lm[i].iterations, r.lm[i].successful_steps, r.lm[i].termination,
                 r.lm[i].num_residual_blocks, r.lm[i].initial_cost, r.lm[i].final_cost) for i in range(n)],
         "map_total_points": r.map_total_points,
+        "q_wmap_wodom": np.array(r.q_wmap_wodom[:]), "t_wmap_wodom": np.array(r.t_wmap_wodom[:]),
+        "frame_count": r.frame_count, "pub_surround": r.pub_surround, "pub_map": r.pub_map,
     }
 
 

@@ -392,6 +392,12 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags, bo
     if (!(L == 16 || L == 32 || L == 64) && !C.P.generic_scan_lines)
         throw ApiError{ALOAM_E_SCAN_LINES, "wrong scan number"};
     if (L > MAXL || L <= 0) throw ApiError{ALOAM_E_SCAN_LINES, "scan_line above the device maximum (128)"};
+    // a previous scan's per-line VoxelGrid still pending on stream2 (its odometry threw before queue_meta
+    // made the stream wait): it reads d_cloud and the line scratch this registration rewrites
+    if (C.lf_pending) {
+        HIPCHK(hipStreamWaitEvent(C.stream, C.ev_lf, 0));
+        C.lf_pending = false;
+    }
     const float4* in = (const float4*)xyzr;
     if (!(flags & ALOAM_INPUT_DEVICE) && n > 0) {
         HIPCHK(hipMemcpyAsync(C.d_in, xyzr, sizeof(float4) * n, hipMemcpyHostToDevice, C.stream));
@@ -682,6 +688,7 @@ void mapping_issue(Ctx& C) {
     C.m_pend[slot][0] = in.nc;
     C.m_pend[slot][1] = in.ns;
     C.m_nfull[slot] = in.nf;
+    C.m_frame[slot] = C.map_frame_count;
     C.n_mc += in.nc;                  // the map can grow by at most the frame's stacks until its sizes arrive
     C.n_ms += in.ns;
     C.have_map_input = false;
@@ -745,6 +752,16 @@ void mapping_complete(Ctx& C, aloam_map_result* R) {
     C.map_slots_hint = stackn[0] + stackn[1];
     r.map_total_points = mapn[0] + mapn[1];
     for (int k = 0; k < 7; k++) (k < 4 ? r.q_w_curr[k] : r.t_w_curr[k - 4]) = C.h_map.parameters[k];
+    std::memcpy(r.q_wmap_wodom, C.h_map.q_wmap_wodom, sizeof(r.q_wmap_wodom));
+    std::memcpy(r.t_wmap_wodom, C.h_map.t_wmap_wodom, sizeof(r.t_wmap_wodom));
+    r.frame_count = C.m_frame[slot];
+    r.pub_surround = r.frame_count % 5 == 0;      // laserMapping.cpp:806
+    r.pub_map = r.frame_count % 20 == 0;          // :823
+    {
+        std::lock_guard<std::mutex> g(C.hf_mu);
+        std::memcpy(C.hf_q, r.q_wmap_wodom, sizeof(C.hf_q));
+        std::memcpy(C.hf_t, r.t_wmap_wodom, sizeof(C.hf_t));
+    }
     if (C.profiling) {
         C.timing.mapping_ms = ev_ms(C, 4, 5);
         float s = 0, sol = 0;
@@ -1260,6 +1277,27 @@ int aloam_get_registered_cloud(aloam_ctx* ctx, aloam_cloud* out) {
     d2h_cloud(C, C.d_registered, C.n_registered, out);
     sync(C);
     API_END
+}
+
+// laserOdometryHandler's republication (laserMapping.cpp:212-215): host double arithmetic in Eigen's
+// order (aloam_device.hpp qmul / qrot are the same __host__ __device__ routines the device's
+// transformAssociateToMap uses); no HIP call, so no device is set and no stream is touched
+int aloam_map_high_freq_pose(aloam_ctx* ctx, const double q_wodom[4], const double t_wodom[3], double q_out[4], double t_out[3]) {
+    if (!ctx || !q_wodom || !t_wodom || !q_out || !t_out) return ALOAM_E_ARG;
+    Ctx& C = *(Ctx*)ctx;
+    dquat qm;
+    double tm[3];
+    {
+        std::lock_guard<std::mutex> g(C.hf_mu);
+        qm = {C.hf_q[0], C.hf_q[1], C.hf_q[2], C.hf_q[3]};
+        tm[0] = C.hf_t[0]; tm[1] = C.hf_t[1]; tm[2] = C.hf_t[2];
+    }
+    const dquat qo{q_wodom[0], q_wodom[1], q_wodom[2], q_wodom[3]};
+    const dquat qw = qmul(qm, qo);
+    const dvec3 r = qrot(qm, {t_wodom[0], t_wodom[1], t_wodom[2]});
+    q_out[0] = qw.x; q_out[1] = qw.y; q_out[2] = qw.z; q_out[3] = qw.w;
+    t_out[0] = r.x + tm[0]; t_out[1] = r.y + tm[1]; t_out[2] = r.z + tm[2];
+    return ALOAM_OK;
 }
 
 int aloam_process_scan(aloam_ctx* ctx, const float* xyzr, int n, int flags, aloam_odom_result* o, aloam_map_result* m) {

@@ -276,6 +276,11 @@ struct Ctx {
     int m_pend[2][2] = {{0, 0}, {0, 0}};  // corner / surf stack upper bounds of the frame (map growth)
     int m_nfull[2] = {0, 0};
     int m_set[2] = {0, 0};               // input set of the frame
+    int m_frame[2] = {0, 0};             // frameCount of the frame (laserMapping.cpp:806,823,888)
+    // the odometry -> map correction of the latest completed frame (/aft_mapped_to_init_high_frec):
+    // written by mapping_complete, read by aloam_map_high_freq_pose from any thread
+    std::mutex hf_mu;
+    double hf_q[4] = {0, 0, 0, 1}, hf_t[3] = {0, 0, 0};
     struct GraphSlot { const void* key[2] = {nullptr, nullptr}; int n = -1; hipGraphExec_t exec = nullptr; };
     GraphSlot graphs[4];             // 0,1: odometry rounds (last-cloud buffer parity), 2,3: mapping rounds (input set)
     bool use_graphs = true;          // round loops replayed as HIP graphs when not profiling

@@ -916,6 +916,10 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
     const int c = m->valid_ind[r];
     const CubeArrays& a = K.a;
     const int p0 = a.off[c], n = a.off[c + 1] - p0;
+    int* segl = K.segl + (size_t)r * LS_SEGL;
+    // finished here unless split below; reset before any early return, or k_rb_cubeseg / k_rb_cubered would
+    // read the list a split cube left in this slot in an earlier frame
+    if (threadIdx.x == 0) segl[0] = 0;
     if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
     int fbv[3];
     const int* fb = nullptr;
@@ -925,8 +929,6 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
         for (int d = 0; d < 3; d++) fbv[d] = (int)floorf((float)(50.0 * (cc[d] - cen[d]) - 26.0) * inv);
         fb = fbv;
     }
-    int* segl = K.segl + (size_t)r * LS_SEGL;
-    if (threadIdx.x == 0) segl[0] = 0;            // finished here unless split below
     if (n <= fit) rbv_cube<true>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb, segl, seg_limit);
     else rbv_cube<false>(smem, K.B, a, c, p0, n, K.leaf, K.Cf, K.gscr, fb, segl, seg_limit);
 }
@@ -1041,7 +1043,7 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     prof_phase(C, Ctx::PM_MAP_ADD);
     // tuning knobs: segment size of the split cubes' parallel sorts; cubes up to `fit` points are sorted
     // whole by their own workgroup, larger ones split
-    static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
+    static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(2048, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
     static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_FIT")))) : 4096;
     k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit);
     if (seg_limit <= RBQ_CAP) k_rb_cubeseg_s<<<dim3(125 * RBQ_SEGW, 2), RBQ_T, RBQ_LDS, st>>>(P, C.d_map);

@@ -55,7 +55,7 @@ struct VoxJobs { VoxJob j[2]; };
 // g_vox_seg elements, k_vox_seg sorts the segments in parallel (VX_SEGW workgroups per cloud), k_vox_reduce
 // sums the leaves.
 constexpr int VX_SEGW = 16;
-static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : 4096;   // tuning knob
+static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(2048, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : 4096;   // tuning knob
 // tuning knob: clouds up to this size are sorted whole by their own workgroup, larger ones split
 static const int g_vox_fit = getenv("ALOAM_VOX_FIT") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_FIT")))) : VX_LDS_N;
 static_assert(ls_split_scratch_bytes(VX_T, VX_LDS_N) <= ls_global_scratch_bytes(VX_T, VX_LDS_N), "split scratch");

@@ -153,6 +153,9 @@ __device__ inline void ps_adjust_heap(unsigned long long* first, int hole, int l
 }
 // std::__partial_sort(first, last, last): __make_heap then __sort_heap
 __device__ inline void ps_heap_sort(unsigned long long* first, unsigned long long* last) {
+#ifdef PS_EXP_NOHEAP                         // timing experiment only (results invalid): skip every heap sort
+    return;
+#endif
     const int len = (int)(last - first);
     if (len >= 2) {
         int parent = (len - 2) / 2;

@@ -1,0 +1,214 @@
+// Analysis tool (not product code): statistics of the per-cube VoxelGrid inputs of laserMapping's map filter
+// (src/laserMapping.cpp:788-801) over a synthetic HDL-64 sequence, from the oracle run with a compile-time hook.
+// Per cube filter call: points, leaves by multiplicity (1, 2, >=3), whether the input is already one point per
+// leaf in leaf order, and how libstdc++'s introsort treats it: elements that end in a heap-sorted segment, and
+// whether any heap-sorted segment holds two or more points of a >=3-point leaf (the only case in which the heap
+// sort's tie order can change a centroid's bits: a leaf sum from zero is commutative in its first two terms).
+//
+// build: g++ -O2 -std=c++17 -ffp-contract=off -I include -o /tmp/cube_stats micro/cube_stats.cpp \
+//        lidar-visual-odometry_amd/tools/synth_scan.c -lm
+// run:   /tmp/cube_stats FRAMES [report_every]
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <functional>
+#include <vector>
+
+struct PtI_;
+namespace stats {
+struct Acc {
+    long calls = 0, pts = 0, leaves1 = 0, leaves2 = 0, leaves3 = 0, pts3 = 0, cubes_with3 = 0, cubes_sorted_unique = 0;
+    long heap_elems = 0, heap_segs = 0, heap_calls = 0, heap_matter_calls = 0, heap_matter_segs = 0;
+    long maxn = 0, heap_max = 0, matter_max = 0;
+    long part_full = 0, part_pruned = 0, depth_full = 0, depth_pruned = 0;   // elements partitioned; max recursion depth
+    long heap_steps_full = 0, heap_steps_pruned = 0, heap_steps_max_full = 0, heap_steps_max_pruned = 0;
+};
+Acc acc[2], frame_acc[2];
+template <class V> void hook(const V& in, float leaf, int kind);
+}  // namespace stats
+#define ORACLE_CUBE_HOOK(arr, leaf, kind) stats::hook(arr, leaf, kind)
+#include "../oracle/aloam_oracle.cpp"
+
+extern "C" {
+struct synth_config { int model, n_azimuth; double range_sigma, max_range; unsigned long long seed; double speed, yaw_amp_deg; };
+int synth_generate(const synth_config* cfg, int k, float* out, int max_pts);
+}
+
+namespace stats {
+// introsort replica with instrumentation: records the heap-sorted segments
+struct HS { long f, l; };
+static std::vector<HS> g_heaps;
+template <class T, class Less>
+static void introsort_loop_i(T* base, T* first, T* last, long depth, Less less) {
+    while (last - first > 16) {
+        if (depth == 0) { g_heaps.push_back({first - base, last - base}); orc::heap_sort(first, last, less); return; }
+        --depth;
+        T* mid = first + (last - first) / 2;
+        orc::move_median_to_first(first, first + 1, mid, last - 1, less);
+        T* cut = orc::unguarded_partition(first + 1, last, first, less);
+        introsort_loop_i(base, cut, last, depth, less);
+        last = cut;
+    }
+}
+template <class V> void hook(const V& in, float leaf, int kind) {
+    using orc::PtI;
+    const size_t n = in.size();
+    if (n == 0) return;
+    const float inv = 1.0f / leaf;
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (const auto& p : in) { float c[3] = {p.x, p.y, p.z}; for (int d = 0; d < 3; d++) { mn[d] = std::min(mn[d], c[d]); mx[d] = std::max(mx[d], c[d]); } }
+    int minb[3], maxb[3], divb[3];
+    for (int d = 0; d < 3; d++) { minb[d] = (int)std::floor(mn[d] * inv); maxb[d] = (int)std::floor(mx[d] * inv); divb[d] = maxb[d] - minb[d] + 1; }
+    const int mul1 = divb[0], mul2 = divb[0] * divb[1];
+    struct IV { unsigned idx; unsigned ci; };
+    std::vector<IV> iv(n);
+    for (size_t i = 0; i < n; i++) {
+        int i0 = (int)(std::floor(in[i].x * inv) - (float)minb[0]);
+        int i1 = (int)(std::floor(in[i].y * inv) - (float)minb[1]);
+        int i2 = (int)(std::floor(in[i].z * inv) - (float)minb[2]);
+        iv[i] = {(unsigned)(i0 + i1 * mul1 + i2 * mul2), (unsigned)i};
+    }
+    bool uniq_sorted = true;
+    for (size_t i = 1; i < n; i++) uniq_sorted = uniq_sorted && iv[i - 1].idx < iv[i].idx;
+    std::map<unsigned, int> mult;
+    for (auto& e : iv) mult[e.idx]++;
+    Acc& A = frame_acc[kind];
+    A.calls++; A.pts += n; A.maxn = std::max<long>(A.maxn, n);
+    bool any3 = false;
+    for (auto& kv : mult) {
+        if (kv.second == 1) A.leaves1++; else if (kv.second == 2) A.leaves2++; else { A.leaves3++; A.pts3 += kv.second; any3 = true; }
+    }
+    A.cubes_with3 += any3; A.cubes_sorted_unique += uniq_sorted;
+    g_heaps.clear();
+    auto less = [](const IV& a, const IV& b) { return a.idx < b.idx; };
+    long lg = 63 - __builtin_clzl((unsigned long)n);
+    introsort_loop_i(iv.data(), iv.data(), iv.data() + n, lg * 2, less);
+    if (!g_heaps.empty()) A.heap_calls++;
+    bool matter = false;
+    for (auto& h : g_heaps) {
+        A.heap_segs++; A.heap_elems += h.l - h.f; A.heap_max = std::max(A.heap_max, h.l - h.f);
+        std::map<unsigned, int> in_seg;
+        for (long p = h.f; p < h.l; p++) if (mult[iv[p].idx] >= 3) in_seg[iv[p].idx]++;
+        bool m = false;
+        for (auto& kv : in_seg) m = m || kv.second >= 2;
+        A.heap_matter_segs += m; matter = matter || m; if (m) A.matter_max = std::max(A.matter_max, h.l - h.f);
+    }
+    A.heap_matter_calls += matter;
+    // pruned replay: a segment needs its exact order only if it holds >= 2 members of a >= 3-point leaf at group
+    // ranks where the sum's order matters (not just the group's first two); heap sorts stop after the last
+    // relevant group is popped
+    {
+        std::vector<IV> w(n);
+        for (size_t i = 0; i < n; i++) w[i] = {0, (unsigned)i};
+        for (size_t i = 0; i < n; i++) w[i].idx = 0;
+        // recompute keys in the input order
+        std::vector<unsigned> key(n);
+        for (size_t i = 0; i < n; i++) {
+            int i0 = (int)(std::floor(in[i].x * inv) - (float)minb[0]);
+            int i1 = (int)(std::floor(in[i].y * inv) - (float)minb[1]);
+            int i2 = (int)(std::floor(in[i].z * inv) - (float)minb[2]);
+            key[i] = (unsigned)(i0 + i1 * mul1 + i2 * mul2);
+            w[i] = {key[i], (unsigned)i};
+        }
+        long full_work = 0, pr_work = 0, dfull = 0, dpr = 0, hs_full = 0, hs_pr = 0;
+        std::map<unsigned, int> before;   // unused
+        auto relevant = [&](IV* f, IV* l, IV* base) {
+            std::map<unsigned, int> c;
+            for (IV* p = f; p < l; p++) if (mult[p->idx] >= 3) c[p->idx]++;
+            for (auto& kv : c) {
+                if (kv.second < 2) continue;
+                if (kv.second >= 3) return true;
+                // exactly 2 here: their group ranks = members before f + 1, + 2 (segments partition by key)
+                int b = 0;
+                for (IV* p = base; p < f; p++) b += p->idx == kv.first;
+                if (b >= 1) return true;
+            }
+            return false;
+        };
+        std::function<void(IV*, IV*, long, int, bool)> rec = [&](IV* first, IV* last, long depth, int lev, bool prune_on) {
+            while (last - first > 16) {
+                bool rel = relevant(first, last, w.data());
+                if (depth == 0) {
+                    long m = last - first, lg2 = 64 - __builtin_clzl((unsigned long)m);
+                    hs_full += m * lg2 * 3 / 2;
+                    if (rel) {
+                        unsigned kmin = ~0u;
+                        std::map<unsigned, int> c;
+                        for (IV* p = first; p < last; p++) if (mult[p->idx] >= 3) c[p->idx]++;
+                        for (auto& kv : c) if (kv.second >= 2) kmin = std::min(kmin, kv.first);
+                        long pops = 0;
+                        for (IV* p = first; p < last; p++) pops += p->idx >= kmin;
+                        hs_pr += m / 2 * 2 + pops * lg2;
+                    }
+                    orc::heap_sort(first, last, less);
+                    return;
+                }
+                --depth;
+                full_work += last - first;
+                if (rel) pr_work += last - first;
+                dfull = std::max<long>(dfull, lev + 1);
+                if (rel) dpr = std::max<long>(dpr, lev + 1);
+                IV* mid = first + (last - first) / 2;
+                orc::move_median_to_first(first, first + 1, mid, last - 1, less);
+                IV* cut = orc::unguarded_partition(first + 1, last, first, less);
+                rec(cut, last, depth, lev + 1, prune_on);
+                last = cut;
+                lev++;
+            }
+        };
+        rec(w.data(), w.data() + n, lg * 2, 0, true);
+        A.part_full += full_work; A.part_pruned += pr_work;
+        A.depth_full = std::max(A.depth_full, dfull); A.depth_pruned = std::max(A.depth_pruned, dpr);
+        A.heap_steps_full += hs_full; A.heap_steps_pruned += hs_pr;
+        A.heap_steps_max_full = std::max(A.heap_steps_max_full, hs_full); A.heap_steps_max_pruned = std::max(A.heap_steps_max_pruned, hs_pr);
+    }
+}
+}  // namespace stats
+
+int main(int argc, char** argv) {
+    const int frames = argc > 1 ? atoi(argv[1]) : 60;
+    const int every = argc > 2 ? atoi(argv[2]) : 20;
+    aloam_params p{};
+    p.scan_line = 64; p.minimum_range = 5.0f; p.mapping_skip_frame = 1; p.mapping_line_resolution = 0.4f;
+    p.mapping_plane_resolution = 0.8f; p.input_is_dense = 1; p.odom_rounds = 10; p.map_rounds = 10; p.max_solver_iterations = 4;
+    p.max_scan_points = 400000; p.max_map_points = 4000000;
+    void* o = oracle_create(&p);
+    oracle_set_voxel_order(o, 1);
+    synth_config cfg{64, 2083, 0.02, 120.0, 2, 1.0, 2.0};
+    std::vector<float> buf(64 * 2083 * 4);
+    for (int k = 0; k < frames; k++) {
+        int n = synth_generate(&cfg, k, buf.data(), 64 * 2083);
+        for (auto& a : stats::frame_acc) a = stats::Acc{};
+        oracle_process_scan(o, buf.data(), n, nullptr, nullptr);
+        for (int w = 0; w < 2; w++) {
+            auto& a = stats::frame_acc[w];
+            auto& t = stats::acc[w];
+            t.calls += a.calls; t.pts += a.pts; t.leaves1 += a.leaves1; t.leaves2 += a.leaves2; t.leaves3 += a.leaves3; t.pts3 += a.pts3;
+            t.cubes_with3 += a.cubes_with3; t.cubes_sorted_unique += a.cubes_sorted_unique; t.heap_elems += a.heap_elems;
+            t.heap_segs += a.heap_segs; t.heap_calls += a.heap_calls; t.heap_matter_calls += a.heap_matter_calls;
+            t.part_full += a.part_full; t.part_pruned += a.part_pruned; t.depth_full = std::max(t.depth_full, a.depth_full);
+            t.depth_pruned = std::max(t.depth_pruned, a.depth_pruned); t.heap_steps_full += a.heap_steps_full; t.heap_steps_pruned += a.heap_steps_pruned;
+            t.heap_steps_max_full = std::max(t.heap_steps_max_full, a.heap_steps_max_full); t.heap_steps_max_pruned = std::max(t.heap_steps_max_pruned, a.heap_steps_max_pruned);
+            t.heap_matter_segs += a.heap_matter_segs; t.maxn = std::max(t.maxn, a.maxn); t.heap_max = std::max(t.heap_max, a.heap_max); t.matter_max = std::max(t.matter_max, a.matter_max);
+            if ((k + 1) % every == 0)
+                printf("frame %3d %s: cubes %ld (unique-sorted %ld, with >=3 leaf %ld, heap %ld, heap-order-matters %ld) pts %ld max %ld | "
+                       "leaves 1:%ld 2:%ld >=3:%ld (pts in >=3: %ld) | heap elems %ld segs %ld (matter %ld)\n",
+                       k, w ? "surf  " : "corner", a.calls, a.cubes_sorted_unique, a.cubes_with3, a.heap_calls, a.heap_matter_calls, a.pts,
+                       a.maxn, a.leaves1, a.leaves2, a.leaves3, a.pts3, a.heap_elems, a.heap_segs, a.heap_matter_segs);
+        }
+    }
+    for (int w = 0; w < 2; w++) {
+        auto& t = stats::acc[w];
+        printf("TOTAL %s: cubes %ld (unique-sorted %ld, with >=3 %ld, heap %ld, heap-order-matters %ld) pts %ld max %ld | leaves 1:%ld 2:%ld >=3:%ld pts3 %ld | heap elems %ld segs %ld matter %ld | heap max %ld matter max %ld\n",
+               w ? "surf  " : "corner", t.calls, t.cubes_sorted_unique, t.cubes_with3, t.heap_calls, t.heap_matter_calls, t.pts, t.maxn,
+               t.leaves1, t.leaves2, t.leaves3, t.pts3, t.heap_elems, t.heap_segs, t.heap_matter_segs, t.heap_max, t.matter_max);
+    }
+    for (int w = 0; w < 2; w++) {
+        auto& t = stats::acc[w];
+        printf("PRUNE %s: partition work full %ld pruned %ld | depth full %ld pruned %ld | heap steps full %ld (max/cube %ld) pruned %ld (max/cube %ld)\n",
+               w ? "surf  " : "corner", t.part_full, t.part_pruned, t.depth_full, t.depth_pruned, t.heap_steps_full, t.heap_steps_max_full,
+               t.heap_steps_pruned, t.heap_steps_max_pruned);
+    }
+    oracle_destroy(o);
+    return 0;
+}

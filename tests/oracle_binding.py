@@ -50,6 +50,7 @@ def lib():
         L.oracle_tictoc.argtypes = [vp, C.POINTER(C.c_double)]
         L.oracle_get_map_cloud.argtypes = [vp, C.c_int, C.POINTER(abi.Cloud)]
         L.oracle_get_registered_cloud.argtypes = [vp, C.POINTER(abi.Cloud)]
+        L.oracle_map_high_freq_pose.argtypes = [vp] + [C.POINTER(C.c_double)] * 4
         L.oracle_cube_check.argtypes = [vp, C.POINTER(C.c_int)]
         L.oracle_eval_factors.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int,
                                           C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -179,6 +180,12 @@ class Oracle:
         c, b = abi.make_cloud(cap)
         lib().oracle_get_registered_cloud(self.h, C.byref(c))
         return b[:min(c.n, cap)].copy()
+
+    def high_freq_pose(self, q_wodom, t_wodom):
+        q, t = np.ascontiguousarray(q_wodom, np.float64), np.ascontiguousarray(t_wodom, np.float64)
+        qo, to = np.zeros(4), np.zeros(3)
+        lib().oracle_map_high_freq_pose(self.h, abi.dptr(q), abi.dptr(t), abi.dptr(qo), abi.dptr(to))
+        return qo, to
 
 
 def eval_factors(factors, x, robust=True):
