@@ -21,6 +21,7 @@
 #include "aloam_internal.hpp"
 #include "eigen_small.hpp"
 #include "ls_sort.hpp"
+#include "rvg.hpp"
 
 namespace aloam {
 #ifdef ALOAM_WSTAMP_MAP
@@ -573,76 +574,110 @@ __global__ void k_map_register(const float4* __restrict__ full, int n, const Map
 
 
 // ------------------------------------------------------------------------------------------
-// Per-cube VoxelGrid of the surrounding cubes (:788-801) in ONE launch: one 1024-thread workgroup per
-// surrounding cube c, over its points in B[off[c], off[c+1]) = the cube's old points, then its appended
-// stack points (the order laserCloudCornerArray[ind] has when downSizeFilter.filter runs). The cube's
-// (leaf, position) pairs are put in PCL's order — libstdc++ std::sort by leaf, pcl_sort.hpp — and every
-// leaf is summed from zero in that order (CentroidPoint), so the cube's new points equal PCL's bit for
-// bit. Cubes up to RBV_CAP points sort in LDS, larger ones in the cube's global scratch.
+// Per-cube VoxelGrid of the surrounding cubes (:788-801): one 1024-thread workgroup per surrounding cube c,
+// over its points in B[off[c], off[c+1]) = the cube's old points, then its appended stack points (the order
+// laserCloudCornerArray[ind] has when downSizeFilter.filter runs). PCL sums every leaf from zero in the
+// order libstdc++'s std::sort by leaf leaves the (leaf, position) pairs; rvg.hpp: that order only matters
+// inside leaves of >= 3 points, so the cube is first sorted order-free (R2: the leaves in key order and the
+// points of >= 3-point leaves), and only when such leaves exist is the exact std::sort replayed (R3, heap
+// sorts only where two relevant points meet), each relevant leaf then summed in replay order (R4).
+// Cubes up to RVG_FIT points sort in LDS; larger ones keep their keys in the cube's global scratch
+// (4 u64 per point: E | S | merge buffer | positions + relevance bits), are split by this kernel and their
+// segments replayed by k_rb_cubeseg, summed by k_rb_cubered.
 constexpr int RBV_T = 1024;
 constexpr int RBV_CPW = 10;          // ls_sort: 64-position chunks per wave
-constexpr int RBV_CAP = RBV_T * RBV_CPW;   // cube points sorted in LDS (more: global scratch, staged)
-constexpr size_t RBV_HDR = 64;
+constexpr int RBV_CAP = RBV_T * RBV_CPW;   // LDS element region (E | S | positions for cubes <= RVG_FIT)
+constexpr int RVG_FIT = 4096;        // cubes sorted in LDS (E, S and positions share the element region)
+constexpr int RVG_NEW = 4096;        // big cubes: appended points sorted in LDS for the merge with the old ones
+constexpr int RVG_OLD = 16384;       // big cubes: old keys held in LDS for the merge
+constexpr size_t RBV_HDR = 64 + 512 + 256;   // RbvShared | relevance bits (RVG_FIT) | reduce scan ints
 constexpr size_t RBV_LDS = RBV_HDR + 8 * (size_t)RBV_CAP + ls_global_scratch_bytes(RBV_T, RBV_CAP);
 constexpr int RBV_PER = 8;           // points per thread held in registers for the bbox and the keys
 static_assert(RBV_LDS <= 160 * 1024, "LDS");
-struct RbvShared { unsigned bb[6]; int bad; int pad; };
+static_assert(2 * (size_t)RVG_FIT + RVG_FIT / 2 <= (size_t)RBV_CAP, "E | S | positions (int) in the element region");
+static_assert(4 * (size_t)RVG_OLD + 16 * (size_t)RVG_NEW <= RBV_LDS - RBV_HDR, "merge buffers");
+static_assert(8 * (size_t)RVG_FIT <= ls_global_scratch_bytes(RBV_T, RBV_CAP), "merge-sort buffer in the scratch");
+struct RbvShared { unsigned bb[6]; int bad; int nrel; };
 
-// the cube's sorted (leaf, position) pairs -> centroids (fp32 from zero, in sorted order) at the cube's
-// offset; thread k owns sorted positions [k C, (k+1) C), a run is summed by the thread of its head
-__device__ __forceinline__ void rbv_reduce(const unsigned long long* E, const float4* __restrict__ B, CubeArrays a, int c, int p0,
-                                           int n, float4* __restrict__ Cf, int* sc) {
+// global layout of a split cube's scratch region G = gscr + 4 p0 (4 n u64, n > RVG_FIT >= 512)
+__device__ __forceinline__ unsigned long long* rvg_S(unsigned long long* G, int n) { return G + n; }
+__device__ __forceinline__ unsigned long long* rvg_T(unsigned long long* G, int n) { return G + 2 * (size_t)n + 64; }
+__device__ __forceinline__ int* rvg_fpos(unsigned long long* G, int n) { return (int*)(G + 3 * (size_t)n + 128); }
+__device__ __forceinline__ unsigned* rvg_rel(unsigned long long* G, int n) {
+    return (unsigned*)(G + 3 * (size_t)n + 128 + (size_t)n / 2 + 1);
+}
+
+// R2 of a split cube: S = its (leaf, position) pairs sorted by leaf, in global scratch. The old points are the
+// previous filter's output, one per leaf in leaf order: when their keys are strictly increasing the appended
+// points are sorted in LDS and merged in by rank (binary searches); otherwise one global merge sort.
+__device__ __forceinline__ void rvg_sort_big(unsigned char* smem, unsigned long long* E, int n, int n_old, unsigned long long* S,
+                                             unsigned long long* T) {
+    RbvShared& SH = *(RbvShared*)smem;
     const int tid = threadIdx.x;
-    const int C = (n + RBV_T - 1) / RBV_T;
-    const int q0 = min(n, tid * C), q1 = min(n, q0 + C);
-    int nh = 0;
-    for (int q = q0; q < q1; q++) nh += (q == 0 || ps_key(E[q]) != ps_key(E[q - 1]));
-    int run = nh, dummy = 0, tot, td;
-    ps_exscan2<RBV_T>(run, dummy, sc + 16, tot, td);
-    for (int q = q0; q < q1; q++) {
-        const unsigned k = ps_key(E[q]);
-        if (!(q == 0 || k != ps_key(E[q - 1]))) continue;
-        float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
-        int cnt = 0;
-        for (int t = q; t < n; t += 4) {        // 4 points in flight per step
-            unsigned long long e[4];
-            bool in[4];
-            float4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) { e[u] = t + u < n ? E[t + u] : ~0ull; }
-            bool go = true;
-#pragma unroll
-            for (int u = 0; u < 4; u++) { go = go && t + u < n && ps_key(e[u]) == k; in[u] = go; }
-#pragma unroll
-            for (int u = 0; u < 4; u++) if (in[u]) v[u] = B[p0 + (int)(e[u] & 0xffffffffu)];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (in[u]) { cc.x += v[u].x; cc.y += v[u].y; cc.z += v[u].z; cc.w += v[u].w; cnt++; }
-            if (!in[3]) break;
-        }
-        Cf[p0 + run] = div4_by_count(cc, cnt);
-        run++;
+    const int n_new = n - n_old;
+    if (tid == 0) SH.bad = !(n_old <= RVG_OLD && n_new <= RVG_NEW);
+    __syncthreads();
+    if (!SH.bad) {
+        bool up = true;
+        for (int i = tid; i + 1 < n_old; i += RBV_T) up = up && ps_key(E[i]) < ps_key(E[i + 1]);
+        if (__ballot(!up) && lane_id() == 0) SH.bad = 1;
     }
-    if (tid == 0) a.seg_nout[c] = tot;
+    __syncthreads();
+    if (SH.bad) {                         // generic: the whole cube by one merge sort in global scratch
+        const int n64 = (n + WAVE - 1) / WAVE * WAVE;
+        for (int i = tid; i < n64; i += RBV_T) S[i] = i < n ? E[i] : ~0ull;
+        __syncthreads();
+        const unsigned long long* R = block_merge_sort<unsigned long long, 16, true>(S, T, n64);
+        if (R != S) {
+            for (int i = tid; i < n; i += RBV_T) S[i] = R[i];
+            __syncthreads();
+        }
+        return;
+    }
+    unsigned* OK = (unsigned*)(smem + RBV_HDR);
+    unsigned long long* X = (unsigned long long*)(smem + RBV_HDR + 4 * (size_t)RVG_OLD);
+    unsigned long long* Y = X + RVG_NEW;
+    const int m64 = (n_new + WAVE - 1) / WAVE * WAVE;
+    for (int i = tid; i < n_old; i += RBV_T) OK[i] = ps_key(E[i]);
+    for (int j = tid; j < m64; j += RBV_T) X[j] = j < n_new ? E[n_old + j] : ~0ull;
+    lds_barrier();
+    const unsigned long long* Xs = m64 ? block_merge_sort<unsigned long long, 16>(X, Y, m64) : X;
+    for (int i = tid; i < n_old; i += RBV_T) {          // old point i: after the appended keys below it
+        const unsigned k = OK[i];
+        int lo = 0, hi = n_new;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (ps_key(Xs[mid]) < k) lo = mid + 1; else hi = mid; }
+        S[i + lo] = ((unsigned long long)k << 32) | (unsigned)i;
+    }
+    for (int j = tid; j < n_new; j += RBV_T) {          // appended point: after the old keys <= it
+        const unsigned long long x = Xs[j];
+        const unsigned k = ps_key(x);
+        int lo = 0, hi = n_old;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (OK[mid] <= k) lo = mid + 1; else hi = mid; }
+        S[j + lo] = x;
+    }
+    __syncthreads();
 }
 
 // FITS: the whole cube in LDS. Else (n <= 65536): keys in the cube's global scratch, split into segments of
 // <= seg_limit elements whose list goes to segl (count 0: the cube is finished here) for k_rb_cubeseg and
-// k_rb_cubered; beyond 65536 points one thread sorts (rare).
+// k_rb_cubered.
 template <bool FITS>
 __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __restrict__ B, CubeArrays a, int c, int p0, int n,
                                          float leaf, float4* __restrict__ Cf, unsigned long long* __restrict__ gscr, const int* fb,
                                          int* segl, int seg_limit) {
     RbvShared& SH = *(RbvShared*)smem;
+    unsigned* relL = (unsigned*)(smem + 64);
+    int* rsc = (int*)(smem + 64 + 512);
     const int tid = threadIdx.x;
     // keys in LDS when the cube fits, else in the cube's global scratch (staged through the same LDS
     // buffer by the sort); the sort's scratch behind the buffer
     unsigned long long* EL = (unsigned long long*)(smem + RBV_HDR);
-    unsigned long long* E = FITS ? EL : gscr + 4 * (size_t)p0;
+    unsigned long long* G = gscr + 4 * (size_t)p0;
+    unsigned long long* E = FITS ? EL : G;
     int* sc = (int*)(smem + RBV_HDR + 8 * (size_t)RBV_CAP);
     RBSTAMP(0);
     if (tid < 6) SH.bb[tid] = tid < 3 ? 0xffffffffu : 0u;
-    if (tid == 0) SH.bad = 0;
+    if (tid == 0) { SH.bad = 0; SH.nrel = 0; }
     lds_barrier();
     // the cube's points: up to RBV_PER per thread in registers (bbox, then keys without a reload)
     float4 pt[RBV_PER];
@@ -739,18 +774,55 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
             return;
         }
     }
+    auto ptf = [&](int i) { return B[p0 + i]; };
+    auto outf = [&](int r, float4 v) { Cf[p0 + r] = v; };
     if (FITS) {
-        ls_sort<RBV_T, RBV_CPW>(E, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, RBV_CAP);
-    } else if (n <= RBV_T * PS_MAX_CHUNK) {
-        ls_split_to_list<RBV_T>(E, n, seg_limit, segl, (unsigned char*)sc);   // -> k_rb_cubeseg, k_rb_cubered
+        // R2 in LDS: S = E sorted by one merge sort (buffer: the sort scratch), relevance bits
+        unsigned long long* S = EL + RVG_FIT;
+        int* fpos = (int*)(EL + 2 * RVG_FIT);
+        const int n64 = (n + WAVE - 1) / WAVE * WAVE;
+        for (int i = tid; i < n64; i += RBV_T) S[i] = i < n ? E[i] : ~0ull;
+        for (int i = tid; i < (n + 31) / 32; i += RBV_T) relL[i] = 0u;
+        lds_barrier();
+        const unsigned long long* R = block_merge_sort<unsigned long long, 16>(S, (unsigned long long*)sc, n64);
+        if (R != S) {
+            for (int i = tid; i < n; i += RBV_T) S[i] = R[i];
+            lds_barrier();
+        }
+        rvg_mark<RBV_T>(S, n, relL, &SH.nrel);
+        lds_barrier();
+        RBSTAMP(2);
+        if (SH.nrel > 0) {                    // R3: the exact replay, then the relevant points' positions
+            ls_sort<RBV_T, RBV_CPW>(E, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, RBV_CAP, relL);
+            rvg_positions<RBV_T>(E, n, relL, fpos);
+            lds_barrier();
+        }
+        RBSTAMP(4);
+        const int tot = rvg_reduce<RBV_T>(S, n, relL, fpos, ptf, outf, rsc);
+        if (tid == 0) a.seg_nout[c] = tot;
+        RBSTAMP(5);
         return;
-    } else {                                  // beyond the parallel replay's reach: one thread
+    }
+    if (n > RBV_T * PS_MAX_CHUNK) {           // beyond the parallel replay's reach: one thread, every heap sort
         if (tid == 0) ps_serial_std_sort(E, n);
         __syncthreads();
+        const int tot = rvg_reduce<RBV_T>(E, n, nullptr, nullptr, ptf, outf, rsc);
+        if (tid == 0) a.seg_nout[c] = tot;
+        return;
     }
-    RBSTAMP(4);
-    rbv_reduce(E, B, a, c, p0, n, Cf, sc);
-    RBSTAMP(5);
+    unsigned long long* S = rvg_S(G, n);
+    unsigned* rel = rvg_rel(G, n);
+    for (int i = tid; i < (n + 31) / 32; i += RBV_T) rel[i] = 0u;
+    rvg_sort_big(smem, E, n, old_count(a, c), S, rvg_T(G, n));
+    rvg_mark<RBV_T>(S, n, rel, &SH.nrel);
+    __syncthreads();
+    RBSTAMP(2);
+    if (SH.nrel == 0) {                       // no leaf of >= 3 points: no replay
+        const int tot = rvg_reduce<RBV_T>(S, n, rel, rvg_fpos(G, n), ptf, outf, rsc);
+        if (tid == 0) a.seg_nout[c] = tot;
+        return;
+    }
+    ls_split_to_list<RBV_T>(E, n, seg_limit, segl, (unsigned char*)sc, rel);   // -> k_rb_cubeseg, k_rb_cubered
 }
 
 // ------------------------------------------------------------------------------------------
@@ -942,9 +1014,11 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubeseg(RbKinds P, const MapState*
     if (r >= m->valid_num) return;
     const int* segl = K.segl + (size_t)r * LS_SEGL;
     if (segl[0] == 0) return;
-    const int p0 = K.a.off[m->valid_ind[r]];
+    const int c = m->valid_ind[r];
+    const int p0 = K.a.off[c], n = K.a.off[c + 1] - p0;
+    unsigned long long* G = K.gscr + 4 * (size_t)p0;
     unsigned long long* EL = (unsigned long long*)(smem + RBV_HDR);
-    ls_sort_list<RBV_T, RBV_CPW>(K.gscr + 4 * (size_t)p0, segl, w, RBV_SEGW, EL, RBV_CAP, (unsigned char*)(EL + RBV_CAP));
+    ls_sort_list<RBV_T, RBV_CPW>(G, segl, w, RBV_SEGW, EL, RBV_CAP, (unsigned char*)(EL + RBV_CAP), rvg_rel(G, n));
 }
 // The same for segments of <= RBQ_CAP elements (seg_limit <= RBQ_CAP): 256 threads and ~28 KB of LDS, so
 // several workgroups share a CU. One segment's sort is bound by its levels' barriers and dependent LDS
@@ -959,19 +1033,29 @@ __global__ void __launch_bounds__(RBQ_T) k_rb_cubeseg_s(RbKinds P, const MapStat
     if (r >= m->valid_num) return;
     const int* segl = K.segl + (size_t)r * LS_SEGL;
     if (segl[0] == 0) return;
-    const int p0 = K.a.off[m->valid_ind[r]];
+    const int c = m->valid_ind[r];
+    const int p0 = K.a.off[c], n = K.a.off[c + 1] - p0;
+    unsigned long long* G = K.gscr + 4 * (size_t)p0;
     unsigned long long* EL = (unsigned long long*)smem;
-    ls_sort_list<RBQ_T, RBQ_CPW>(K.gscr + 4 * (size_t)p0, segl, w, RBQ_SEGW, EL, RBQ_CAP, (unsigned char*)(EL + RBQ_CAP));
+    ls_sort_list<RBQ_T, RBQ_CPW>(G, segl, w, RBQ_SEGW, EL, RBQ_CAP, (unsigned char*)(EL + RBQ_CAP), rvg_rel(G, n));
 }
+// the split cubes' relevant points' positions after the segment replays, then the leaf sums (rvg.hpp R4)
 __global__ void __launch_bounds__(RBV_T) k_rb_cubered(RbKinds P, const MapState* __restrict__ m) {
-    __shared__ int sc[16 + 2 * (RBV_T / WAVE) + 2];
+    __shared__ int sc[2 * (RBV_T / WAVE) + 2];
     const RbKind& K = P.k[blockIdx.y];
     const int r = blockIdx.x;
     if (r >= m->valid_num) return;
     if (K.segl[(size_t)r * LS_SEGL] == 0) return;
     const int c = m->valid_ind[r];
     const int p0 = K.a.off[c], n = K.a.off[c + 1] - p0;
-    rbv_reduce(K.gscr + 4 * (size_t)p0, K.B, K.a, c, p0, n, K.Cf, sc);
+    unsigned long long* G = K.gscr + 4 * (size_t)p0;
+    rvg_positions<RBV_T>(G, n, rvg_rel(G, n), rvg_fpos(G, n));
+    __syncthreads();
+    const float4* B = K.B;
+    float4* Cf = K.Cf;
+    const int tot = rvg_reduce<RBV_T>(rvg_S(G, n), n, rvg_rel(G, n), rvg_fpos(G, n), [&](int i) { return B[p0 + i]; },
+                                      [&](int q, float4 v) { Cf[p0 + q] = v; }, sc);
+    if (threadIdx.x == 0) K.a.seg_nout[c] = tot;
 }
 
 __global__ void __launch_bounds__(1024) k_rb_final_scan(RbKinds P, const unsigned char* __restrict__ valid) {
@@ -1044,7 +1128,7 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     // tuning knobs: segment size of the split cubes' parallel sorts; cubes up to `fit` points are sorted
     // whole by their own workgroup, larger ones split
     static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(2048, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
-    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(256, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_FIT")))) : 4096;
+    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(512, std::min(RVG_FIT, atoi(getenv("ALOAM_CUBE_FIT")))) : RVG_FIT;
     k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit);
     if (seg_limit <= RBQ_CAP) k_rb_cubeseg_s<<<dim3(125 * RBQ_SEGW, 2), RBQ_T, RBQ_LDS, st>>>(P, C.d_map);
     else k_rb_cubeseg<<<dim3(125 * RBV_SEGW, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);

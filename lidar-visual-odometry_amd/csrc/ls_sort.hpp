@@ -121,7 +121,7 @@ __device__ __forceinline__ unsigned ls_median_to_first(unsigned long long* E, in
 // RS[j] for j < k as lane gathers, the cut from k. Depth exhausted: heap sort (std::__partial_sort) of the
 // remaining > 16 sub-segments by one lane each. Then every final sub-segment of <= 16 is stably ranked (the
 // final insertion sort) and written back.
-__device__ __forceinline__ void ws_small(unsigned long long* E, const int f, const int m, int d) {
+__device__ __forceinline__ void ws_small(unsigned long long* E, const int f, const int m, int d, const unsigned* rel = nullptr) {
     const int lane = lane_id();
     const unsigned long long lt = lanemask_lt64(), le = lt | (1ull << lane), gt = ~le;
     const unsigned long long all = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
@@ -139,7 +139,7 @@ __device__ __forceinline__ void ws_small(unsigned long long* E, const int f, con
         if (d == 0) {                                    // (rare) heap sort the > 16 sub-segments
             if (in) E[f + lane] = e;
             ps_wsync<false>();
-            if (act && lane == a) ps_heap_sort(E + f + a, E + f + b);
+            if (act && lane == a) ps_heap_sort_rel(E, f + a, f + b, rel);
             ps_wsync<false>();
             e = in ? E[f + lane] : ~0ull;
             k = ps_key(e);
@@ -264,17 +264,17 @@ __device__ __forceinline__ int ws_partition(unsigned long long* E, const int f, 
 
 // introsort_loop of one segment by one wave: partitions while > 64 elements (right children on a lane
 // stack), the <= 64-element parts in registers
-__device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, int d, unsigned short* RS) {
+__device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, int d, unsigned short* RS, const unsigned* rel = nullptr) {
     const int lane = lane_id();
     int sp = 0, stf = 0, stl = 0, std_ = 0;
     for (;;) {
         for (;;) {
             if (l - f <= WAVE) {
-                if (l - f >= 2) ws_small(E, f, l - f, d);
+                if (l - f >= 2) ws_small(E, f, l - f, d, rel);
                 break;
             }
             if (d == 0) {
-                PS_SAME(ps_heap_sort(E + f, E + l));
+                PS_SAME(ps_heap_sort_rel(E, f, l, rel));
                 ps_wsync<false>();
                 break;
             }
@@ -297,7 +297,8 @@ __device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, 
 // payloads (E[i] & 0xffffffff) < 2^16. All NT threads call it with the same arguments; it ends with a
 // barrier.
 template <int NT, int CPW>
-__device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, const int d0, unsigned char* scratch, const int nmax) {
+__device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, const int d0, unsigned char* scratch, const int nmax,
+                                        const unsigned* rel = nullptr) {
     constexpr int W = NT / 64;
     static_assert(NT % 64 == 0 && CPW >= 1 && CPW <= 16, "ls_sort: chunks per wave, one segment per thread");
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
@@ -322,7 +323,7 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             S.seg(0, 2)[0] = d0 | (o << 8);
         }
     } else if (n > PS_THRESHOLD) {
-        if (tid == 0) ps_heap_sort(E, E + n);
+        if (tid == 0) ps_heap_sort_rel(E, 0, n, rel);
     }
     lds_barrier();
     int b = 0;
@@ -442,8 +443,8 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
                 f = F[tid]; l = L[tid]; d = (D[tid] & 0xff) - 1; cut = S.cut[tid];
                 PS_CHECK(cut > f && cut < l, "ls cut: f %d l %d cut %d\n", f, l, cut);
                 atomicOr(&S.bits[cut >> 6], 1ull << (cut & 63));
-                if (cut - f > PS_THRESHOLD) { if (d > 0) aL = 1; else ps_heap_sort(E + f, E + cut); }
-                if (l - cut > PS_THRESHOLD) { if (d > 0) aR = 1; else ps_heap_sort(E + cut, E + l); }
+                if (cut - f > PS_THRESHOLD) { if (d > 0) aL = 1; else ps_heap_sort_rel(E, f, cut, rel); }
+                if (l - cut > PS_THRESHOLD) { if (d > 0) aR = 1; else ps_heap_sort_rel(E, cut, l, rel); }
             }
             const int mine = aL + aR;
             const int incl = wave_incl_scan(mine);
@@ -487,7 +488,7 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
                 const int sf = ps_u(S.seg(b, 0)[wid]), sl = ps_u(S.seg(b, 1)[wid]), sd = ps_u(S.seg(b, 2)[wid]);
                 PS_SAME({ const unsigned long long t_ = E[sf]; E[sf] = E[sf + (sd >> 8)]; E[sf + (sd >> 8)] = t_; });   // undo the median move
                 ps_wsync<false>();
-                ws_segment(E, sf, sl, sd & 0xff, S.rs);
+                ws_segment(E, sf, sl, sd & 0xff, S.rs, rel);
             }
             ns = 0;
         }
@@ -602,7 +603,8 @@ __host__ __device__ constexpr size_t ls_split_scratch_bytes(int NT, int limit) {
     return 4 * (size_t)(16 + 3 * PS_GLIST) + 4 * (size_t)ps_scratch_ints(NT, limit, true);
 }
 template <int NT>
-__device__ __noinline__ void ls_split_to_list_lds(unsigned long long* gE, const int n, const int limit, int* gseg, lds_u8* scrs) {
+__device__ __noinline__ void ls_split_to_list_lds(unsigned long long* gE, const int n, const int limit, int* gseg, lds_u8* scrs,
+                                                  const unsigned* rel) {
     int* H = (int*)(unsigned char*)scrs;
     int* GL = H + 16;
     int* wsc = GL + 3 * PS_GLIST;
@@ -617,22 +619,23 @@ __device__ __noinline__ void ls_split_to_list_lds(unsigned long long* gE, const 
         else if (n >= 2) { GL[0] = 0; GL[1] = n; GL[2] = D0 + 1; H[4] = 1; }
     }
     __syncthreads();
-    if (n > limit) ps_wg_split<NT, true>(gE, n, wsc, limit, &H[4], &H[5], GL, PS_GLIST);
+    if (n > limit) ps_wg_split<NT, true>(gE, n, wsc, limit, &H[4], &H[5], GL, PS_GLIST, rel);
     __syncthreads();
     const int ns = min(H[4], PS_GLIST);
     for (int i = tid; i < 3 * ns; i += NT) gseg[1 + i] = GL[i];
     if (tid == 0) gseg[0] = ns;
 }
 template <int NT>
-__device__ __forceinline__ void ls_split_to_list(unsigned long long* gE, const int n, const int limit, int* gseg, unsigned char* scratch) {
-    ls_split_to_list_lds<NT>(gE, n, limit, gseg, (lds_u8*)scratch);
+__device__ __forceinline__ void ls_split_to_list(unsigned long long* gE, const int n, const int limit, int* gseg, unsigned char* scratch,
+                                                 const unsigned* rel = nullptr) {
+    ls_split_to_list_lds<NT>(gE, n, limit, gseg, (lds_u8*)scratch, rel);
 }
 // Workgroup w of nw: the list's segments of > 64 elements w, w + nw, ... (in list order, counting only
 // those), each copied into EL (cap elements of LDS), sorted by ls_sort from its remaining depth, copied
 // back; the <= 64-element ones one per wave (all waves of all nw workgroups), in registers in place.
 template <int NT, int CPW>
 __device__ __forceinline__ void ls_sort_list(unsigned long long* gE, const int* gseg, int w, int nw, unsigned long long* EL,
-                                             const int cap, unsigned char* scratch) {
+                                             const int cap, unsigned char* scratch, const unsigned* rel = nullptr) {
     const int tid = threadIdx.x, wid = tid / WAVE;
     const int ns = min(gseg[0], PS_GLIST);
     int big = 0, small = 0;
@@ -643,12 +646,12 @@ __device__ __forceinline__ void ls_sort_list(unsigned long long* gE, const int* 
             if (big++ % nw != w) continue;
             for (int t = tid; t < m; t += NT) EL[t] = gE[f + t];
             __syncthreads();
-            ls_sort<NT, CPW>(EL, m, d, scratch, cap);
+            ls_sort<NT, CPW>(EL, m, d, scratch, cap, rel);
             for (int t = tid; t < m; t += NT) gE[f + t] = EL[t];
             __syncthreads();
         } else if (m >= 2) {
             if (small++ % (nw * (NT / WAVE)) != w * (NT / WAVE) + wid) continue;
-            ws_small(gE, f, m, d);
+            ws_small(gE, f, m, d, rel);
         }
     }
 }

@@ -172,6 +172,27 @@ __device__ inline void ps_heap_sort(unsigned long long* first, unsigned long lon
         ps_adjust_heap(first, 0, (int)(last - first), v);
     }
 }
+// Where PCL's order matters (relevance gating). A leaf's CentroidPoint sum starts at zero, so its first two
+// terms commute, ((0 + a) + b) == ((0 + b) + a) bit for bit: the order std::sort leaves equal keys in only
+// changes a centroid for leaves of >= 3 points. rel (may be null: everything matters) marks the points of
+// such leaves, bit i for the point of payload index i (payload bits 0-15). A depth-exhausted introsort
+// segment that holds fewer than two of them is left unsorted instead of heap-sorted: the caller's leaf
+// sums take their order from an order-free sort of the keys, and each relevant point keeps the position
+// range of its segment, which is all its leaf's order needs from it (segments are ordered by key).
+__device__ inline bool ps_order_matters(const unsigned long long* E, int f, int l, const unsigned* rel) {
+    if (!rel) return true;
+    int c = 0;
+    for (int p = f; p < l; p++) {
+        const unsigned i = (unsigned)E[p] & 0xffffu;
+        c += (int)((rel[i >> 5] >> (i & 31u)) & 1u);
+        if (c >= 2) return true;
+    }
+    return false;
+}
+__device__ inline void ps_heap_sort_rel(unsigned long long* E, int f, int l, const unsigned* rel) {
+    if (ps_order_matters(E, f, l, rel)) ps_heap_sort(E + f, E + l);
+}
+
 // The whole std::sort by one thread (arrays beyond NT * PS_MAX_CHUNK elements): introsort_loop with an
 // explicit stack (the right part is pushed, the left continued — disjoint ranges, same result), then
 // __final_insertion_sort.
@@ -282,7 +303,7 @@ __device__ __forceinline__ int ps_prev_stop(const unsigned long long* mask, int 
 // Elements stay in E (LDS, or global with G: loads are batched 8 at a time).
 template <int NT, bool G>
 __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const int limit, int* tail, int* pend, int* Qs,
-                            const int qcap) {
+                            const int qcap, const unsigned* rel = nullptr) {
     const int tid = threadIdx.x;
     int* hdr = sc;
     int* ws = sc + 16;
@@ -307,7 +328,7 @@ __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const i
         if (nbig == 0) break;
         // depth-exhausted segments: heap sort (rare), emptied from the list below
         for (int s = tid; s < nbig; s += NT)
-            if (Bd[s] == 0) ps_heap_sort(E + Bf[s], E + Bl[s]);
+            if (Bd[s] == 0) ps_heap_sort_rel(E, Bf[s], Bl[s], rel);
         if (tid < nbig && Bd[tid] > 0) { Bk[tid] = ps_median_to_first(E, Bf[tid], Bl[tid]); Bkk[tid] = 0; }
         ps_bar<G>();
         int cl = 0, cr = 0;

@@ -1,0 +1,124 @@
+// rvg.hpp — PCL VoxelGrid leaf sums with PCL's order only where it can change a bit ("relevance").
+//
+// pcl::VoxelGrid::applyFilter (PCL 1.8.0) sums every leaf's points from zero in the order an unstable
+// libstdc++ std::sort by leaf leaves them (src/scanRegistration.cpp:401-405, src/laserMapping.cpp:542-550,
+// 788-801). fp32 addition is commutative, so ((0 + a) + b) == ((0 + b) + a) bit for bit: the sort's tie
+// order changes a centroid only for leaves of three or more points. The filter therefore runs in three
+// parts:
+//   R2  an order-free sort S of the (leaf, point) pairs: the leaves in key order (PCL's output order), their
+//       sizes, and `rel`, one bit per point of a >= 3-point leaf;
+//   R3  only when some leaf is relevant: the exact replay of std::sort (ls_sort.hpp), where a depth-exhausted
+//       segment is heap-sorted only if it holds two or more relevant points (pcl_sort.hpp
+//       ps_order_matters); afterwards every relevant point's position orders it inside its leaf (segments
+//       are ordered by key, and inside one only the exact parts' order is used);
+//   R4  the sums: a leaf of <= 2 points in S's order, a relevant one in R3 position order.
+// Checked against the oracle's PCL order (std::sort replica) by the VoxelGrid / mapping parity tests; the
+// equivalence itself on every cube filter of a 60-frame sequence by micro/cube_stats.cpp (CS_RVG=1).
+#pragma once
+#include "pcl_sort.hpp"
+
+namespace aloam {
+
+__device__ __forceinline__ bool rvg_is_rel(const unsigned* rel, unsigned i) { return (rel[i >> 5] >> (i & 31u)) & 1u; }
+
+// S (n pairs sorted by key, any tie order) -> rel bits (zeroed by the caller) for the points of >= 3-point
+// leaves; *nrel (zeroed by the caller) += their count. Thread t walks the leaves that start in its chunk.
+template <int NT>
+__device__ __forceinline__ void rvg_mark(const unsigned long long* S, const int n, unsigned* rel, int* nrel) {
+    const int C = (n + NT - 1) / NT;
+    const int q0 = min(n, (int)threadIdx.x * C), q1 = min(n, q0 + C);
+    int mine = 0;
+    for (int q = q0; q < q1; q++) {
+        const unsigned k = ps_key(S[q]);
+        if (q > 0 && ps_key(S[q - 1]) == k) continue;
+        int e = q + 1;
+        while (e < n && ps_key(S[e]) == k) e++;
+        if (e - q >= 3) {
+            for (int t = q; t < e; t++) {
+                const unsigned i = (unsigned)S[t] & 0xffffu;
+                atomicOr(&rel[i >> 5], 1u << (i & 31u));
+            }
+            mine += e - q;
+        }
+    }
+    if (mine) atomicAdd(nrel, mine);
+}
+
+// the final array E of the exact replay -> fpos[point] = position, for the relevant points
+template <int NT>
+__device__ __forceinline__ void rvg_positions(const unsigned long long* E, const int n, const unsigned* rel, int* fpos) {
+    for (int p = threadIdx.x; p < n; p += NT) {
+        const unsigned i = (unsigned)E[p] & 0xffffu;
+        if (rvg_is_rel(rel, i)) fpos[i] = p;
+    }
+}
+
+// Leaf sums: thread t owns the leaves starting in its chunk of S; out(r, centroid) for the r-th leaf in key
+// order; returns the number of leaves (all threads). A relevant leaf's points are added in fpos order (up
+// to 16 by a register sorting network, more by repeated selection). fpos == null: S is PCL's order itself
+// (every leaf summed in S order; payloads are then full 32-bit point indices). sc: 2 (NT / 64) + 2 ints of
+// LDS.
+template <int NT, typename PtF, typename OutF>
+__device__ __forceinline__ int rvg_reduce(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos, PtF pt,
+                                          OutF out, int* sc) {
+    const bool exact = fpos == nullptr;
+    const unsigned pm = exact ? 0xffffffffu : 0xffffu;
+    const int C = (n + NT - 1) / NT;
+    const int q0 = min(n, (int)threadIdx.x * C), q1 = min(n, q0 + C);
+    int nh = 0;
+    for (int q = q0; q < q1; q++) nh += (q == 0 || ps_key(S[q]) != ps_key(S[q - 1]));
+    int run = nh, dummy = 0, tot, td;
+    ps_exscan2<NT>(run, dummy, sc, tot, td);
+    for (int q = q0; q < q1; q++) {
+        const unsigned k = ps_key(S[q]);
+        if (q > 0 && ps_key(S[q - 1]) == k) continue;
+        int e = q + 1;
+        while (e < n && ps_key(S[e]) == k) e++;
+        const int len = e - q;
+        float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto add = [&](unsigned i) {
+            const float4 v = pt((int)i);
+            cc.x += v.x; cc.y += v.y; cc.z += v.z; cc.w += v.w;
+        };
+        if (len < 3 || exact) {
+            for (int t = q; t < e; t++) add((unsigned)S[t] & pm);
+        } else if (len <= 16) {
+            unsigned v[16];                  // (position << 16) | point, sorted ascending = position order
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const unsigned i = u < len ? ((unsigned)S[q + u] & 0xffffu) : 0u;
+                v[u] = u < len ? (((unsigned)fpos[i] << 16) | i) : 0xffffffffu;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) {   // odd-even transposition network
+#pragma unroll
+                for (int u = r & 1; u + 1 < 16; u += 2) {
+                    const unsigned a = v[u], b = v[u + 1];
+                    v[u] = a < b ? a : b;
+                    v[u + 1] = a < b ? b : a;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 16; u++)
+                if (u < len) add(v[u] & 0xffffu);
+        } else {
+            int last = -1;
+            for (int m = 0; m < len; m++) {
+                int best = 0x7fffffff;
+                unsigned bi = 0;
+                for (int t = q; t < e; t++) {
+                    const unsigned i = (unsigned)S[t] & 0xffffu;
+                    const int fp = fpos[i];
+                    if (fp > last && fp < best) { best = fp; bi = i; }
+                }
+                add(bi);
+                last = best;
+            }
+        }
+        out(run, div4_by_count(cc, len));
+        run++;
+    }
+    return tot;
+}
+
+}  // namespace aloam

@@ -22,6 +22,7 @@ struct Acc {
     long maxn = 0, heap_max = 0, matter_max = 0;
     long part_full = 0, part_pruned = 0, depth_full = 0, depth_pruned = 0;   // elements partitioned; max recursion depth
     long heap_steps_full = 0, heap_steps_pruned = 0, heap_steps_max_full = 0, heap_steps_max_pruned = 0;
+    long po_segs = 0, po_grab = 0, po_ok = 0, po_bad = 0, po_grab_g = 0;   // post-order closed form checks
 };
 Acc acc[2], frame_acc[2];
 template <class V> void hook(const V& in, float leaf, int kind);
@@ -35,6 +36,115 @@ int synth_generate(const synth_config* cfg, int k, float* out, int max_pts);
 }
 
 namespace stats {
+// heap sort of [f, l) with the closed-form prediction for the relevant groups: after make_heap, every key
+// group's pop order (ties go to the right child in __adjust_heap) is the (node, right, left) pre-order of its
+// members' positions, so their final order is the (left, right, node) post-order -- exact as long as no
+// element >= the group's key is taken as the re-inserted `value` (a "grab") before the group is popped.
+template <class T, class Less>
+static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigned, int>& rel, Acc& A) {
+    const long len = last - first;
+    // make_heap
+    if (len >= 2) { long parent = (len - 2) / 2; while (true) { T v = first[parent]; orc::adjust_heap(first, parent, len, v, less); if (parent == 0) break; parent--; } }
+    // post-order positions per relevant group
+    std::map<unsigned, std::vector<unsigned>> pred;
+    std::function<void(long)> post = [&](long x) {
+        if (x >= len) return;
+        post(2 * x + 1); post(2 * x + 2);
+        if (rel.count(first[x].idx)) pred[first[x].idx].push_back(first[x].ci);
+    };
+    post(0);
+    // sort_heap with grab detection per group
+    std::map<unsigned, bool> grabbed;
+    long l = len;
+    while (l > 1) {
+        --l;
+        T v = first[l];
+        for (auto& kv : rel) if (v.idx >= kv.first) {
+            // grab of an element >= K before group K is fully popped: group K still has members in [0, l)?
+            bool left = false;
+            for (long p = 0; p < l; p++) left = left || first[p].idx == kv.first;
+            if (left) grabbed[kv.first] = true;
+        }
+        first[l] = first[0];
+        orc::adjust_heap(first, 0L, l, v, less);
+    }
+    A.po_segs++;
+    bool anyg = false;
+    for (auto& kv : rel) {
+        std::vector<unsigned> got;
+        for (long p = 0; p < len; p++) if (first[p].idx == kv.first) got.push_back(first[p].ci);
+        if (grabbed[kv.first]) { A.po_grab_g++; anyg = true; continue; }
+        if (got == pred[kv.first]) A.po_ok++; else A.po_bad++;
+    }
+    A.po_grab += anyg;
+}
+// Relevance-pruned VoxelGrid (prototype of the device design): the leaf sums need PCL's order only inside
+// leaves of >= 3 points ("relevant"); an introsort segment holding fewer than 2 relevant points is dropped
+// from the replay, and each relevant point's position when its segment is dropped / becomes a <= 16 leaf /
+// is heap-sorted orders it among its leaf's points.
+static long g_rvg_calls = 0, g_rvg_bad = 0;
+template <class V> static void rvg_check(const V& in, float leaf) {
+    using orc::PtI;
+    const size_t n = in.size();
+    if (n == 0) return;
+    std::vector<PtI> ref;
+    orc::voxel_grid(std::vector<PtI>(in.begin(), in.end()), leaf, ref, 1);
+    const float inv = 1.0f / leaf;
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (const auto& p : in) { float c[3] = {p.x, p.y, p.z}; for (int d = 0; d < 3; d++) { mn[d] = std::min(mn[d], c[d]); mx[d] = std::max(mx[d], c[d]); } }
+    int minb[3], maxb[3], divb[3];
+    for (int d = 0; d < 3; d++) { minb[d] = (int)std::floor(mn[d] * inv); maxb[d] = (int)std::floor(mx[d] * inv); divb[d] = maxb[d] - minb[d] + 1; }
+    const int mul1 = divb[0], mul2 = divb[0] * divb[1];
+    struct IV { unsigned idx; unsigned ci; };
+    std::vector<IV> iv(n);
+    for (size_t i = 0; i < n; i++) {
+        int i0 = (int)(std::floor(in[i].x * inv) - (float)minb[0]);
+        int i1 = (int)(std::floor(in[i].y * inv) - (float)minb[1]);
+        int i2 = (int)(std::floor(in[i].z * inv) - (float)minb[2]);
+        iv[i] = {(unsigned)(i0 + i1 * mul1 + i2 * mul2), (unsigned)i};
+    }
+    // R2: order-free grouping
+    std::vector<IV> srt = iv;
+    std::stable_sort(srt.begin(), srt.end(), [](const IV& a, const IV& b) { return a.idx < b.idx; });
+    std::vector<char> rel(n, 0);
+    for (size_t i = 0; i < n;) { size_t j = i; while (j < n && srt[j].idx == srt[i].idx) j++; if (j - i >= 3) for (size_t k = i; k < j; k++) rel[srt[k].ci] = 1; i = j; }
+    // R3: pruned replay; pos[ci] = final ordering position of relevant points
+    std::vector<long> pos(n, -1);
+    std::vector<IV> w = iv;
+    auto less = [](const IV& a, const IV& b) { return a.idx < b.idx; };
+    auto nrel = [&](IV* f, IV* l) { int c = 0; for (IV* p = f; p < l; p++) c += rel[p->ci]; return c; };
+    auto record = [&](IV* f, IV* l) { for (IV* p = f; p < l; p++) if (rel[p->ci]) pos[p->ci] = p - w.data(); };
+    std::function<void(IV*, IV*, long)> rec = [&](IV* first, IV* last, long depth) {
+        while (last - first > 16) {
+            if (nrel(first, last) < 2) { record(first, last); return; }
+            if (depth == 0) { orc::heap_sort(first, last, less); record(first, last); return; }
+            --depth;
+            IV* mid = first + (last - first) / 2;
+            orc::move_median_to_first(first, first + 1, mid, last - 1, less);
+            IV* cut = orc::unguarded_partition(first + 1, last, first, less);
+            rec(cut, last, depth);
+            last = cut;
+        }
+        record(first, last);   // a <= 16 leaf: the final insertion sort keeps equal keys in position order
+    };
+    long lg = 63 - __builtin_clzl((unsigned long)n);
+    rec(w.data(), w.data() + n, lg * 2);
+    // R4: centroids in key order
+    std::vector<PtI> out;
+    for (size_t i = 0; i < n;) {
+        size_t j = i; while (j < n && srt[j].idx == srt[i].idx) j++;
+        std::vector<unsigned> mem;
+        for (size_t k = i; k < j; k++) mem.push_back(srt[k].ci);
+        if (j - i >= 3) std::sort(mem.begin(), mem.end(), [&](unsigned a, unsigned b) { return pos[a] < pos[b]; });
+        float c[4] = {0.f, 0.f, 0.f, 0.f};
+        for (unsigned ci : mem) { const PtI& p = in[ci]; c[0] += p.x; c[1] += p.y; c[2] += p.z; c[3] += p.intensity; }
+        const float cnt = (float)(j - i);
+        out.push_back({c[0] / cnt, c[1] / cnt, c[2] / cnt, c[3] / cnt});
+        i = j;
+    }
+    g_rvg_calls++;
+    if (out.size() != ref.size() || std::memcmp(out.data(), ref.data(), out.size() * sizeof(PtI)) != 0) g_rvg_bad++;
+}
 // introsort replica with instrumentation: records the heap-sorted segments
 struct HS { long f, l; };
 static std::vector<HS> g_heaps;
@@ -94,6 +204,7 @@ template <class V> void hook(const V& in, float leaf, int kind) {
         A.heap_matter_segs += m; matter = matter || m; if (m) A.matter_max = std::max(A.matter_max, h.l - h.f);
     }
     A.heap_matter_calls += matter;
+    if (getenv("CS_RVG")) rvg_check(in, leaf);
     // pruned replay: a segment needs its exact order only if it holds >= 2 members of a >= 3-point leaf at group
     // ranks where the sum's order matters (not just the group's first two); heap sorts stop after the last
     // relevant group is popped
@@ -139,6 +250,11 @@ template <class V> void hook(const V& in, float leaf, int kind) {
                         long pops = 0;
                         for (IV* p = first; p < last; p++) pops += p->idx >= kmin;
                         hs_pr += m / 2 * 2 + pops * lg2;
+                        if (getenv("CS_HEAPS")) printf("HEAP kind %d m %ld pops %ld\n", kind, m, pops);
+                        std::map<unsigned, int> relg;
+                        for (auto& kv : c) if (kv.second >= 2) relg[kv.first] = kv.second;
+                        heap_sort_check(first, last, less, relg, A);
+                        return;
                     }
                     orc::heap_sort(first, last, less);
                     return;
@@ -189,6 +305,7 @@ int main(int argc, char** argv) {
             t.part_full += a.part_full; t.part_pruned += a.part_pruned; t.depth_full = std::max(t.depth_full, a.depth_full);
             t.depth_pruned = std::max(t.depth_pruned, a.depth_pruned); t.heap_steps_full += a.heap_steps_full; t.heap_steps_pruned += a.heap_steps_pruned;
             t.heap_steps_max_full = std::max(t.heap_steps_max_full, a.heap_steps_max_full); t.heap_steps_max_pruned = std::max(t.heap_steps_max_pruned, a.heap_steps_max_pruned);
+            t.po_segs += a.po_segs; t.po_grab += a.po_grab; t.po_ok += a.po_ok; t.po_bad += a.po_bad; t.po_grab_g += a.po_grab_g;
             t.heap_matter_segs += a.heap_matter_segs; t.maxn = std::max(t.maxn, a.maxn); t.heap_max = std::max(t.heap_max, a.heap_max); t.matter_max = std::max(t.matter_max, a.matter_max);
             if ((k + 1) % every == 0)
                 printf("frame %3d %s: cubes %ld (unique-sorted %ld, with >=3 leaf %ld, heap %ld, heap-order-matters %ld) pts %ld max %ld | "
@@ -208,7 +325,10 @@ int main(int argc, char** argv) {
         printf("PRUNE %s: partition work full %ld pruned %ld | depth full %ld pruned %ld | heap steps full %ld (max/cube %ld) pruned %ld (max/cube %ld)\n",
                w ? "surf  " : "corner", t.part_full, t.part_pruned, t.depth_full, t.depth_pruned, t.heap_steps_full, t.heap_steps_max_full,
                t.heap_steps_pruned, t.heap_steps_max_pruned);
+        printf("POSTORDER %s: relevant heap segments %ld (with a grab %ld) | groups predicted ok %ld wrong %ld grabbed %ld\n",
+               w ? "surf  " : "corner", t.po_segs, t.po_grab, t.po_ok, t.po_bad, t.po_grab_g);
     }
+    if (getenv("CS_RVG")) printf("RVG: %ld cube filters, %ld differ from PCL order\n", stats::g_rvg_calls, stats::g_rvg_bad);
     oracle_destroy(o);
     return 0;
 }
