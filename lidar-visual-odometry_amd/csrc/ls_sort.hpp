@@ -45,8 +45,10 @@ constexpr int LS_TAIL = LS_TAIL_DEF;     // the waves take over when every activ
 __host__ __device__ constexpr int ls_nc(int nmax) { return (nmax + 63) / 64; }
 __host__ __device__ constexpr int ls_smax(int nmax) { return nmax / 17 + 2; }
 __host__ __device__ constexpr size_t ls_al8(size_t b) { return (b + 7) & ~(size_t)7; }
+constexpr int LS_HQ = 128;                // depth-exhausted segments queued for the waves' heap sorts (rel)
 __host__ __device__ constexpr size_t ls_scratch_bytes(int NT, int nmax) {
     return ls_al8(4 * (size_t)(16 + 2 * (NT / 64) + 2))          // hdr + scan words
+           + 8 * (size_t)LS_HQ                                   // heap queue (f, l)
            + 3 * 8 * (size_t)(ls_nc(nmax) + 1)                   // maskL, maskR, boundary bits
            + 8 * 64                                              // active-chunk bits (2 levels x 32 words)
            + ls_al8(2 * 4 * (size_t)(ls_nc(nmax) + 1))           // prefL, prefR
@@ -61,12 +63,15 @@ struct LsScr {
     unsigned short* rs;
     int* seg0;           // 2 buffers x (F, L, D, K) x sm ints
     int sm;
+    int* hq;             // heap queue: f, l per entry (count in hdr[6])
     int *bL, *eR, *nR, *cut, *idx;
     __device__ __forceinline__ int* seg(int b, int k) const { return seg0 + (b * 4 + k) * sm; }
     __device__ __forceinline__ LsScr(unsigned char* p, int NT, int nmax) {
         const int nc = ls_nc(nmax), sm = ls_smax(nmax);
         hdr = (int*)p; ws = hdr + 16;
         p += ls_al8(4 * (size_t)(16 + 2 * (NT / 64) + 2));
+        hq = (int*)p;
+        p += 8 * (size_t)LS_HQ;
         maskL = (unsigned long long*)p; maskR = maskL + nc + 1; bits = maskR + nc + 1;
         p += 3 * 8 * (size_t)(nc + 1);
         act = (unsigned long long*)p;
@@ -138,9 +143,15 @@ __device__ __forceinline__ void ws_small(unsigned long long* E, const int f, con
         if (!__ballot(act)) break;
         if (d == 0) {                                    // (rare) heap sort the > 16 sub-segments
             if (in) E[f + lane] = e;
-            ps_wsync<false>();
-            if (act && lane == a) ps_heap_sort_rel(E, f + a, f + b, rel);
-            ps_wsync<false>();
+            ps_wsync<true>();
+            unsigned long long hm = __ballot(act && lane == a);   // the sub-segments, each by the whole wave
+            while (hm) {
+                const int a2 = __builtin_ctzll(hm);
+                hm &= hm - 1ull;
+                const int b2 = readlane_i(b, a2);
+                if (ws_order_matters(E, f + a2, f + b2, rel)) ws_heap_sort(E, f + a2, f + b2, rel);
+            }
+            ps_wsync<true>();
             e = in ? E[f + lane] : ~0ull;
             k = ps_key(e);
             ps_wsync<false>();
@@ -274,7 +285,7 @@ __device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, 
                 break;
             }
             if (d == 0) {
-                PS_SAME(ps_heap_sort_rel(E, f, l, rel));
+                if (ws_order_matters(E, f, l, rel)) ws_heap_sort(E, f, l, rel);
                 ps_wsync<false>();
                 break;
             }
@@ -443,8 +454,16 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
                 f = F[tid]; l = L[tid]; d = (D[tid] & 0xff) - 1; cut = S.cut[tid];
                 PS_CHECK(cut > f && cut < l, "ls cut: f %d l %d cut %d\n", f, l, cut);
                 atomicOr(&S.bits[cut >> 6], 1ull << (cut & 63));
-                if (cut - f > PS_THRESHOLD) { if (d > 0) aL = 1; else ps_heap_sort_rel(E, f, cut, rel); }
-                if (l - cut > PS_THRESHOLD) { if (d > 0) aR = 1; else ps_heap_sort_rel(E, cut, l, rel); }
+                // depth exhausted: heap sort (with rel: queued for the waves, after the levels)
+                auto heap = [&](int f2, int l2) {
+                    if (rel) {
+                        const int q = atomicAdd(&S.hdr[6], 1);
+                        if (q < LS_HQ) { S.hq[2 * q] = f2; S.hq[2 * q + 1] = l2; return; }
+                    }
+                    ps_heap_sort_rel(E, f2, l2, rel);
+                };
+                if (cut - f > PS_THRESHOLD) { if (d > 0) aL = 1; else heap(f, cut); }
+                if (l - cut > PS_THRESHOLD) { if (d > 0) aR = 1; else heap(cut, l); }
             }
             const int mine = aL + aR;
             const int incl = wave_incl_scan(mine);
@@ -494,6 +513,14 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         }
     }
     LS_TS(6);
+    if (rel) {                              // the queued heap sorts, one wave each
+        if (!first) lds_barrier();
+        const int nh = min(S.hdr[6], LS_HQ);
+        for (int i = wid; i < nh; i += W) {
+            const int hf = ps_u(S.hq[2 * i]), hl2 = ps_u(S.hq[2 * i + 1]);
+            if (ws_order_matters(E, hf, hl2, rel)) ws_heap_sort(E, hf, hl2, rel);
+        }
+    }
     // final insertion sort (stable, whole array): every element ranked inside its leaf (<= 16 elements
     // between consecutive boundaries; longer runs were heap-sorted and stay), segment bits cleared
     if (!first) lds_barrier();

@@ -193,6 +193,108 @@ __device__ inline void ps_heap_sort_rel(unsigned long long* E, int f, int l, con
     if (ps_order_matters(E, f, l, rel)) ps_heap_sort(E + f, E + l);
 }
 
+// ---- the heap sort by a whole wave ----------------------------------------------------------------
+// One pop of libstdc++'s __adjust_heap(first, 0, hl, v) (after *last = *first) is, top-down: from the root
+// hole, the larger child (the right one on a tie) moves up while its key is >= v's, then v fills the hole
+// -- Floyd's descend-to-the-leaf-then-push-up gives the same array, as along the max-child path the keys
+// do not increase. The wave resolves six levels per LDS round trip: lane r (< 63) loads the two children
+// of the hole's subtree node r (relative heap numbering, depths 0-5) and votes (child chosen, moves up),
+// the path is walked on the two ballots in scalar registers, and the path's lanes shift their winners up
+// with one store.
+__device__ inline void ws_sift(unsigned long long* H, const int hl, const unsigned long long v) {
+    const int lane = lane_id();
+    const int dr = 31 - __builtin_clz((unsigned)(lane + 1));   // depth of subtree node `lane` (lane 63: unused)
+    const int o = lane + 1 - (1 << dr);
+    const unsigned vk = ps_key(v);
+    int h = 0;
+    for (;;) {
+        int a = 0;
+        bool go = false, right = false;
+        unsigned long long w = 0ull;
+        if (lane < 63) {
+            a = ((h + 1) << dr) - 1 + o;
+            const int c1 = 2 * a + 1;
+            if (c1 < hl) {
+                const unsigned long long e1 = H[c1];
+                unsigned long long e2 = 0ull;
+                if (c1 + 1 < hl) { e2 = H[c1 + 1]; right = !(ps_key(e2) < ps_key(e1)); }
+                w = right ? e2 : e1;
+                go = ps_key(w) >= vk;
+            }
+        }
+        const unsigned long long mgo = __ballot(go), mr = __ballot(right);
+        int r = 0, steps = 0;
+        unsigned long long pm = 0ull;
+        while (steps < 6 && ((mgo >> r) & 1ull)) {
+            pm |= 1ull << r;
+            r = 2 * r + 1 + (int)((mr >> r) & 1ull);
+            steps++;
+        }
+        if ((pm >> lane) & 1ull) H[a] = w;
+        if (steps < 6) {                        // v fills the hole at subtree node r
+            const int ar = readlane_i(a, r);
+            if (lane == 0) H[ar] = v;
+            ps_wsync<true>();
+            return;
+        }
+        ps_wsync<true>();
+        h = ((h + 1) << 6) - 1 + (r - 63);      // the hole went six levels down
+    }
+}
+// std::__partial_sort(E + f, E + l, E + l) (= __make_heap + __sort_heap) by one wave, E in LDS or global.
+// __make_heap adjusts the parents (len - 2) / 2 .. 0 in turn; parents of one depth have disjoint subtrees,
+// so each depth runs on the lanes at once, deepest first. With rel (rvg.hpp), only the order of the
+// relevant points is needed: the pops stop once every element with a key >= the smallest relevant key has
+// been popped into its final slot (pops go in decreasing key order); the rest stays in heap order.
+__device__ inline void ws_heap_sort(unsigned long long* E, const int f, const int l, const unsigned* rel) {
+    const int len = l - f;
+    if (len < 2) return;
+    unsigned long long* H = E + f;
+    const int lane = lane_id();
+    int npop = len - 1;
+    if (rel) {
+        unsigned km = 0xffffffffu;
+        for (int p = lane; p < len; p += WAVE) {
+            const unsigned long long e = H[p];
+            const unsigned i = (unsigned)e & 0xffffu;
+            if ((rel[i >> 5] >> (i & 31u)) & 1u) km = min(km, ps_key(e));
+        }
+        km = allreduce_u32<6>(km, [](unsigned x, unsigned y) { return x < y ? x : y; });
+        int c = 0;
+        for (int p = lane; p < len; p += WAVE) c += ps_key(H[p]) >= km;
+        c = wave_sum_i(c);
+        npop = ps_u(min(len - 1, c));
+    }
+    const int P = (len - 2) / 2;
+    const int D = 31 - __builtin_clz((unsigned)(P + 1));
+    for (int d = D; d >= 0; d--) {
+        const int a0 = (1 << d) - 1, a1 = min((2 << d) - 2, P);
+        for (int base = a0; base <= a1; base += WAVE) {
+            const int node = base + lane;
+            if (node <= a1) ps_adjust_heap(H, node, len, H[node]);
+        }
+        ps_wsync<true>();
+    }
+    for (int i = 0; i < npop; i++) {
+        const int hl = len - 1 - i;
+        const unsigned long long v = H[hl], top = H[0];
+        ps_wsync<true>();
+        if (lane == 0) H[hl] = top;
+        ps_wsync<true>();
+        ws_sift(H, hl, v);
+    }
+}
+// ps_order_matters by a wave (all lanes get the answer)
+__device__ inline bool ws_order_matters(const unsigned long long* E, int f, int l, const unsigned* rel) {
+    if (!rel) return true;
+    int c = 0;
+    for (int p = f + lane_id(); p < l; p += WAVE) {
+        const unsigned i = (unsigned)E[p] & 0xffffu;
+        c += (int)((rel[i >> 5] >> (i & 31u)) & 1u);
+    }
+    return wave_sum_i(c) >= 2;
+}
+
 // The whole std::sort by one thread (arrays beyond NT * PS_MAX_CHUNK elements): introsort_loop with an
 // explicit stack (the right part is pushed, the left continued — disjoint ranges, same result), then
 // __final_insertion_sort.

@@ -118,7 +118,7 @@ using std::min;
 
 // the level-synchronous sort (csrc/ls_sort.hpp) on one emulated workgroup of NT threads
 template <int NT, int CPW>
-static void run_ls(std::vector<unsigned long long>& E) {
+static void run_ls(std::vector<unsigned long long>& E, const unsigned* rel = nullptr) {
     const int n = (int)E.size(), nmax = NT * CPW;
     std::vector<unsigned long long> scr((aloam::ls_scratch_bytes(NT, nmax) + 7) / 8);
     g_waves.clear();
@@ -135,14 +135,14 @@ static void run_ls(std::vector<unsigned long long>& E) {
             threadIdx.x = t;
             t_lane = t % WAVE;
             t_wave = t / WAVE;
-            aloam::ls_sort<NT, CPW>(E.data(), n, d0, (unsigned char*)scr.data(), nmax);
+            aloam::ls_sort<NT, CPW>(E.data(), n, d0, (unsigned char*)scr.data(), nmax, rel);
         });
     for (auto& x : th) x.join();
 }
 // csrc/ls_sort.hpp's split-to-list + ls_sort_list: one emulated workgroup splits, then nw = 2 workgroups
 // (run one after the other) sort their share of the segments
 template <int NT, int CPW>
-static void run_ls_list(std::vector<unsigned long long>& E, int limit) {
+static void run_ls_list(std::vector<unsigned long long>& E, int limit, const unsigned* rel = nullptr) {
     const int n = (int)E.size(), cap = NT * CPW;
     std::vector<unsigned long long> scr((aloam::ls_global_scratch_bytes(NT, cap) + 7) / 8), EL(cap);
     std::vector<int> gseg(aloam::LS_SEGL);
@@ -160,8 +160,8 @@ static void run_ls_list(std::vector<unsigned long long>& E, int limit) {
                 threadIdx.x = t;
                 t_lane = t % WAVE;
                 t_wave = t / WAVE;
-                if (phase == 0) aloam::ls_split_to_list<NT>(E.data(), n, limit, gseg.data(), (unsigned char*)scr.data());
-                else aloam::ls_sort_list<NT, CPW>(E.data(), gseg.data(), phase - 1, 2, EL.data(), cap, (unsigned char*)scr.data());
+                if (phase == 0) aloam::ls_split_to_list<NT>(E.data(), n, limit, gseg.data(), (unsigned char*)scr.data(), rel);
+                else aloam::ls_sort_list<NT, CPW>(E.data(), gseg.data(), phase - 1, 2, EL.data(), cap, (unsigned char*)scr.data(), rel);
             });
         for (auto& x : th) x.join();
     }
@@ -201,6 +201,9 @@ int main(int argc, char** argv) {
     // 1: every trial a sorted prefix of distinct keys + a short unsorted tail of keys next to them (a map
     // cube's old points + the appended ones): introsort exhausts its depth on much of it (heap sorts)
     const bool cube_pattern = argc > 4 && atoi(argv[4]) == 1;
+    // relevance mode (csrc/rvg.hpp): rel = the points of >= 3-point keys; then only those keys' point order
+    // must equal std::sort's (heap sorts gated / queued / stopped early, other ties free)
+    const bool relmode = argc > 5 && atoi(argv[5]) == 1;
     int bad = 0;
     for (int t = 0; t < trials; t++) {
         const bool big = t % 2 == 1;
@@ -231,9 +234,36 @@ int main(int argc, char** argv) {
         }
         std::vector<unsigned long long> A = E;
         std::sort(A.begin(), A.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
+        std::vector<unsigned> rel((n + 31) / 32 + 1, 0u);
+        if (relmode) {
+            for (int i = 0; i < n;) {
+                int j = i;
+                while (j < n && (A[j] >> 32) == (A[i] >> 32)) j++;
+                if (j - i >= 3) for (int k = i; k < j; k++) { const unsigned x = (unsigned)A[k] & 0xffffu; rel[x >> 5] |= 1u << (x & 31); }
+                i = j;
+            }
+        }
+        const unsigned* relp = relmode ? rel.data() : nullptr;
         if (lsm == 2) run_ls_global<128, 16>(E, 300 + (int)(rng() % 1748));
-        else if (lsm == 3) run_ls_list<128, 16>(E, 100 + (int)(rng() % 1948));
-        else run_ls<128, 16>(E);
+        else if (lsm == 3) run_ls_list<128, 16>(E, 100 + (int)(rng() % 1948), relp);
+        else run_ls<128, 16>(E, relp);
+        if (relmode) {            // every >= 3-point key: its points in std::sort's order; E a permutation
+            std::vector<unsigned long long> B = E;
+            std::sort(B.begin(), B.end());
+            std::vector<unsigned long long> A2 = A;
+            std::sort(A2.begin(), A2.end());
+            bool ok = B == A2;
+            std::vector<std::vector<unsigned>> ga, ge;
+            auto order = [&](const std::vector<unsigned long long>& X) {
+                std::vector<std::pair<unsigned, unsigned>> v;   // (key, index) of relevant points in X's order
+                for (auto x : X) { const unsigned i = (unsigned)x & 0xffffu; if ((rel[i >> 5] >> (i & 31)) & 1u) v.push_back({(unsigned)(x >> 32), i}); }
+                std::stable_sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.first < b.first; });
+                return v;
+            };
+            ok = ok && order(A) == order(E);
+            if (!ok) { bad++; std::printf("rel mismatch trial %d n %d kinds %u mode %d\n", t, n, kinds, lsm); }
+            continue;
+        }
         if (A != E) {
             bad++;
             int first = 0;

@@ -52,3 +52,15 @@ def test_heap_sort_fallbacks_match_libstdcxx_under_emulation(emu, mode):
     r = subprocess.run([emu, "5", str(20 + mode), str(mode), "1"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+@pytest.mark.parametrize("mode,cube", [(1, 0), (3, 0), (1, 1), (3, 1)], ids=["lds", "split_list", "lds_cube", "split_list_cube"])
+def test_relevance_gated_sort_orders_relevant_leaves_like_libstdcxx(emu, mode, cube):
+    # csrc/rvg.hpp relevance mode: rel marks the points of >= 3-point keys; depth-exhausted segments with
+    # fewer than two of them are left unsorted, the others heap-sorted by a whole wave (ws_heap_sort: make_heap
+    # by depth levels, six-level pops, stop once the smallest relevant key is out). Every >= 3-point key's
+    # points must still come out in std::sort's order.
+    r = subprocess.run([emu, "8" if cube else "24", str(40 + 2 * mode + cube), str(mode), str(cube), "1"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
