@@ -676,6 +676,9 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     unsigned long long* E = FITS ? EL : G;
     int* sc = (int*)(smem + RBV_HDR + 8 * (size_t)RBV_CAP);
     RBSTAMP(0);
+#ifdef ALOAM_WSTAMP_RB
+    if (threadIdx.x == 0 && blockIdx.x < 128) g_wstamp[(blockIdx.x + (leaf > 0.6f ? 128 : 0)) * WSTAMP_SLOTS + 7] = (unsigned long long)n | ((unsigned long long)FITS << 32) | ((unsigned long long)new_count(a, c) << 40);
+#endif
     if (tid < 6) SH.bb[tid] = tid < 3 ? 0xffffffffu : 0u;
     if (tid == 0) { SH.bad = 0; SH.nrel = 0; }
     lds_barrier();
@@ -789,8 +792,13 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
             for (int i = tid; i < n; i += RBV_T) S[i] = R[i];
             lds_barrier();
         }
+        RBSTAMP(3);
         rvg_mark<RBV_T>(S, n, relL, &SH.nrel);
         lds_barrier();
+#ifdef RVG_EXP_NOREPLAY                         // timing experiment only (results invalid): no exact replay
+        if (tid == 0) SH.nrel = 0;
+        lds_barrier();
+#endif
         RBSTAMP(2);
         if (SH.nrel > 0) {                    // R3: the exact replay, then the relevant points' positions
             ls_sort<RBV_T, RBV_CPW>(E, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, RBV_CAP, relL);
@@ -814,15 +822,22 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     unsigned* rel = rvg_rel(G, n);
     for (int i = tid; i < (n + 31) / 32; i += RBV_T) rel[i] = 0u;
     rvg_sort_big(smem, E, n, old_count(a, c), S, rvg_T(G, n));
+    RBSTAMP(3);
     rvg_mark<RBV_T>(S, n, rel, &SH.nrel);
     __syncthreads();
+#ifdef RVG_EXP_NOREPLAY
+    if (tid == 0) SH.nrel = 0;
+    __syncthreads();
+#endif
     RBSTAMP(2);
     if (SH.nrel == 0) {                       // no leaf of >= 3 points: no replay
         const int tot = rvg_reduce<RBV_T>(S, n, rel, rvg_fpos(G, n), ptf, outf, rsc);
         if (tid == 0) a.seg_nout[c] = tot;
+        RBSTAMP(5);
         return;
     }
     ls_split_to_list<RBV_T>(E, n, seg_limit, segl, (unsigned char*)sc, rel);   // -> k_rb_cubeseg, k_rb_cubered
+    RBSTAMP(6);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -49,17 +49,17 @@ constexpr int LS_HQ = 128;                // depth-exhausted segments queued for
 __host__ __device__ constexpr size_t ls_scratch_bytes(int NT, int nmax) {
     return ls_al8(4 * (size_t)(16 + 2 * (NT / 64) + 2))          // hdr + scan words
            + 8 * (size_t)LS_HQ                                   // heap queue (f, l)
-           + 3 * 8 * (size_t)(ls_nc(nmax) + 1)                   // maskL, maskR, boundary bits
+           + 4 * 8 * (size_t)(ls_nc(nmax) + 1)                   // maskL, maskR, boundary bits, maskV (relevant)
            + 8 * 64                                              // active-chunk bits (2 levels x 32 words)
-           + ls_al8(2 * 4 * (size_t)(ls_nc(nmax) + 1))           // prefL, prefR
+           + ls_al8(3 * 4 * (size_t)(ls_nc(nmax) + 1))           // prefL, prefR, prefV
            + ls_al8(2 * (size_t)nmax)                            // RS_pos (u16)
            + 4 * (size_t)ls_smax(nmax) * 13;                     // 2 x (F, L, D, K) + bL, eR, nR, cut, idx
 }
 
 struct LsScr {
     int* hdr; int* ws;
-    unsigned long long *maskL, *maskR, *bits, *act;
-    int *prefL, *prefR;
+    unsigned long long *maskL, *maskR, *bits, *act, *maskV;
+    int *prefL, *prefR, *prefV;
     unsigned short* rs;
     int* seg0;           // 2 buffers x (F, L, D, K) x sm ints
     int sm;
@@ -72,12 +72,12 @@ struct LsScr {
         p += ls_al8(4 * (size_t)(16 + 2 * (NT / 64) + 2));
         hq = (int*)p;
         p += 8 * (size_t)LS_HQ;
-        maskL = (unsigned long long*)p; maskR = maskL + nc + 1; bits = maskR + nc + 1;
-        p += 3 * 8 * (size_t)(nc + 1);
+        maskL = (unsigned long long*)p; maskR = maskL + nc + 1; bits = maskR + nc + 1; maskV = bits + nc + 1;
+        p += 4 * 8 * (size_t)(nc + 1);
         act = (unsigned long long*)p;
         p += 8 * 64;
-        prefL = (int*)p; prefR = prefL + nc + 1;
-        p += ls_al8(2 * 4 * (size_t)(nc + 1));
+        prefL = (int*)p; prefR = prefL + nc + 1; prefV = prefR + nc + 1;
+        p += ls_al8(3 * 4 * (size_t)(nc + 1));
         rs = (unsigned short*)p;
         p += ls_al8(2 * (size_t)nmax);
         int* q = (int*)p;
@@ -139,7 +139,13 @@ __device__ __forceinline__ void ws_small(unsigned long long* E, const int f, con
         a = ps_msb(starts & le);
         const unsigned long long nb = starts & gt & all;
         b = nb ? __builtin_ctzll(nb) : m;
-        const bool act = in && b - a > PS_THRESHOLD;
+        bool act = in && b - a > PS_THRESHOLD;
+        if (rel) {                                       // sub-segments with < 2 relevant points retire (rvg.hpp)
+            const unsigned i = (unsigned)e & 0xffffu;
+            const unsigned long long mv = __ballot(in && ((rel[i >> 5] >> (i & 31u)) & 1u));
+            const unsigned long long sg = (b >= 64 ? ~0ull : ((1ull << b) - 1ull)) & ~((1ull << a) - 1ull);
+            act = act && __popcll(mv & sg) >= 2;
+        }
         if (!__ballot(act)) break;
         if (d == 0) {                                    // (rare) heap sort the > 16 sub-segments
             if (in) E[f + lane] = e;
@@ -289,6 +295,7 @@ __device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, 
                 ps_wsync<false>();
                 break;
             }
+            if (rel && !ws_order_matters(E, f, l, rel)) break;   // < 2 relevant points: retires (rvg.hpp)
             d = ps_u(d - 1);
             const int cut = ws_partition(E, f, l, RS);
             stf = lane == sp ? cut : stf;
@@ -350,10 +357,10 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         // counts (inactive chunks: none)
 #pragma unroll 2
         for (int c = wid; c < nc; c += W) {
-            unsigned long long mL = 0ull, mR = 0ull;
+            unsigned long long mL = 0ull, mR = 0ull, mV = 0ull;
             if ((actb[c >> 6] >> (c & 63)) & 1ull) {
                 const int p = (c << 6) + lane;
-                bool isL = false, isR = false;
+                bool isL = false, isR = false, isV = false;
                 if (p < n) {
                     unsigned long long e = E[p];
                     int s = ls_seg(e);
@@ -367,12 +374,17 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
                         const unsigned key = ps_key(e), kp = (unsigned)K[s];
                         isL = p > F[s] && key >= kp;
                         isR = key <= kp;
+                        if (rel) { const unsigned i = (unsigned)e & 0xffffu; isV = (rel[i >> 5] >> (i & 31u)) & 1u; }
                     }
                 }
                 mL = __ballot(isL);
                 mR = __ballot(isR);
+                if (rel) mV = __ballot(isV);
             }
-            if (lane == 0) { S.maskL[c] = mL; S.maskR[c] = mR; S.prefL[c] = __popcll(mL); S.prefR[c] = __popcll(mR); }
+            if (lane == 0) {
+                S.maskL[c] = mL; S.maskR[c] = mR; S.prefL[c] = __popcll(mL); S.prefR[c] = __popcll(mR);
+                if (rel) { S.maskV[c] = mV; S.prefV[c] = __popcll(mV); }
+            }
         }
         first = false;
         lds_barrier();
@@ -389,6 +401,16 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
                 carryR += readlane_i(ir, WAVE - 1);
             }
             if (lane == 0) { S.prefL[nc] = carryL; S.prefR[nc] = carryR; S.maskL[nc] = 0ull; S.maskR[nc] = 0ull; }
+        } else if (rel && wid == 1) {
+            int carryV = 0;
+            for (int c0 = 0; c0 < nc; c0 += 64) {
+                const int c = c0 + lane;
+                const int v = c < nc ? S.prefV[c] : 0;
+                const int iv = wave_incl_scan(v);
+                if (c < nc) S.prefV[c] = carryV + iv - v;
+                carryV += readlane_i(iv, WAVE - 1);
+            }
+            if (lane == 0) { S.prefV[nc] = carryV; S.maskV[nc] = 0ull; }
         }
         lds_barrier();
         LS_TS(2);
@@ -400,6 +422,9 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             S.eR[tid] = eR;
             S.nR[tid] = eR - ls_before(S.prefR, S.maskR, f);
             S.cut[tid] = 0x7fffffff;
+            // fewer than two relevant points (rvg.hpp): the segment's order is never read, it retires here
+            // (no swaps: no right stops; eR < 0 marks it for phase E)
+            if (rel && ls_before(S.prefV, S.maskV, l) - ls_before(S.prefV, S.maskV, f) < 2) { S.nR[tid] = 0; S.eR[tid] = -1; }
         }
         for (int c = wid; c < nc; c += W) {
             const unsigned long long mR = S.maskR[c];
@@ -438,7 +463,7 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             const int lo = ps_msb(bnd & le);
             const unsigned long long nb = bnd & gt;
             const unsigned long long grp = (nb ? ((1ull << __builtin_ctzll(nb)) - 1ull) : ~0ull) & ~((1ull << lo) - 1ull);
-            if (isL && !sw && (nswm & grp & lt) == 0ull) atomicMin(&S.cut[s], p);
+            if (isL && !sw && (nswm & grp & lt) == 0ull && S.eR[s] >= 0) atomicMin(&S.cut[s], p);
             if (sw && (swm & grp & gt) == 0ull) atomicMin(&S.cut[s], q);
         }
         lds_barrier();
@@ -450,7 +475,8 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             int* cnt = &S.hdr[8 + (b ^ 1)];
             int* mx = &S.hdr[12 + (b ^ 1)];
             int aL = 0, aR = 0, f = 0, l = 0, cut = 0, d = 0;
-            if (tid < ns) {
+            const bool retired = tid < ns && S.eR[tid] < 0;
+            if (tid < ns && !retired) {
                 f = F[tid]; l = L[tid]; d = (D[tid] & 0xff) - 1; cut = S.cut[tid];
                 PS_CHECK(cut > f && cut < l, "ls cut: f %d l %d cut %d\n", f, l, cut);
                 atomicOr(&S.bits[cut >> 6], 1ull << (cut & 63));
@@ -474,7 +500,8 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
             int* Ln = S.seg(b ^ 1, 1);
             int* Dn = S.seg(b ^ 1, 2);
             int* Kn = S.seg(b ^ 1, 3);
-            if (tid < ns) {
+            if (tid < ns && retired) S.idx[tid] = LS_INACT | (LS_INACT << 16);
+            if (tid < ns && !retired) {
                 // D: depth | (median position - f) << 8 (the wave tail undoes the median move)
                 int o = 0;
                 if (aL) { Fn[base] = f; Ln[base] = cut; Kn[base] = (int)ls_median_to_first(E, f, cut, &o); Dn[base] = d | (o << 8); }

@@ -22,9 +22,9 @@ struct Acc {
     long maxn = 0, heap_max = 0, matter_max = 0;
     long part_full = 0, part_pruned = 0, depth_full = 0, depth_pruned = 0;   // elements partitioned; max recursion depth
     long heap_steps_full = 0, heap_steps_pruned = 0, heap_steps_max_full = 0, heap_steps_max_pruned = 0;
-    long po_segs = 0, po_grab = 0, po_ok = 0, po_bad = 0, po_grab_g = 0;   // post-order closed form checks
+    long po_segs = 0, po_grab = 0, po_ok = 0, po_bad = 0, po_grab_g = 0, po_safe = 0, po_safe_ok = 0, po_noown = 0, po_noown_ok = 0;   // post-order closed form checks
 };
-Acc acc[2], frame_acc[2];
+Acc acc[5], frame_acc[5];
 template <class V> void hook(const V& in, float leaf, int kind);
 }  // namespace stats
 #define ORACLE_CUBE_HOOK(arr, leaf, kind) stats::hook(arr, leaf, kind)
@@ -45,6 +45,15 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
     const long len = last - first;
     // make_heap
     if (len >= 2) { long parent = (len - 2) / 2; while (true) { T v = first[parent]; orc::adjust_heap(first, parent, len, v, less); if (parent == 0) break; parent--; } }
+    // conservative no-grab check per group: no member of G in the last c_G slots after make_heap
+    std::map<unsigned, bool> safe;
+    for (auto& kv : rel) {
+        long cg = 0;
+        for (long p = 0; p < len; p++) cg += first[p].idx >= kv.first;
+        bool ok = true;
+        for (long p = len - cg; p < len; p++) ok = ok && first[p].idx != kv.first;
+        safe[kv.first] = ok;
+    }
     // post-order positions per relevant group
     std::map<unsigned, std::vector<unsigned>> pred;
     std::function<void(long)> post = [&](long x) {
@@ -54,11 +63,12 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
     };
     post(0);
     // sort_heap with grab detection per group
-    std::map<unsigned, bool> grabbed;
+    std::map<unsigned, bool> grabbed, grabbed_own;
     long l = len;
     while (l > 1) {
         --l;
         T v = first[l];
+        for (auto& kv : rel) if (v.idx == kv.first) grabbed_own[kv.first] = true;
         for (auto& kv : rel) if (v.idx >= kv.first) {
             // grab of an element >= K before group K is fully popped: group K still has members in [0, l)?
             bool left = false;
@@ -73,6 +83,8 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
     for (auto& kv : rel) {
         std::vector<unsigned> got;
         for (long p = 0; p < len; p++) if (first[p].idx == kv.first) got.push_back(first[p].ci);
+        if (safe[kv.first]) { A.po_safe++; if (got == pred[kv.first]) A.po_safe_ok++; }
+        if (!grabbed_own[kv.first]) { A.po_noown++; if (got == pred[kv.first]) A.po_noown_ok++; }
         if (grabbed[kv.first]) { A.po_grab_g++; anyg = true; continue; }
         if (got == pred[kv.first]) A.po_ok++; else A.po_bad++;
     }
@@ -250,7 +262,7 @@ template <class V> void hook(const V& in, float leaf, int kind) {
                         long pops = 0;
                         for (IV* p = first; p < last; p++) pops += p->idx >= kmin;
                         hs_pr += m / 2 * 2 + pops * lg2;
-                        if (getenv("CS_HEAPS")) printf("HEAP kind %d m %ld pops %ld\n", kind, m, pops);
+                        if (getenv("CS_HEAPS")) printf("HEAP kind %d m %ld pops %ld n %zu\n", kind, m, pops, n);
                         std::map<unsigned, int> relg;
                         for (auto& kv : c) if (kv.second >= 2) relg[kv.first] = kv.second;
                         heap_sort_check(first, last, less, relg, A);
@@ -295,8 +307,9 @@ int main(int argc, char** argv) {
     for (int k = 0; k < frames; k++) {
         int n = synth_generate(&cfg, k, buf.data(), 64 * 2083);
         for (auto& a : stats::frame_acc) a = stats::Acc{};
+        if (getenv("CS_HEAPS")) printf("FRAME %d\n", k);
         oracle_process_scan(o, buf.data(), n, nullptr, nullptr);
-        for (int w = 0; w < 2; w++) {
+        for (int w = 0; w < 5; w++) {
             auto& a = stats::frame_acc[w];
             auto& t = stats::acc[w];
             t.calls += a.calls; t.pts += a.pts; t.leaves1 += a.leaves1; t.leaves2 += a.leaves2; t.leaves3 += a.leaves3; t.pts3 += a.pts3;
@@ -305,6 +318,7 @@ int main(int argc, char** argv) {
             t.part_full += a.part_full; t.part_pruned += a.part_pruned; t.depth_full = std::max(t.depth_full, a.depth_full);
             t.depth_pruned = std::max(t.depth_pruned, a.depth_pruned); t.heap_steps_full += a.heap_steps_full; t.heap_steps_pruned += a.heap_steps_pruned;
             t.heap_steps_max_full = std::max(t.heap_steps_max_full, a.heap_steps_max_full); t.heap_steps_max_pruned = std::max(t.heap_steps_max_pruned, a.heap_steps_max_pruned);
+            t.po_safe += a.po_safe; t.po_safe_ok += a.po_safe_ok; t.po_noown += a.po_noown; t.po_noown_ok += a.po_noown_ok;
             t.po_segs += a.po_segs; t.po_grab += a.po_grab; t.po_ok += a.po_ok; t.po_bad += a.po_bad; t.po_grab_g += a.po_grab_g;
             t.heap_matter_segs += a.heap_matter_segs; t.maxn = std::max(t.maxn, a.maxn); t.heap_max = std::max(t.heap_max, a.heap_max); t.matter_max = std::max(t.matter_max, a.matter_max);
             if ((k + 1) % every == 0)
@@ -314,19 +328,20 @@ int main(int argc, char** argv) {
                        a.maxn, a.leaves1, a.leaves2, a.leaves3, a.pts3, a.heap_elems, a.heap_segs, a.heap_matter_segs);
         }
     }
-    for (int w = 0; w < 2; w++) {
+    static const char* NM[5] = {"corner", "surf  ", "stk-c ", "stk-s ", "lines "};
+    for (int w = 0; w < 5; w++) {
         auto& t = stats::acc[w];
         printf("TOTAL %s: cubes %ld (unique-sorted %ld, with >=3 %ld, heap %ld, heap-order-matters %ld) pts %ld max %ld | leaves 1:%ld 2:%ld >=3:%ld pts3 %ld | heap elems %ld segs %ld matter %ld | heap max %ld matter max %ld\n",
-               w ? "surf  " : "corner", t.calls, t.cubes_sorted_unique, t.cubes_with3, t.heap_calls, t.heap_matter_calls, t.pts, t.maxn,
+               NM[w], t.calls, t.cubes_sorted_unique, t.cubes_with3, t.heap_calls, t.heap_matter_calls, t.pts, t.maxn,
                t.leaves1, t.leaves2, t.leaves3, t.pts3, t.heap_elems, t.heap_segs, t.heap_matter_segs, t.heap_max, t.matter_max);
     }
-    for (int w = 0; w < 2; w++) {
+    for (int w = 0; w < 5; w++) {
         auto& t = stats::acc[w];
         printf("PRUNE %s: partition work full %ld pruned %ld | depth full %ld pruned %ld | heap steps full %ld (max/cube %ld) pruned %ld (max/cube %ld)\n",
-               w ? "surf  " : "corner", t.part_full, t.part_pruned, t.depth_full, t.depth_pruned, t.heap_steps_full, t.heap_steps_max_full,
+               NM[w], t.part_full, t.part_pruned, t.depth_full, t.depth_pruned, t.heap_steps_full, t.heap_steps_max_full,
                t.heap_steps_pruned, t.heap_steps_max_pruned);
-        printf("POSTORDER %s: relevant heap segments %ld (with a grab %ld) | groups predicted ok %ld wrong %ld grabbed %ld\n",
-               w ? "surf  " : "corner", t.po_segs, t.po_grab, t.po_ok, t.po_bad, t.po_grab_g);
+        printf("POSTORDER %s: relevant heap segments %ld (with a grab %ld) | groups predicted ok %ld wrong %ld grabbed %ld | safe %ld (post-order right %ld) | no own-member grab %ld (right %ld)\n",
+               NM[w], t.po_segs, t.po_grab, t.po_ok, t.po_bad, t.po_grab_g, t.po_safe, t.po_safe_ok, t.po_noown, t.po_noown_ok);
     }
     if (getenv("CS_RVG")) printf("RVG: %ld cube filters, %ld differ from PCL order\n", stats::g_rvg_calls, stats::g_rvg_bad);
     oracle_destroy(o);
