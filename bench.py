@@ -64,6 +64,10 @@ def parse():
                     help="timed C4 scan-to-map registrations, queries sharded over all ranks (0 = skip)")
     ap.add_argument("--c4-reg-only", action="store_true", help="run only the C4 registration section (profiling)")
     ap.add_argument("--c4-cpu-rounds", type=int, default=2, help="rounds of the oracle C4 registration sample")
+    ap.add_argument("--late-start", type=int, default=180,
+                    help="steady-state window: the same sequence continued to this frame, then --late-frames timed "
+                         "(the map has grown; 0 = skip)")
+    ap.add_argument("--late-frames", type=int, default=40)
     return ap.parse_args()
 
 
@@ -110,12 +114,13 @@ def c4_traffic(timeout_s=240):
         shutil.rmtree(out, ignore_errors=True)
 
 
-def cpu_baseline(frames, box_frames, start, timeout_s=600):
+def cpu_baseline(frames, box_frames, start, late_start=0, late_frames=0, timeout_s=900):
     """tests/cpu_baseline.py as a child process (no GPU state inherited): the oracle restatement timed
-    serial / 3-node pipelined / P-sequence box on this host's cores. None on any failure."""
+    serial / 3-node pipelined / P-sequence box on this host's cores, and (late_start > 0) the steady-state
+    window of the same sequence. None on any failure."""
     import subprocess
     cmd = [sys.executable, os.path.join(REPO, "tests", "cpu_baseline.py"), "--frames", str(frames), "--start", str(start),
-           "--box-frames", str(box_frames)]
+           "--box-frames", str(box_frames), "--late-start", str(late_start), "--late-frames", str(late_frames)]
     try:
         r = subprocess.run(cmd, cwd=REPO, timeout=timeout_s, check=True, capture_output=True, text=True)
         return json.loads(r.stdout.strip().splitlines()[-1])
@@ -246,7 +251,12 @@ def main():
     # independent replica per rank: a different stretch of the synthetic street
     start = lvo.replicas.replica_start_frame(rank)
     P = max(args.prof_frames, 1)
-    frames = lvo.synth.sequence("hdl64", W + K + P, start=start)
+    LS, LF = args.late_start, args.late_frames
+    late = LS > 0 and LF > 0 and args.mode == "pipeline"
+    if late:
+        LS = max(LS, W + K + P)
+    n_seq = LS + LF + P if late else W + K + P
+    frames = lvo.synth.sequence("hdl64", n_seq, start=start)
     n_pts = [len(f) for f in frames]
     dev = torch.device("cuda", local_rank)
     d_frames = [torch.from_numpy(f).to(dev) for f in frames]
@@ -344,6 +354,61 @@ def main():
             if mp is not None:
                 traj.append(mp["t_w_curr"])
         pipe.set_profiling(False)
+
+    # steady state: the same sequence continued until the map has grown (surrounding cubes
+    # of ~10-17k points), LF timed frames there, then P profiled frames for the TicToc stages
+    steady = None
+    if late:
+        for k in range(W + K + P, LS):
+            od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
+        traj += [mp["t_w_curr"] for _, mp in pipe.flush() if mp is not None]
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        last_mp = None
+        for k in range(LS, LS + LF):
+            od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
+                last_mp = mp
+        for _, mp in pipe.flush():
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
+                last_mp = mp
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el2 = time.perf_counter() - t1
+        if dist:
+            t = torch.tensor([el2], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        tt2, tn2 = np.zeros(NT), np.zeros(NT)
+        pipe.set_profiling(True)
+        for k in range(LS + LF, LS + LF + P):
+            od, mp = pipe.push(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])
+            tb = pipe.last_back_timing if mp is not None else None
+            if tb is not None:
+                for i in range(8, NT):
+                    tt2[i] += tb["tictoc_ms"][i]
+                    tn2[i] += 1
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
+                last_mp = mp
+        for od, mp in pipe.flush():
+            if mp is not None:
+                traj.append(mp["t_w_curr"])
+        pipe.set_profiling(False)
+        steady = {
+            "frames": [LS, LS + LF - 1], "scans_per_s": round(lvo.replicas.aggregate_rate(LF, world, el2), 3),
+            "ms_per_scan": round(el2 / LF * 1000.0, 4),
+            "tictoc_ms": {lvo.abi.TICTOC_NAMES[i]: round(float(tt2[i] / tn2[i]), 4) for i in range(8, NT) if tn2[i]},
+            "map_total_points": int(last_mp["map_total_points"]) if last_mp is not None else None,
+            "surround_points": int(last_mp["map_corner_num"] + last_mp["map_surf_num"]) if last_mp is not None else None,
+        }
 
     value = lvo.replicas.aggregate_rate(K, world, elapsed)
     ms_per_step = elapsed / K * 1000.0
@@ -452,8 +517,11 @@ def main():
         except Exception as e:  # noqa: BLE001
             result["c4_registration"] = {"error": repr(e)}
 
+    if steady is not None:
+        result["steady_state"] = steady
     if rank == 0 and not args.no_cpu:
-        cb = cpu_baseline(args.cpu_frames, args.cpu_box_frames, lvo.replicas.replica_start_frame(rank))
+        cb = cpu_baseline(args.cpu_frames, args.cpu_box_frames, lvo.replicas.replica_start_frame(rank),
+                          late_start=LS if late else 0, late_frames=LF)
         if cb is not None:
             pipelined, serial = cb["pipelined"]["scans_per_s"], cb["serial"]["scans_per_s"]
             cpu_value = pipelined if args.mode == "pipeline" else serial
@@ -477,6 +545,21 @@ def main():
                 "tictoc_ms": cb["serial"]["tictoc_ms"],
             }
             otraj = cb["traj"]
+            lt = cb.get("late")
+            if lt is not None:
+                otraj = lt["traj"]                 # the whole sequence 0 .. late window end
+                lsm = lt["stage_ms"]
+                gpu_ss = result.get("steady_state", {})
+                result.setdefault("steady_state", {})["cpu_baseline"] = {
+                    "frames": lt["frames"], "serial_1core": round(lt["serial_scans_per_s"], 4),
+                    "pipelined_3core_est": round(lt["pipelined_est_scans_per_s"], 4) if lt["pipelined_est_scans_per_s"] else None,
+                    "stage_ms": {k2: round(v2, 3) for k2, v2 in lsm.items()},
+                    "note": "one serial oracle run over the whole sequence (the map grows as in the GPU run), the window "
+                            "timed; the 3-node rate is estimated as 1 / the slowest node's mean time in the window",
+                    "tictoc_ms": lt["tictoc_ms"]}
+                if gpu_ss.get("scans_per_s") and lt["pipelined_est_scans_per_s"]:
+                    result["steady_state"]["gpu_vs_cpu_pipelined"] = round(gpu_ss["scans_per_s"] / world / lt["pipelined_est_scans_per_s"], 2)
+                    result["steady_state"]["gpu_vs_cpu_serial"] = round(gpu_ss["scans_per_s"] / world / lt["serial_scans_per_s"], 2)
             m = min(len(otraj), len(traj))
             ate = float(np.sqrt(np.mean(np.sum((np.array(traj[:m]) - np.array(otraj[:m])) ** 2, axis=1))))
             result["ate_delta_vs_oracle_m"] = ate

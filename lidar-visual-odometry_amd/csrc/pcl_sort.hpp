@@ -246,6 +246,85 @@ __device__ inline void ws_sift(unsigned long long* H, const int hl, const unsign
 // so each depth runs on the lanes at once, deepest first. With rel (rvg.hpp), only the order of the
 // relevant points is needed: the pops stop once every element with a key >= the smallest relevant key has
 // been popped into its final slot (pops go in decreasing key order); the rest stays in heap order.
+// Nodes of the subtree of `node` in a heap of len slots, and a node's index in the heap's post-order
+// (left subtree, right subtree, node).
+__device__ inline int heap_subtree_size(int node, const int len) {
+    int tot = 0;
+    for (int k = 0;; k++) {
+        const long long lo = ((long long)(node + 1) << k) - 1;
+        if (lo >= len) break;
+        tot += (int)(min((long long)len, lo + (1ll << k)) - lo);
+    }
+    return tot;
+}
+__device__ inline int heap_postorder(const int i, const int len) {
+    const int di = 31 - __builtin_clz((unsigned)(i + 1));
+    int a = 0, start = 0;
+    for (int da = 0; da < di; da++) {
+        const int anc = ((i + 1) >> (di - da - 1)) - 1;     // i's ancestor one level below a
+        if (anc != 2 * a + 1) start += heap_subtree_size(2 * a + 1, len);
+        a = anc;
+    }
+    return start + heap_subtree_size(i, len) - 1;
+}
+// __sort_heap without the pops, where that is provably the same for the relevant points (rvg.hpp): after
+// __make_heap, the pops take the root, the larger child (the right one on a tie) moving up, so points of
+// one key leave the heap in (node, right subtree, left subtree) pre-order of their slots -- the moves keep
+// that order among equal keys -- and land in the reverse, the post-order (left, right, node). Only one
+// thing breaks it: a point of the key taken as a pop's re-inserted value (the heap's last slot), which
+// needs it to sit among the last c slots (c = points with keys >= its key: the pops until the key is out)
+// and to stay there; a point taken this way with a larger key only moves larger points, whose order
+// among themselves is not read. So when no relevant point sits in its danger zone, the segment is
+// written in post-order of the heap slots (each relevant leaf's points then in PCL's order, the other
+// points anywhere inside the segment, which rvg.hpp allows) and the pops are skipped. len <= 16 * 64.
+// Checked against libstdc++'s heap sort by micro/cube_stats.cpp (POSTORDER "safe": every safe group
+// right) and the host emulator. Returns false (nothing written) when some relevant point is in danger.
+__device__ inline bool ws_heap_postorder(unsigned long long* H, const int len, const int npop, const unsigned* rel) {
+    const int lane = lane_id();
+    // candidates: relevant points in the last npop slots (npop = points >= the smallest relevant key)
+    bool danger = false;
+    for (int s0 = len - npop; s0 < len; s0 += WAVE) {
+        const int sl = s0 + lane;
+        unsigned long long e = 0ull;
+        bool cand = false;
+        if (sl < len) {
+            e = H[sl];
+            const unsigned i = (unsigned)e & 0xffffu;
+            cand = (rel[i >> 5] >> (i & 31u)) & 1u;
+        }
+        unsigned long long cm = __ballot(cand);
+        while (cm) {                                  // exact zone of each candidate: count_ge(key) >= len - slot
+            const int b = __builtin_ctzll(cm);
+            cm &= cm - 1ull;
+            const unsigned kx = (unsigned)readlane_i((int)ps_key(e), b);
+            const int sx = s0 + b;
+            int c = 0;
+            for (int p = lane; p < len; p += WAVE) c += ps_key(H[p]) >= kx;
+            c = wave_sum_i(c);
+            if (c >= len - sx) { danger = true; break; }
+        }
+        if (danger) break;
+    }
+    if (danger) return false;
+#ifdef PS_POSTORDER_COUNT                           // host-emulator coverage counter (tests/ps_emu.cpp)
+    if (lane == 0) PS_POSTORDER_COUNT++;
+#endif
+    unsigned long long ev[16];
+    int dst[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int i = lane + WAVE * j;
+        dst[j] = -1;
+        if (i < len) { ev[j] = H[i]; dst[j] = heap_postorder(i, len); }
+    }
+    ps_wsync<true>();
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if (dst[j] >= 0) H[dst[j]] = ev[j];
+    ps_wsync<true>();
+    return true;
+}
+
 __device__ inline void ws_heap_sort(unsigned long long* E, const int f, const int l, const unsigned* rel) {
     const int len = l - f;
     if (len < 2) return;
@@ -275,6 +354,7 @@ __device__ inline void ws_heap_sort(unsigned long long* E, const int f, const in
         }
         ps_wsync<true>();
     }
+    if (rel && len <= 16 * WAVE && ws_heap_postorder(H, len, npop, rel)) return;
     for (int i = 0; i < npop; i++) {
         const int hl = len - 1 - i;
         const unsigned long long v = H[hl], top = H[0];
@@ -284,6 +364,72 @@ __device__ inline void ws_heap_sort(unsigned long long* E, const int f, const in
         ws_sift(H, hl, v);
     }
 }
+// The pops of __sort_heap pipelined over the lanes of one wave: pop i runs on lane i % 64, one heap level
+// per step, in the top-down form of __adjust_heap (see ws_sift). Consecutive pops are two levels apart: in
+// a step every pop first writes the element it chose in the previous step into its hole's parent slot,
+// then reads its hole's children, so a pop reads a level only after the pop ahead of it (two levels
+// deeper) has finished writing it. Pop i starts no earlier than two steps after pop i - 1, and only once no
+// pop in flight still has slot hl_i (its value, the heap's last slot) below or at its hole: from then on
+// that slot is pop i's alone, so the popped root goes straight into it. The result is std::__sort_heap's
+// array; pops stop after npop (the early stop of ws_heap_sort).
+__device__ inline void ws_sort_heap_pipelined(unsigned long long* H, const int len, const int npop) {
+    const int lane = lane_id();
+    // this lane's pop (if any): hole h, its level, heap size hl, value v, the element to write next into
+    // slot par (par < 0: none), done flag
+    int h = 0, hl = 0, par = -1;
+    unsigned long long v = 0ull, pend = 0ull;
+    bool act = false, stop = false;
+    int next = 0, last_start = -2;             // next pop to start; step of the last start (uniform)
+    for (int t = 0;; t++) {
+        // phase 1: pending writes (the winner moved up into the parent slot, or v placed: pop done)
+        if (act && par >= 0) {
+            H[par] = pend;
+            if (stop) act = false;
+        }
+        // start the next pop: no pop in flight may still write its value slot hl = len - 1 - next
+        bool started = false;
+        if (next < npop && t - last_start >= 2) {
+            const int hn = len - 1 - next;
+            bool anc = false;
+            if (act) {                          // h an ancestor (or itself) of hn?
+                const int dh = 31 - __builtin_clz((unsigned)(h + 1)), dn = 31 - __builtin_clz((unsigned)(hn + 1));
+                anc = dn >= dh && (((hn + 1) >> (dn - dh)) - 1) == h;
+            }
+            if (!__ballot(anc)) {
+                started = true;
+                if (lane == (next & 63)) {
+                    act = true; stop = false; par = -1; h = 0; hl = hn;
+                    v = H[hn];
+                    H[hn] = H[0];               // the popped root into its final slot
+                }
+                next++;
+                last_start = t;
+            }
+        }
+        if (!__ballot(act) && next >= npop) break;
+        // phase 2: read the hole's children, choose (ties: the right one), decide
+        if (act) {
+            const int c1 = 2 * h + 1;
+            unsigned long long w = 0ull;
+            int wi = -1;
+            if (c1 < hl) {
+                const unsigned long long e1 = H[c1];
+                wi = c1; w = e1;
+                if (c1 + 1 < hl) {
+                    const unsigned long long e2 = H[c1 + 1];
+                    if (!(ps_key(e2) < ps_key(e1))) { wi = c1 + 1; w = e2; }
+                }
+            }
+            par = h;
+            if (wi >= 0 && ps_key(w) >= ps_key(v)) { pend = w; h = wi; stop = false; }
+            else { pend = v; stop = true; }
+        }
+        (void)started;
+        ps_wsync<true>();
+    }
+    ps_wsync<true>();
+}
+
 // ps_order_matters by a wave (all lanes get the answer)
 __device__ inline bool ws_order_matters(const unsigned long long* E, int f, int l, const unsigned* rel) {
     if (!rel) return true;

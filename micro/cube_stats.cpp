@@ -64,10 +64,16 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
     post(0);
     // sort_heap with grab detection per group
     std::map<unsigned, bool> grabbed, grabbed_own;
+    unsigned kmin = ~0u;
+    for (auto& kv : rel) kmin = std::min(kmin, kv.first);
+    long cmin = 0;
+    for (long p = 0; p < len; p++) cmin += first[p].idx >= kmin;
+    long tgrabs = 0;
     long l = len;
     while (l > 1) {
         --l;
         T v = first[l];
+        if (len - 1 - l < cmin && v.idx >= kmin) tgrabs++;
         for (auto& kv : rel) if (v.idx == kv.first) grabbed_own[kv.first] = true;
         for (auto& kv : rel) if (v.idx >= kv.first) {
             // grab of an element >= K before group K is fully popped: group K still has members in [0, l)?
@@ -89,6 +95,7 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
         if (got == pred[kv.first]) A.po_ok++; else A.po_bad++;
     }
     A.po_grab += anyg;
+    if (getenv("CS_TGRAB")) printf("TGRAB len %ld cmin %ld grabs %ld\n", len, cmin, tgrabs);
 }
 // Relevance-pruned VoxelGrid (prototype of the device design): the leaf sums need PCL's order only inside
 // leaves of >= 3 points ("relevant"); an introsort segment holding fewer than 2 relevant points is dropped

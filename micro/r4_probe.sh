@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 120 python micro/ls_bench.py 1300 2000 4000 6000 10000 > gpurun_out/r4_lsbench.txt 2>&1 || exit 1
+#timeout -k 10 120 python micro/ls_bench.py 1300 2000 4000 6000 10000 > gpurun_out/r4_lsbench.txt 2>&1 || exit 1
 B="--no-cpu --c4-launches 0 --c4-reg-steps 0 --no-traffic"
 for st in 50 200; do
   for v in "" micro/_var_noheap/libaloam_hip.so; do

@@ -15,7 +15,12 @@ parent's GPU state is inherited) or by hand. Forms:
              at most --box-max): the host's aggregate scans/s
 Prints one JSON object (stdout).
 
-usage: python tests/cpu_baseline.py [--frames N] [--start K] [--box-frames M] [--box-max P]
+  late       (--late-start S --late-frames F) one serial sequence through frames 0 .. S+F-1 (the map grows as
+             in the GPU run), only the last F frames timed: the steady-state rate at a grown map, its TicToc
+             stages, the 3-node rate estimated as 1 / the slowest node's mean stage time, and the whole
+             trajectory (for the ATE over S+F frames)
+
+usage: python tests/cpu_baseline.py [--frames N] [--start K] [--box-frames M] [--box-max P] [--late-start S --late-frames F]
 """
 import argparse
 import json
@@ -67,6 +72,29 @@ def _serial(core, start, n, q):
     q.put({"core": core, "frames": n - 1, "seconds": t, "traj": traj,
            "tictoc_ms": {k: round(v / max(nt, 1), 3) for k, v in (tt or {}).items()}})
     del np
+
+
+def _late(core, start, s0, nl, q):
+    """Frames start .. start+s0+nl-1 serially on one pinned core; the last nl timed (steady state)."""
+    _pin(core)
+    o = _oracle()
+    traj, t, tt, nt = [], 0.0, None, 0
+    st = [0.0, 0.0, 0.0]
+    for k in range(s0 + nl):
+        f = _frames(start + k, 1)[0]
+        t1 = time.perf_counter()
+        _, m = o.process_scan(f)
+        dt = time.perf_counter() - t1
+        traj.append([float(v) for v in m["t_w_curr"]])
+        if k >= s0:
+            t += dt
+            d = o.tictoc()
+            tt = {key: (tt[key] if tt else 0.0) + v for key, v in d.items()}
+            sm = o.stage_times()
+            st = [a + b for a, b in zip(st, sm)]
+            nt += 1
+    q.put({"frames": [s0, s0 + nl - 1], "seconds": t, "traj": traj, "stage_ms": [v / max(nt, 1) for v in st],
+           "tictoc_ms": {k: round(v / max(nt, 1), 3) for k, v in (tt or {}).items()}})
 
 
 def _node_scan(core, start, n, out):
@@ -133,6 +161,8 @@ def main():
     ap.add_argument("--start", type=int, default=0)
     ap.add_argument("--box-frames", type=int, default=6)
     ap.add_argument("--box-max", type=int, default=16, help="cores of the box form (the GPU box's CPU share is 16)")
+    ap.add_argument("--late-start", type=int, default=0, help="steady-state window: first timed frame (0 = skip)")
+    ap.add_argument("--late-frames", type=int, default=20)
     args = ap.parse_args()
     cores = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
     model = platform.processor() or ""
@@ -146,6 +176,7 @@ def main():
         pass
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
+    late = None
     p = ctx.Process(target=_serial, args=(cores[0], args.start, args.frames, q))
     p.start()
     ser = q.get(timeout=900)
@@ -160,6 +191,12 @@ def main():
     for b in ps:
         b.join()
     wall = time.perf_counter() - t0
+    if args.late_start > 0:                       # after the other forms: no core shared with them
+        ql = ctx.Queue()
+        pl = ctx.Process(target=_late, args=(cores[0], args.start, args.late_start, args.late_frames, ql))
+        pl.start()
+        late = ql.get(timeout=1800)
+        pl.join()
     box_rate = sum(r["frames"] for r in box) / max(max(r["seconds"] for r in box), 1e-9)
     out = {
         "host": {"cpu_model": model, "nproc": os.cpu_count(), "cores_usable": len(cores), "cores_used": cores[:max(3, P)]},
@@ -170,6 +207,12 @@ def main():
         "box": {"scans_per_s": box_rate, "cores": P, "frames_per_sequence": args.box_frames - 1, "wall_s": round(wall, 2)},
         "traj": ser["traj"],
     }
+    if late is not None:
+        sm = late["stage_ms"]
+        out["late"] = {"frames": late["frames"], "serial_scans_per_s": (late["frames"][1] - late["frames"][0] + 1) / late["seconds"],
+                       "stage_ms": {"scan_registration": sm[0], "odometry": sm[1], "mapping": sm[2]},
+                       "pipelined_est_scans_per_s": 1000.0 / max(sm) if max(sm) > 0 else None,
+                       "tictoc_ms": late["tictoc_ms"], "traj": late["traj"]}
     print(json.dumps(out), flush=True)
 
 

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <random>
 #include <thread>
@@ -113,6 +114,8 @@ static inline int atomicMax(int* p, int v) {
 using std::max;
 using std::min;
 #define PS_HOST_EMU 1
+static std::atomic<long> g_postorder{0};      // ws_heap_postorder hits (coverage of the closed form)
+#define PS_POSTORDER_COUNT g_postorder
 #include "../lidar-visual-odometry_amd/csrc/pcl_sort.hpp"
 #include "../lidar-visual-odometry_amd/csrc/ls_sort.hpp"
 
@@ -190,6 +193,54 @@ static void run_ls_global(std::vector<unsigned long long>& E, int cap) {
     for (auto& x : th) x.join();
 }
 
+// csrc/pcl_sort.hpp's wave heap sort (ws_heap_sort: closed form or six-level pops, early stop) on one
+// emulated wave against libstdc++'s heap sort (std::partial_sort(f, l, l) = make_heap + sort_heap): every
+// >= 3-point key's points in the same order. Mode 4.
+static int heap_trials(int trials, std::mt19937_64& rng) {
+    int bad = 0;
+    for (int t = 0; t < trials; t++) {
+        const int n = 17 + (int)(rng() % 1000);
+        const unsigned kinds = 2 + (unsigned)(rng() % (unsigned)(t % 2 ? n / 3 + 1 : 4 * n));
+        std::vector<unsigned long long> E(n);
+        for (int i = 0; i < n; i++) E[i] = ((unsigned long long)(unsigned)(rng() % kinds) << 32) | (unsigned)i;
+        if (t % 4 == 3) {                         // distinct keys but one group of 3-5 (few relevant points)
+            for (int i = 0; i < n; i++) E[i] = ((unsigned long long)(unsigned)(7 * i + 3) << 32) | (unsigned)i;
+            std::shuffle(E.begin(), E.end(), rng);
+            const int g = 3 + (int)(rng() % 3);
+            const unsigned kg = (unsigned)(E[rng() % n] >> 32);
+            for (int j = 0; j < g; j++) { const int p = (int)(rng() % n); E[p] = ((unsigned long long)kg << 32) | (E[p] & 0xffffffffull); }
+            for (int i = 0; i < n; i++) E[i] = (E[i] & ~0xffffffffull) | (unsigned)i;
+        }
+        if (t % 3 == 2) std::sort(E.begin(), E.begin() + n * 3 / 4);     // mostly ascending input
+        std::vector<unsigned long long> A = E;
+        std::partial_sort(A.begin(), A.end(), A.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
+        std::map<unsigned, int> cnt;
+        for (auto x : E) cnt[(unsigned)(x >> 32)]++;
+        std::vector<unsigned> rel(n / 32 + 2, 0u);
+        for (auto x : E) if (cnt[(unsigned)(x >> 32)] >= 3) { const unsigned i = (unsigned)x & 0xffffu; rel[i >> 5] |= 1u << (i & 31); }
+        g_waves.clear();
+        auto c = std::make_unique<WaveCtx>();
+        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        g_waves.push_back(std::move(c));
+        g_block = std::make_unique<std::barrier<>>(WAVE);
+        std::vector<std::thread> th;
+        for (int l = 0; l < WAVE; l++)
+            th.emplace_back([&, l] { threadIdx.x = l; t_lane = l; t_wave = 0; aloam::ws_heap_sort(E.data(), 0, n, rel.data()); });
+        for (auto& x : th) x.join();
+        auto order = [&](const std::vector<unsigned long long>& X) {
+            std::vector<std::pair<unsigned, unsigned>> v;
+            for (auto x : X) if (cnt[(unsigned)(x >> 32)] >= 3) v.push_back({(unsigned)(x >> 32), (unsigned)x & 0xffffu});
+            std::stable_sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.first < b.first; });
+            return v;
+        };
+        std::vector<unsigned long long> B = E, A2 = A;
+        std::sort(B.begin(), B.end());
+        std::sort(A2.begin(), A2.end());
+        if (B != A2 || order(A) != order(E)) { bad++; std::printf("heap mismatch trial %d n %d kinds %u\n", t, n, kinds); }
+    }
+    return bad;
+}
+
 #ifndef NTHREADS
 #define NTHREADS 128
 #endif
@@ -205,6 +256,12 @@ int main(int argc, char** argv) {
     // must equal std::sort's (heap sorts gated / queued / stopped early, other ties free)
     const bool relmode = argc > 5 && atoi(argv[5]) == 1;
     int bad = 0;
+    if (lsm == 4) {
+        bad = heap_trials(trials, rng);
+        std::printf("postorder segments %ld\n", (long)g_postorder.load());
+        std::printf("trials %d mismatches %d\n", trials, bad);
+        return bad != 0;
+    }
     for (int t = 0; t < trials; t++) {
         const bool big = t % 2 == 1;
         int n = big ? 4000 + (int)(rng() % 4000) : 1 + (int)(rng() % 4096);
@@ -271,6 +328,7 @@ int main(int argc, char** argv) {
             std::printf("mismatch trial %d n %d kinds %u mode %d first diff at %d\n", t, n, kinds, lsm, first);
         }
     }
+    std::printf("postorder segments %ld\n", (long)g_postorder.load());
     std::printf("trials %d mismatches %d\n", trials, bad);
     return bad != 0;
 }

@@ -64,3 +64,14 @@ def test_relevance_gated_sort_orders_relevant_leaves_like_libstdcxx(emu, mode, c
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+def test_wave_heap_sort_orders_relevant_keys_like_libstdcxx(emu):
+    # csrc/pcl_sort.hpp ws_heap_sort on one emulated wave vs libstdc++'s heap sort (std::partial_sort(f, l, l)):
+    # random / mostly ascending / distinct-but-one-group inputs up to 1016 points; the post-order closed form
+    # (no relevant point in its danger zone) and the six-level pops with the early stop must both leave every
+    # >= 3-point key's points in libstdc++'s order
+    r = subprocess.run([emu, "120", "53", "4"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
+    assert "postorder segments 0" not in r.stdout
