@@ -5,9 +5,15 @@
 // Replaces the reference's kittiHelper player + the three nodes for offline runs
 // (src/kittiHelper.cpp:25-35,130-151 read the .bin files; the nodes publish /aft_mapped_to_init).
 // Output: one line per scan with the mapped pose as a KITTI 3x4 row-major [R|t] (the format of
-// kittiHelper's ground-truth path), to stdout or -o FILE; a timing summary on stderr.
+// kittiHelper's ground-truth path), to stdout or -o FILE; a timing summary on stderr. Optional:
+//   --map-path FILE   the /aft_mapped_path Path (laserMapping.cpp:866-873): every mapped pose appended,
+//                     one "index tx ty tz qx qy qz qw" line each (TUM layout, the scan index as stamp)
+//   --odom-path FILE  the /laser_odom_path Path (laserOdometry.cpp:598-607), same layout
+//   --hf FILE         /aft_mapped_to_init_high_frec (laserMapping.cpp:218-246): each odometry pose mapped
+//                     through the latest q/t_wmap_wodom (aloam_map_high_freq_pose), same layout
 //
-// usage: aloam_kitti [-l scan_line] [-s stages] [-n max_frames] [-o poses.txt] file0.bin file1.bin ...
+// usage: aloam_kitti [-l scan_line] [-s stages] [-n max_frames] [-o poses.txt] [--map-path F] [--odom-path F]
+//                    [--hf F] file0.bin file1.bin ...
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -38,19 +44,35 @@ static void write_pose(FILE* o, const double q[4], const double t[3]) {
                  R[5], t[1], R[6], R[7], R[8], t[2]);
 }
 
+static void write_tum(FILE* o, long index, const double q[4], const double t[3]) {
+    if (o) std::fprintf(o, "%ld %.9e %.9e %.9e %.12e %.12e %.12e %.12e\n", index, t[0], t[1], t[2], q[0], q[1], q[2], q[3]);
+}
+
+static FILE* open_out(const char* path) {
+    if (!path) return nullptr;
+    FILE* f = std::fopen(path, "w");
+    if (!f) { std::perror(path); std::exit(1); }
+    return f;
+}
+
 int main(int argc, char** argv) {
     int scan_line = 64, stages = 2, max_frames = -1;
     const char* out_path = nullptr;
+    const char *map_path = nullptr, *odom_path = nullptr, *hf_path = nullptr;
     std::vector<const char*> files;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "-l") && i + 1 < argc) scan_line = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "-s") && i + 1 < argc) stages = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "-n") && i + 1 < argc) max_frames = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "-o") && i + 1 < argc) out_path = argv[++i];
+        else if (!std::strcmp(argv[i], "--map-path") && i + 1 < argc) map_path = argv[++i];
+        else if (!std::strcmp(argv[i], "--odom-path") && i + 1 < argc) odom_path = argv[++i];
+        else if (!std::strcmp(argv[i], "--hf") && i + 1 < argc) hf_path = argv[++i];
         else files.push_back(argv[i]);
     }
     if (files.empty()) {
-        std::fprintf(stderr, "usage: %s [-l scan_line] [-s stages] [-n max_frames] [-o poses.txt] scans.bin...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-l scan_line] [-s stages] [-n max_frames] [-o poses.txt] [--map-path F] [--odom-path F] "
+                             "[--hf F] scans.bin...\n", argv[0]);
         return 2;
     }
     if (max_frames >= 0 && (size_t)max_frames < files.size()) files.resize(max_frames);
@@ -63,9 +85,26 @@ int main(int argc, char** argv) {
     }
     FILE* o = out_path ? std::fopen(out_path, "w") : stdout;
     if (!o) { std::perror(out_path); return 1; }
+    FILE *fmap = open_out(map_path), *fodom = open_out(odom_path), *fhf = open_out(hf_path);
+    // the mapping stage's context holds q/t_wmap_wodom (the last context of the pipeline)
+    aloam_ctx* mctx = aloam_pipeline_context(pl, stages >= 2 ? 1 : 0);
     std::vector<float> bufs[2];     // a pushed sweep is read until the next push returns: alternate buffers
     size_t mapped = 0, pushed = 0;
+    long odom_n = 0;
     double busy_s = 0;
+    auto on_odom = [&](const aloam_odom_result& r) {
+        write_tum(fodom, odom_n, r.q_w_curr, r.t_w_curr);
+        if (fhf) {                  // laserMapping's odometry callback: the pose in the map frame right away
+            double q[4], t[3];
+            if (aloam_map_high_freq_pose(mctx, r.q_w_curr, r.t_w_curr, q, t) == ALOAM_OK) write_tum(fhf, odom_n, q, t);
+        }
+        odom_n++;
+    };
+    auto on_map = [&](const aloam_map_result& r) {
+        write_pose(o, r.q_w_curr, r.t_w_curr);
+        write_tum(fmap, (long)mapped, r.q_w_curr, r.t_w_curr);   // the Path grows by one pose per mapped scan
+        mapped++;
+    };
     for (const char* path : files) {
         std::vector<float>& pts = bufs[pushed++ & 1];
         if (!read_bin(path, pts)) {
@@ -82,7 +121,8 @@ int main(int argc, char** argv) {
             std::fprintf(stderr, "%s: rc=%d %s\n", path, rc, aloam_pipeline_last_error(pl));
             return 1;
         }
-        if (have_mp) { write_pose(o, mp.q_w_curr, mp.t_w_curr); mapped++; }
+        if (have_od) on_odom(od);
+        if (have_mp) on_map(mp);
     }
     aloam_odom_result od;
     aloam_map_result mp, mp2;
@@ -92,11 +132,13 @@ int main(int argc, char** argv) {
             std::fprintf(stderr, "flush: %s\n", aloam_pipeline_last_error(pl));
             return 1;
         }
-        if (hm) { write_pose(o, mp.q_w_curr, mp.t_w_curr); mapped++; }
-        if (hm2) { write_pose(o, mp2.q_w_curr, mp2.t_w_curr); mapped++; }
+        if (ho) on_odom(od);
+        if (hm) on_map(mp);
+        if (hm2) on_map(mp2);
         if (!ho && !hm && !hm2) break;
     }
     if (o != stdout) std::fclose(o);
+    for (FILE* f : {fmap, fodom, fhf}) if (f) std::fclose(f);
     aloam_pipeline_destroy(pl);
     std::fprintf(stderr, "aloam_kitti: %zu scans, %zu mapped poses, %.3f ms/scan (incl. .bin upload)\n", files.size(),
                  mapped, 1e3 * busy_s / files.size());

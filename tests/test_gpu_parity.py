@@ -584,14 +584,43 @@ def test_cpp_host_tool_matches_python_host(lvo, tmp_path):
         synth.write_kitti_bin(pth, f)
         paths.append(pth)
     out = str(tmp_path / "poses.txt")
-    subprocess.check_call([exe, "-l", "64", "-o", out] + paths, timeout=120)
+    mpath, opath, hpath = (str(tmp_path / n) for n in ("map_path.txt", "odom_path.txt", "hf.txt"))
+    subprocess.check_call([exe, "-l", "64", "-o", out, "--map-path", mpath, "--odom-path", opath, "--hf", hpath] + paths,
+                          timeout=120)
     poses = np.loadtxt(out).reshape(-1, 3, 4)
     ctx = lvo.Context(abi.default_params(64))
-    ref = [ctx.process_scan(f)[1] for f in frames]
+    res = [ctx.process_scan(f) for f in frames]
     ctx.close()
+    ref = [m for _, m in res]
     assert len(poses) == len(frames)
     for P, m in zip(poses, ref):
         np.testing.assert_allclose(P[:, 3], m["t_w_curr"], rtol=1e-9, atol=1e-9)
+    # the Paths: one pose appended per mapped / odometry scan (laserMapping.cpp:866-873, laserOdometry.cpp:598-607)
+    mp, op, hf = np.loadtxt(mpath, ndmin=2), np.loadtxt(opath, ndmin=2), np.loadtxt(hpath, ndmin=2)
+    assert mp.shape == (len(frames), 8) and op.shape == (len(frames), 8) and hf.shape == (len(frames), 8)
+    np.testing.assert_array_equal(mp[:, 0], np.arange(len(frames)))
+    for k, (o, m) in enumerate(res):
+        np.testing.assert_allclose(mp[k, 1:4], m["t_w_curr"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(mp[k, 4:8], m["q_w_curr"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(op[k, 1:4], o["t_w_curr"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(op[k, 4:8], o["q_w_curr"], rtol=1e-9, atol=1e-9)
+    # high-frequency poses: each odometry pose through one of the map corrections published so far
+    def through(qm, tm, qo, to):
+        x1, y1, z1, w1 = qm
+        x2, y2, z2, w2 = qo
+        q = np.array([w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2, w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+                      w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2, w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2])
+        u = np.array([x1, y1, z1])
+        v = np.asarray(to, float)
+        t = v + 2.0 * w1 * np.cross(u, v) + 2.0 * np.cross(u, np.cross(u, v))
+        return q, t + np.asarray(tm, float)
+    corrections = [([0.0, 0.0, 0.0, 1.0], [0.0, 0.0, 0.0])] + [(m["q_wmap_wodom"], m["t_wmap_wodom"]) for m in ref]
+    for k, (o, _) in enumerate(res):
+        ok = False
+        for qm, tm in corrections[:k + 1]:
+            q, t = through(qm, tm, o["q_w_curr"], o["t_w_curr"])
+            ok = ok or (np.allclose(hf[k, 4:8], q, rtol=0, atol=1e-9) and np.allclose(hf[k, 1:4], t, rtol=0, atol=1e-9))
+        assert ok, (k, hf[k])
 
 
 def test_cu_mask_contexts_match(gpu_ctx_factory):
