@@ -443,6 +443,8 @@ def main():
             "tictoc_ms": {name: round(float(tictoc[i] / tictoc_n[i]), 4) if tictoc_n[i] else None
                           for i, name in enumerate(lvo.abi.TICTOC_NAMES)},
             "parallelism": f"replicas x{world}",
+            # sorts past the workgroup replay's reach (n > 65,536) that ran the exact one-thread std::sort
+            "serial_sort_fallbacks": lvo.serial_sort_fallbacks(),
             "mode": args.mode + ((" (scanRegistration k+2 || laserOdometry k+1 || laserMapping k, one context/stream each)"
                                   if args.stages == 3 else " (front end k+1 || mapping k, 2 contexts)")
                                  if args.mode == "pipeline" else ""),

@@ -290,6 +290,10 @@ int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);
 /* Restricts the context's streams to a set of CUs (bit i of mask[i / 32] = CU i; nwords = 0 lifts the
  * restriction). Used to give concurrent pipeline stages disjoint CUs. The context must be idle. */
 int aloam_set_cu_mask(aloam_ctx* ctx, const unsigned* mask, int nwords);
+/* Number of VoxelGrid / segment sorts (process-wide, all contexts on the current device) that exceeded
+ * the workgroup replay's reach (n > 65,536) and ran the exact one-thread std::sort instead: correct but
+ * slow, so a workload that reaches it is visible (bench.py reports it). */
+int aloam_serial_sort_fallbacks(unsigned long long* count);
 
 /* ---- native pipeline: the reference's node split on one GPU ---------------------------------
  * scanRegistration, laserOdometry and laserMapping run as three ROS processes in the reference, one

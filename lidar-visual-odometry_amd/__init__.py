@@ -70,6 +70,8 @@ def _declare(L):
     L.aloam_shard_slot_range.argtypes = [C.c_int, C.c_int, C.c_int, I, I]
     L.aloam_set_cu_mask.argtypes = [vp, C.POINTER(C.c_uint), C.c_int]
     L.aloam_set_cu_mask.restype = C.c_int
+    L.aloam_serial_sort_fallbacks.argtypes = [C.POINTER(C.c_ulonglong)]
+    L.aloam_serial_sort_fallbacks.restype = C.c_int
     L.aloam_scan_registration_pc2.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int]
     L.aloam_scan_registration_pc2.restype = C.c_int
     L.aloam_pipeline_create.restype = vp
@@ -125,7 +127,7 @@ EXPORTED_SYMBOLS = [
     "aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features",
     "aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
     "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range",
-    "aloam_scan_registration_pc2", "aloam_set_cu_mask",
+    "aloam_scan_registration_pc2", "aloam_set_cu_mask", "aloam_serial_sort_fallbacks",
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
     "aloam_map_high_freq_pose",
@@ -364,6 +366,15 @@ class Context:
         t = abi.Timing()
         self._check(lib().aloam_get_timing(self.h, C.byref(t)))
         return abi.timing_to_dict(t)
+
+
+def serial_sort_fallbacks():
+    """VoxelGrid / segment sorts that ran the exact one-thread std::sort (n > 65,536), process-wide."""
+    v = C.c_ulonglong(0)
+    rc = lib().aloam_serial_sort_fallbacks(C.byref(v))
+    if rc:
+        raise ALOAMError(f"aloam_serial_sort_fallbacks: {rc}")
+    return int(v.value)
 
 
 def s2m_register_group(contexts, x):

@@ -207,6 +207,12 @@ static void allocate(Ctx& C) {
     rebuild_init(C);                                              // map rebuild's run tables: reset
     grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f, 1, true);     // 5-NN within 1 m, 3x3x3 cells
     grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f, 1, true);
+    // candidate cache of the registration rounds: stack points beyond cap_mq always search the grid
+    C.cap_mq = std::min(C.cap_factors, 1 << 16);
+    C.d_mc_ctr = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_mq);
+    C.d_mc_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_mq * MC_CAP_PTS);
+    C.d_mc_pos = (int*)dalloc(C, sizeof(int) * (size_t)C.cap_mq * MC_CAP_PTS);
+    C.d_mc_prev = (int*)dalloc(C, sizeof(int) * 5 * (size_t)C.cap_mq);
     for (auto& m : C.mset) {
         m.corner = (float4*)dalloc(C, sizeof(float4) * capLS);
         m.surf = (float4*)dalloc(C, sizeof(float4) * N);
@@ -1465,6 +1471,16 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
         C.timing.knn_streamed_bytes = 16.0 * nq + 16.0 * (double)cand[1] + 8.0 * k * (double)nq;
     }
     API_END
+}
+
+int aloam_serial_sort_fallbacks(unsigned long long* count) {
+    if (!count) return ALOAM_E_ARG;
+    try {
+        *count = serial_sort_calls_map() + serial_sort_calls_scan() + serial_sort_calls_voxel();
+        return ALOAM_OK;
+    } catch (...) {
+        return ALOAM_E_HIP;
+    }
 }
 
 int aloam_set_cu_mask(aloam_ctx* ctx, const unsigned* mask, int nwords) {

@@ -379,6 +379,37 @@ __device__ __forceinline__ int thread_knn27(const float ox, const float oy, cons
     }
     return found;
 }
+// merge of a GS-lane group's per-lane sorted top-K lists (bd, bi, bp): K rounds of a group min over
+// 64-bit (d2, index) keys; every lane returns the same result
+template <int K, int GS>
+__device__ __forceinline__ int group_merge_topk(const float* bd, const int* bi, const int* bp, int* out_pos, float* out_d2,
+                                                int* out_idx) {
+    int head = 0, found = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
+#pragma unroll
+        for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
+        const unsigned long long key = hp < 0 ? ~0ull : dist_key(hd, hi);
+        constexpr int NS = GS >= 64 ? 6 : GS >= 32 ? 5 : GS >= 16 ? 4 : GS >= 8 ? 3 : GS >= 4 ? 2 : GS >= 2 ? 1 : 0;
+        const unsigned long long mn = allreduce_u64<NS>(key, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
+        // the owner of the minimum (unique: indices are unique) publishes its position
+        const bool mine = key == mn && mn != ~0ull;
+        int pos = mine ? hp : -1;
+        pos = (int)allreduce_u32<NS>((unsigned)(pos + 1), [](unsigned a, unsigned b) { return a > b ? a : b; }) - 1;
+        if (mine) head++;
+        out_pos[k] = pos;
+        out_d2[k] = mn == ~0ull ? INFINITY : __uint_as_float((unsigned)(mn >> 32));
+        out_idx[k] = mn == ~0ull ? -1 : (int)(mn & 0xffffffffu);
+        found += mn != ~0ull;
+    }
+    return found;
+}
+// Candidate collection riding on a group search (the mapping rounds' per-query cache): every block
+// point within sqrt(r2) of the query is appended (point, grid position) at pts / pos[0, cap), group
+// lanes compacting by ballot; *n ends as the number within, which may exceed cap (then the list is
+// incomplete and must not be used).
+struct KnnCollect { float r2; float4* pts; int* pos; int cap; };
 // Exact radius k-NN of one query by a GROUP of GS aligned lanes (GS | 64) over the 3x3x3 cell
 // block. The 9 row bounds are loaded together (same addresses across the group: one coalesced
 // round trip) into a per-group LDS table tab[20] (row base - prefix, prefix); the rows are
@@ -386,13 +417,14 @@ __device__ __forceinline__ int thread_knn27(const float ox, const float oy, cons
 // only move forward), U loads in flight, and keeps a sorted top-K by (d2, index); K rounds of a
 // group min over 64-bit keys merge the lanes' lists. IDXW: the grid stores each point's original
 // index in w (no second load per candidate). Same total order as the wave / thread versions;
-// every lane returns the same result.
-template <int K, int GS, bool IDXW, int U = 4>
+// every lane returns the same result. COL: also collect the block points within col.r2 (above).
+template <int K, int GS, bool IDXW, int U = 4, bool COL = false>
 __device__ __forceinline__ int group_knn27(const float ox, const float oy, const float oz, const float inv_cell,
                                            const int gdx, const int gdy, const int gdz,
                                            const int* __restrict__ start, const float4* __restrict__ spts,
                                            const int* __restrict__ sidx, float qx, float qy, float qz, float r2, bool active,
-                                           int* out_pos, float* out_d2, int* out_idx, int* ncand, int* tab, int npts) {
+                                           int* out_pos, float* out_d2, int* out_idx, int* ncand, int* tab, int npts,
+                                           const KnnCollect col = KnnCollect{0.f, nullptr, nullptr, 0}, int* ncol = nullptr) {
     const int gl = lane_id() & (GS - 1);
     int total;
     {
@@ -424,6 +456,7 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
 #pragma unroll
     for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
     int row = 0, base = tab[0], nxt = tab[10];
+    int nc = 0;
     for (int t0 = gl; t0 < total; t0 += U * GS) {
         float4 v[U];
         int id[U], ps[U];
@@ -443,6 +476,17 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+            if constexpr (COL) {
+                // lanes still in the loop are exactly the group lanes with candidates left (the group's
+                // lane 0 stays longest, so its count is complete)
+                const bool take = ps[u] >= 0 && d2 < col.r2;
+                const unsigned long long m = __ballot(take);
+                const int gb = lane_id() & ~(GS - 1);
+                const unsigned long long gm = GS == 64 ? m : (m >> gb) & ((1ull << (GS & 63)) - 1);
+                const int slot = nc + __popcll(gm & ((1ull << gl) - 1));
+                if (take && slot < col.cap) { col.pts[slot] = v[u]; col.pos[slot] = ps[u]; }
+                nc += __popcll(gm);
+            }
             if (!(d2 < r2) || d2 > bd[K - 1]) continue;
             const int iu = IDXW ? __float_as_int(v[u].w) : id[u];
             if (d2 < bd[K - 1] || iu < bi[K - 1]) {
@@ -455,27 +499,46 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
             }
         }
     }
-    // merge: K rounds of a group-wide min over the lanes' heads
-    int head = 0, found = 0;
+    if constexpr (COL) { if (ncol) *ncol = nc; }
+    return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
+}
+// The same k-NN over an explicit candidate list (a query's collected block points, w = original
+// index): lane l takes entries l, l + GS, ... (U in flight), same (d2, index) order and radius test,
+// so over any list holding every point within sqrt(r2) of the query it returns group_knn27's result.
+template <int K, int GS, int U>
+__device__ __forceinline__ int group_knn_list(const float4* __restrict__ lpts, const int* __restrict__ lpos, int n, float qx,
+                                              float qy, float qz, float r2, int* out_pos, float* out_d2, int* out_idx) {
+    const int gl = lane_id() & (GS - 1);
+    float bd[K];
+    int bi[K], bp[K];
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        float hd = INFINITY; int hi = 0x7fffffff, hp = -1;
+    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    for (int t0 = gl; t0 < n; t0 += U * GS) {
+        float4 v[U];
+        int ps[U];
 #pragma unroll
-        for (int j = 0; j < K; j++) if (j == head) { hd = bd[j]; hi = bi[j]; hp = bp[j]; }
-        const unsigned long long key = hp < 0 ? ~0ull : dist_key(hd, hi);
-        constexpr int NS = GS >= 64 ? 6 : GS >= 32 ? 5 : GS >= 16 ? 4 : GS >= 8 ? 3 : GS >= 4 ? 2 : GS >= 2 ? 1 : 0;
-        const unsigned long long mn = allreduce_u64<NS>(key, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
-        // the owner of the minimum (unique: indices are unique) publishes its position
-        const bool mine = key == mn && mn != ~0ull;
-        int pos = mine ? hp : -1;
-        pos = (int)allreduce_u32<NS>((unsigned)(pos + 1), [](unsigned a, unsigned b) { return a > b ? a : b; }) - 1;
-        if (mine) head++;
-        out_pos[k] = pos;
-        out_d2[k] = mn == ~0ull ? INFINITY : __uint_as_float((unsigned)(mn >> 32));
-        out_idx[k] = mn == ~0ull ? -1 : (int)(mn & 0xffffffffu);
-        found += mn != ~0ull;
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + u * GS;
+            v[u] = load_or(lpts, t, t < n, make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+            ps[u] = load_or(lpos, t, t < n, -1);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (ps[u] < 0) continue;
+            const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+            if (!(d2 < r2) || d2 > bd[K - 1]) continue;
+            const int iu = __float_as_int(v[u].w);
+            if (d2 < bd[K - 1] || iu < bi[K - 1]) {
+                float nd = d2; int ni = iu, np = ps[u];
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                    if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
+                }
+            }
+        }
     }
-    return found;
+    return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
 }
 // v / k for a point count k in [1, 2^24), correctly rounded like the IEEE division PCL's centroid
 // (Eigen "/= num_pts") does. For |x| in [2^-89, 2^90) or x == 0, v_div_scale / v_div_fmas /

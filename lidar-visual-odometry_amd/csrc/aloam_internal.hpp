@@ -30,6 +30,7 @@ struct ScanMeta {
 };
 
 // ---- dense uniform grid over a point set (kd-tree-free radius search) ----
+constexpr int MC_CAP_PTS = 64;   // cached candidates per mapping query (k_map.hip MC_CAP)
 struct GridDesc {
     unsigned bb[6];                // ordered-encoded bbox: min xyz, max xyz
     float ox, oy, oz, cell, inv_cell;
@@ -241,6 +242,10 @@ struct Ctx {
     KindScratch ksv;                     // stack VoxelGrid scratch of stream3
     int* d_tmp_n = nullptr;              // [2] counts scratch of the utility entry points
     int* d_nbr = nullptr;                                // [queries][5] neighbour slots
+    // mapping rounds' per-query candidate cache (k_map.hip MapCache): centres, points, positions, last neighbours
+    float4* d_mc_ctr = nullptr; float4* d_mc_pts = nullptr; int* d_mc_pos = nullptr; int* d_mc_prev = nullptr;
+    int cap_mq = 0;
+
     int* d_s2m_nbr = nullptr; int cap_s2m_nbr = 0;       // split registration association: parked neighbours
     float4* d_registered = nullptr;
     int n_registered = 0;
@@ -338,6 +343,9 @@ void knn_device_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
                               unsigned long long* cand);
 void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
 void odom_round_search(Ctx& C, int round);
+unsigned long long serial_sort_calls_map();
+unsigned long long serial_sort_calls_scan();
+unsigned long long serial_sort_calls_voxel();
 void rebuild_init(Ctx& C);
 void forward_stacks_pending(Ctx& C, int t);
 void set_counts2(Ctx& C, int* dst, int a, int b);

@@ -419,10 +419,196 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
     }
 }
 
+// The same two-phase search with phase 1 read from LDS: a workgroup takes a tile of 256 / GS consecutive
+// queries (ring order: neighbours along a scan line, a metre or two of arc), loads the fine-grid cells of
+// the union of their 3x3x3 blocks into LDS once — row by row, each (y, z) row of the box one contiguous
+// run of the sorted points — and every group searches its block there (the same candidates in the same
+// cells, so the same (d2, index) result as from global memory). Neighbouring queries share most of their
+// blocks, so the tile reads each cell once instead of once per query, in one burst of coalesced loads
+// instead of one dependent gather per query. A tile whose box exceeds the LDS budget searches phase 1 in
+// global memory as k_knn_2phase does. Phase 2 (the queries phase 1 leaves unsettled) stays global.
+constexpr int KT_MAXC = 768;     // fine cells per tile box
+constexpr int KT_MAXP = 2048;    // points per tile (32 KB)
+constexpr int KT_MAXR = 64;      // (y, z) rows per tile box (one wave scans their lengths)
+struct TileBox { int x0, y0, z0, nx, ny, nz; };
+template <int K, int GS>
+__device__ __forceinline__ int group_knn27_lds(int cx, int cy, int cz, const GridDesc& gd, const TileBox& b, const int* lstart,
+                                               const float4* lpts, float qx, float qy, float qz, float r2, bool active, int* out_pos,
+                                               float* out_d2, int* out_idx, int* ncand, int* tab) {
+    const int gl = lane_id() & (GS - 1);
+    int total;
+    {
+        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gd.dx - 1);
+        int rb[9], pre[10];
+        pre[0] = 0;
+#pragma unroll
+        for (int r = 0; r < 9; r++) {
+            const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
+            const bool ok = active && x0 <= x1 && y >= 0 && y < gd.dy && z >= 0 && z < gd.dz;
+            const int lc = ok ? ((z - b.z0) * b.ny + (y - b.y0)) * b.nx + (x0 - b.x0) : 0;
+            rb[r] = ok ? lstart[lc] : 0;
+            pre[r + 1] = pre[r] + (ok ? lstart[lc + (x1 - x0) + 1] - rb[r] : 0);
+        }
+        total = pre[9];
+        __builtin_amdgcn_wave_barrier();
+        if (gl == 0) {
+#pragma unroll
+            for (int r = 0; r < 9; r++) { tab[r] = rb[r] - pre[r]; tab[10 + r] = pre[r + 1]; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (ncand) *ncand = total;
+    float bd[K];
+    int bi[K], bp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+    int row = 0, base = tab[0], nxt = tab[10];
+    for (int t = gl; t < total; t += GS) {
+        while (t >= nxt && row < 8) { row++; base = tab[row]; nxt = tab[10 + row]; }
+        const int p = base + t;
+        const float4 v = lpts[p];
+        const float d2 = sqdist(v.x, v.y, v.z, qx, qy, qz);
+        if (!(d2 < r2) || d2 > bd[K - 1]) continue;
+        const int iu = __float_as_int(v.w);
+        if (d2 < bd[K - 1] || iu < bi[K - 1]) {
+            float nd = d2; int ni = iu, np = p;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
+            }
+        }
+    }
+    return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
+}
+
+template <int K, int GS, bool CNT>
+__global__ void __launch_bounds__(256) k_knn_tile(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
+                                                  const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
+                                                  const int* __restrict__ cstart, const float4* __restrict__ cpts,
+                                                  const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
+                                                  float* __restrict__ d2, unsigned long long* cand) {
+    constexpr int T = 256 / GS;
+    __shared__ int tabs[T][20];
+    __shared__ int lstart[KT_MAXC + 1];
+    __shared__ int rowg[KT_MAXR], rows0[KT_MAXR], rowoff[KT_MAXR + 1];
+    __shared__ float4 lpts[KT_MAXP];
+    __shared__ int bb[6];
+    __shared__ int tile_ok;
+    const int tid = threadIdx.x;
+    const int qi = blockIdx.x * T + tid / GS;
+    const bool live = qi < nq;
+    const float4 qq = q[live ? qi : 0];
+    const GridDesc gf = *fgd;
+    const int cx = (int)floorf((qq.x - gf.ox) * gf.inv_cell), cy = (int)floorf((qq.y - gf.oy) * gf.inv_cell),
+              cz = (int)floorf((qq.z - gf.oz) * gf.inv_cell);
+    // the tile box: union of the live queries' blocks, clipped to the grid
+    if (tid < 6) bb[tid] = (tid & 1) ? -1 : 0x7fffffff;
+    __syncthreads();
+    {
+        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gf.dx - 1), y0 = max(cy - 1, 0), y1 = min(cy + 1, gf.dy - 1),
+                  z0 = max(cz - 1, 0), z1 = min(cz + 1, gf.dz - 1);
+        if (live && (tid & (GS - 1)) == 0 && x0 <= x1 && y0 <= y1 && z0 <= z1) {
+            atomicMin(&bb[0], x0); atomicMax(&bb[1], x1);
+            atomicMin(&bb[2], y0); atomicMax(&bb[3], y1);
+            atomicMin(&bb[4], z0); atomicMax(&bb[5], z1);
+        }
+    }
+    __syncthreads();
+    TileBox b{bb[0], bb[2], bb[4], bb[1] - bb[0] + 1, bb[3] - bb[2] + 1, bb[5] - bb[4] + 1};
+    const bool any = bb[1] >= 0;
+    const int nrow = any ? b.ny * b.nz : 0, ncell = nrow * (any ? b.nx : 0);
+    bool ok = any && ncell <= KT_MAXC && nrow <= KT_MAXR;
+    if (ok) {
+        // per-cell global starts (lstart, rebased below) and each row's global start
+        for (int j = tid; j < ncell; j += 256) {
+            const int x = j % b.nx, r = j / b.nx, y = b.y0 + r % b.ny, z = b.z0 + r / b.ny;
+            lstart[j] = fstart[(z * gf.dy + y) * gf.dx + b.x0 + x];
+        }
+        if (tid < nrow) {
+            const int y = b.y0 + tid % b.ny, z = b.z0 + tid / b.ny, c = (z * gf.dy + y) * gf.dx + b.x0;
+            rows0[tid] = fstart[c];                     // the row's first point
+            rowg[tid] = fstart[c + b.nx];               // its end (start of the cell after the row)
+        }
+        __syncthreads();
+        if (tid < WAVE) {                               // row lengths -> LDS offsets (one wave, nrow <= 64)
+            const int len = tid < nrow ? rowg[tid] - rows0[tid] : 0;
+            const int inc = wave_incl_scan(len);
+            if (tid < nrow) rowoff[tid + 1] = inc;
+            if (tid == 0) { rowoff[0] = 0; tile_ok = readlane_i(inc, WAVE - 1) <= KT_MAXP; }
+        }
+        __syncthreads();
+        ok = tile_ok != 0;
+        if (ok) {
+            const int P = rowoff[nrow];
+            for (int p = tid; p < P; p += 256) {        // the box's points, row after row
+                int lo = 0, hi = nrow - 1;
+                while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rowoff[mid] <= p) lo = mid; else hi = mid - 1; }
+                lpts[p] = fpts[rows0[lo] + (p - rowoff[lo])];
+            }
+            for (int j = tid; j <= ncell; j += 256) {   // cell starts -> LDS positions (lstart[ncell] = P)
+                const int r = j / b.nx;
+                lstart[j] = j == ncell ? P : rowoff[r] + (lstart[j] - rows0[r]);
+            }
+        }
+    }
+    __syncthreads();
+    int pos[K], oi[K], nf = 0, nc = 0;
+    float od[K];
+    int f;
+    if (ok) f = group_knn27_lds<K, GS>(cx, cy, cz, gf, b, lstart, lpts, qq.x, qq.y, qq.z, r2, live, pos, od, oi, &nf, tabs[tid / GS]);
+    else f = group_knn27<K, GS, true>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, nullptr, qq.x, qq.y, qq.z,
+                                      r2, live, pos, od, oi, &nf, tabs[tid / GS], gf.n);
+    float dk = INFINITY;
+#pragma unroll
+    for (int j = 0; j < K; j++) if (j == k - 1) dk = od[j];
+    const float lim = 0.99f * gf.cell;
+    const bool need = live && !(f >= k && dk < lim * lim);
+    const GridDesc gc = *cgd;
+    if (__any(need)) {
+        int p2[K], i2[K];
+        float e2[K];
+        const int f2 = group_knn27<K, GS, true>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, nullptr,
+                                                qq.x, qq.y, qq.z, r2, need, p2, e2, i2, &nc, tabs[tid / GS], gc.n);
+        if (need) {
+#pragma unroll
+            for (int j = 0; j < K; j++) { od[j] = e2[j]; oi[j] = i2[j]; }
+            f = f2;
+        }
+    }
+    const int gl = lane_id() & (GS - 1);
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if (j < k && j % GS == gl) {
+                idx[(size_t)qi * k + j] = j < f ? oi[j] : -1;
+                d2[(size_t)qi * k + j] = j < f ? od[j] : INFINITY;
+            }
+    }
+    if (CNT) {
+        const int c27 = live && gl == 0 ? (need ? nc : block27_total(gc, cstart, qq.x, qq.y, qq.z)) : 0;
+        const int a = wave_sum_i(c27), s = wave_sum_i(live && gl == 0 ? nf + (need ? nc : 0) : 0);
+        if (lane_id() == 0) {
+            if (a) atomicAdd(&cand[0], (unsigned long long)a);
+            if (s) atomicAdd(&cand[1], (unsigned long long)s);
+        }
+    }
+}
+
 template <int GS>
 static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int nq, int k, float r2, int* idx, float* d2,
                               unsigned long long* cand) {
     const int blocks = (int)(((long long)nq * GS + 255) / 256);
+    static const bool tile = getenv("ALOAM_KNN_TILE") == nullptr || atoi(getenv("ALOAM_KNN_TILE")) != 0;   // A/B knob
+    if (tile) {
+#define KNNT(KK, CN) k_knn_tile<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+        if (k <= 5) { if (cand) KNNT(5, true); else KNNT(5, false); }
+        else { if (cand) KNNT(8, true); else KNNT(8, false); }
+#undef KNNT
+        return;
+    }
     // CNT: the candidate-counting instance (profiling), a separate symbol so kernel traces tell it apart
 #define KNN2(KK, CN) k_knn_2phase<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
     if (k <= 5) { if (cand) KNN2(5, true); else KNN2(5, false); }

@@ -675,18 +675,145 @@ __device__ __forceinline__ bool gather_partials(unsigned long long* buf, unsigne
     return true;
 }
 
+// ---- k_lm_coop's per-pass reduction and exchange ---------------------------------------------------
+// Wave sum of NACC (<= 32) doubles by transposition: five halving steps, each exchanging half of the
+// lane's remaining values with a partner lane and adding the other half (partners l^32 and l^16 by
+// the gfx950 lane swaps, then l^15, l^7, l^2 within rows by DPP), so every step moves half as much as
+// the last; a final l^1 add leaves lane l with the wave sum of value (l >> 1) & 31. The masks
+// {32, 16, 15, 7, 2, 1} span all 64 lanes, so each lane's result sums all of them, in a fixed order.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    int l2, h2;
+    switch (ctrl_sel) {   // the DPP control must be a constant
+        case 0: l2 = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xf, 0xf, false); h2 = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xf, 0xf, false); break;   // row_mirror: l^15
+        case 1: l2 = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xf, 0xf, false); h2 = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xf, 0xf, false); break;   // row_half_mirror: l^7
+        case 2: l2 = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xf, 0xf, false); h2 = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xf, 0xf, false); break;    // quad_perm [2,3,0,1]: l^2
+        default: l2 = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xf, 0xf, false); h2 = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xf, 0xf, false); break;   // quad_perm [1,0,3,2]: l^1
+    }
+    return __hiloint2double(h2, l2);
+}
+template <bool ROW16>
+__device__ __forceinline__ double swap_add(double x, double y) {   // lane-swap step: keep x (low) or y (high) by lane bit
+    const unsigned xl = (unsigned)__double2loint(x), xh = (unsigned)__double2hiint(x);
+    const unsigned yl = (unsigned)__double2loint(y), yh = (unsigned)__double2hiint(y);
+    const auto a = ROW16 ? __builtin_amdgcn_permlane16_swap(xl, yl, false, false) : __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+    const auto b = ROW16 ? __builtin_amdgcn_permlane16_swap(xh, yh, false, false) : __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+__device__ __forceinline__ double wave_transpose_sum(const double* acc) {
+    double v[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) v[j] = j < NACC ? acc[j] : 0.0;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = swap_add<false>(v[j], v[j + 16]);   // bit 5
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = swap_add<true>(v[j], v[j + 8]);      // bit 4
+#pragma unroll
+    for (int s = 0; s < 3; s++) {                                           // bits 3, 2, 1: partners l^15, l^7, l^2
+        const int half = 4 >> s;
+        const bool hi = (lane >> (3 - s)) & 1;
+#pragma unroll
+        for (int j = 0; j < half; j++) {
+            const double send = hi ? v[j] : v[j + half], keep = hi ? v[j + half] : v[j];
+            v[j] = keep + dpp_f64(send, s);
+        }
+    }
+    return v[0] + dpp_f64(v[0], 3);
+}
+// splitmix64 finaliser: record words carry a keyed hash so a reader can tell a complete current record
+// from a stale or partly written one without a separate tag (no store ordering to wait for)
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ unsigned long long word_key(unsigned long long w, int i, unsigned long long epoch) {
+    return mix64(w ^ (epoch * 0x9e3779b97f4a7c15ull) ^ ((unsigned long long)(i + 1) * 0xd1b54a32d192ed03ull));
+}
+__device__ __forceinline__ unsigned long long xor32_lanes(unsigned long long v) {   // XOR over each aligned 32-lane half
+    auto step = [](unsigned long long x, int sel) {
+        const double d = __longlong_as_double((long long)x);
+        return x ^ (unsigned long long)__double_as_longlong(dpp_f64(d, sel));
+    };
+    {
+        const unsigned l = (unsigned)v, h = (unsigned)(v >> 32);
+        const auto a = __builtin_amdgcn_permlane16_swap(l, l, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+        v = ((unsigned long long)b[0] << 32 | a[0]) ^ ((unsigned long long)b[1] << 32 | a[1]);   // l ^ (l^16)
+    }
+    v = step(v, 0);   // l^15
+    v = step(v, 1);   // l^7
+    v = step(v, 2);   // l^2
+    return step(v, 3);   // l^1
+}
+// Workgroup partial -> record (tot[0..NACC) in wsum[0..NACC) after the wave sums), then the all-gather
+// of the G records into rows[b * NACC + i]. Record b = NACC words (the doubles' bits) + one check word
+// (XOR of the words' keyed hashes); readers load every record with a 32-lane half each and accept it
+// when the hashes of what they read XOR to zero. A stale record (another epoch) or one whose stores
+// are still landing fails the check (up to 2^-64). Stores and loads are agent-scope relaxed atomics
+// (64-bit single-copy atomic, coherent across XCDs); no fence, no completion wait before a tag.
+constexpr int LM_COOP_MAX_RECS = 128;   // records per pass buffer (k_lm_coop's workgroup cap)
+__device__ __forceinline__ void publish_record(unsigned long long* buf, unsigned long long epoch, double v) {
+    const int lane = threadIdx.x & 63;   // wave 0 only; lane i < NACC holds partial i
+    const unsigned long long w = lane < NACC ? (unsigned long long)__double_as_longlong(v) : 0ull;
+    const unsigned long long chk = xor32_lanes(lane < NACC ? word_key(w, lane, epoch) : 0ull);
+    unsigned long long* mine = buf + (size_t)blockIdx.x * LM_REC;
+    if (lane < NACC) __hip_atomic_store(&mine[lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (lane == NACC) __hip_atomic_store(&mine[lane], chk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int NT>
+__device__ __forceinline__ bool gather_records(const unsigned long long* buf, unsigned long long epoch, double* rows, unsigned G, int* err) {
+    constexpr int HALVES = NT / 32, MAXK = (LM_COOP_MAX_RECS + HALVES - 1) / HALVES;
+    const int lane32 = threadIdx.x & 31, half = threadIdx.x >> 5;
+    const int K = ((int)G + HALVES - 1) / HALVES;   // block-uniform
+    int spins = 0;
+    while (true) {
+        unsigned long long w[MAXK];
+#pragma unroll
+        for (int k = 0; k < MAXK; k++) {
+            const int b = half + k * HALVES;
+            w[k] = (k < K && b < (int)G && lane32 <= NACC)
+                       ? __hip_atomic_load(&buf[(size_t)b * LM_REC + lane32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < MAXK; k++) {
+            if (k >= K) continue;   // block-uniform
+            const bool rec = half + k * HALVES < (int)G;
+            const unsigned long long h = !rec ? 0ull : lane32 < NACC ? word_key(w[k], lane32, epoch) : (lane32 == NACC ? w[k] : 0ull);
+            bad |= xor32_lanes(h) != 0ull;
+        }
+        if (!__syncthreads_or(bad)) {
+#pragma unroll
+            for (int k = 0; k < MAXK; k++) {
+                const int b = half + k * HALVES;
+                if (k < K && b < (int)G && lane32 < NACC) rows[b * NACC + lane32] = __longlong_as_double((long long)w[k]);
+            }
+            __syncthreads();
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 20)) {   // uniform: every thread counts the same votes
+            if (threadIdx.x == 0) atomicExch(err, 1);
+            return false;
+        }
+    }
+}
+
 // Whole Solve as ONE persistent launch over G workgroups: each pass evaluates its slice, publishes
 // a 29-double partial, meets the others at a grid barrier, then EVERY workgroup reduces the G
 // partials in the same fixed order and runs the identical LM tail on its own LDS copy of the state
 // (bitwise-identical on all workgroups, so no broadcast and one barrier per pass).
 constexpr int CB = 256;
-constexpr int LM_COOP_MAX = 128;                   // records per pass buffer (gather_partials polls 2 per lane)
+constexpr int LM_COOP_MAX = LM_COOP_MAX_RECS;      // records per pass buffer
 constexpr int LM_CACHE = 1024;                      // factor slots per workgroup kept in LDS (80 KB)
 #ifdef ALOAM_LM_TIMING
 __device__ unsigned long long g_lm_ts[8][5];   // micro-benchmark only: block-0 phase stamps per pass
-#define LM_TS(p, k) do { if (blockIdx.x == 0 && threadIdx.x == 0 && (p) < 8) g_lm_ts[p][k] = wall_clock64(); } while (0)
+// (ALOAM_LM_TIMING = the solve index stamped: lm_run flags that launch in max_iter's bit 16)
+#define LM_TS(p, k) do { if (lm_stamp && blockIdx.x == 0 && threadIdx.x == 0 && (p) < 8) g_lm_ts[p][k] = wall_clock64(); } while (0)
 __device__ unsigned long long g_lm_ts_edge[2];   // kernel entry / exit of block 0
-#define LM_TS_EDGE(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_lm_ts_edge[k] = wall_clock64(); } while (0)
+#define LM_TS_EDGE(k) do { if (lm_stamp && blockIdx.x == 0 && threadIdx.x == 0) g_lm_ts_edge[k] = wall_clock64(); } while (0)
 extern "C" int aloam_dbg_lm_ts(unsigned long long* out) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lm_ts), sizeof(g_lm_ts));
     if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 40, HIP_SYMBOL(g_lm_ts_edge), sizeof(g_lm_ts_edge));
@@ -702,10 +829,15 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
     __shared__ double rows[(CB / 4 > LM_COOP_MAX ? CB / 4 : LM_COOP_MAX) * NACC];   // wave-folded rows, then the G records
     __shared__ double part8[8 * NACC];
     __shared__ double tot[NACC];
+    __shared__ double wsum[CB / WAVE * NACC];
     __shared__ double xl[7];
     __shared__ int done;
     __shared__ LMState ls;
     extern __shared__ aloam_factor fcache[];        // this workgroup's contiguous slice of factor slots
+#ifdef ALOAM_LM_TIMING
+    const bool lm_stamp = (max_iter >> 16) & 1;
+    max_iter &= 0xffff;
+#endif
     LM_TS_EDGE(0);
     if (gate && *gate == 0) return;                 // mapping skipped (laserMapping.cpp:554)
     if (dn) nslots = min(nslots, dn[0] + dn[1]);    // live slot count known on the device only
@@ -733,10 +865,25 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
             for (int i = threadIdx.x; i < f1 - f0; i += CB) accumulate(fcache[i], q, t, acc);
         }
         LM_TS(pass, 4);
-        block_reduce_acc<CB>(acc, rows, part8, tot);
+        {   // wave sums -> LDS; wave 0 adds the waves' sums in wave order and publishes the record
+            const double s = wave_transpose_sum(acc);
+            const int lane = threadIdx.x & 63;
+            if (!(lane & 1) && (lane >> 1) < NACC) wsum[(threadIdx.x >> 6) * NACC + (lane >> 1)] = s;
+        }
+        __syncthreads();
+        unsigned long long* rbuf = recs + (size_t)(pass & 1) * LM_COOP_MAX * LM_REC;
+        if (threadIdx.x < WAVE) {
+            double v = 0;
+            if (threadIdx.x < NACC) {
+                v = wsum[threadIdx.x];
+#pragma unroll
+                for (int w = 1; w < CB / WAVE; w++) v += wsum[w * NACC + threadIdx.x];
+            }
+            publish_record(rbuf, epoch0 + pass, v);
+        }
         LM_TS(pass, 0);
-        if (pass > 0 && threadIdx.x == WAVE) lm_post(&ls);   // wave 1, while wave 0 exchanges the partials
-        if (!gather_partials(recs + (size_t)(pass & 1) * LM_COOP_MAX * LM_REC, epoch0 + pass, tot, rows, G, err)) return;
+        if (pass > 0 && threadIdx.x == WAVE) lm_post(&ls);   // wave 1, while the records travel
+        if (!gather_records<CB>(rbuf, epoch0 + pass, rows, G, err)) return;
         LM_TS(pass, 1);
         reduce_rows(rows, G, part8, tot);
         LM_TS(pass, 2);
@@ -782,8 +929,11 @@ void lm_run(Ctx& C, const aloam_factor* d_f, int nslots, double* d_x, int round,
     G = std::max(1, std::min(std::min(gmax, C.n_cus), G));   // every workgroup must be co-resident (<= 1 per CU)
     const int cap = std::min(LM_CACHE, (nslots + G - 1) / G);          // LDS slots per workgroup
     const size_t lds = sizeof(aloam_factor) * (size_t)cap;
-    k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_lm_recs, C.d_lm_seq, C.d_bar_err, out,
-                                      std::min(C.P.max_solver_iterations, 200), gate, d_nslots2, cap);
+    int mi = std::min(C.P.max_solver_iterations, 200);
+#ifdef ALOAM_LM_TIMING
+    if (round == ALOAM_LM_TIMING) mi |= 1 << 16;
+#endif
+    k_lm_coop<<<G, CB, lds, C.stream>>>(d_f, nslots, d_x, C.d_lm, C.d_lm_recs, C.d_lm_seq, C.d_bar_err, out, mi, gate, d_nslots2, cap);
     HIPCHK(hipGetLastError());
 }
 

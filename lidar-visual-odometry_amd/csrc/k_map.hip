@@ -24,9 +24,9 @@
 #include "rvg.hpp"
 
 namespace aloam {
-#ifdef ALOAM_WSTAMP_MAP
+#ifdef ALOAM_WSTAMP_MAP      // k_map_assoc phases of round ALOAM_WSTAMP_MAP (profiling builds only)
 WSTAMP_DEFINE_TABLE
-#define WSTAMP(k) WSTAMP_ON(k)
+#define WSTAMP(k) do { if (wst_round == ALOAM_WSTAMP_MAP) WSTAMP_ON(k); } while (0)
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
@@ -129,7 +129,6 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
             pts[j][0] = v.x; pts[j][1] = v.y; pts[j][2] = v.z;
             cx = cx + pts[j][0]; cy = cy + pts[j][1]; cz = cz + pts[j][2];
         }
-        WSTAMP(6);
         cx = cx / 5.0; cy = cy / 5.0; cz = cz / 5.0;
         double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -157,7 +156,6 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
             A[j * 3] = P[j][0]; A[j * 3 + 1] = P[j][1]; A[j * 3 + 2] = P[j][2];
             b[j] = -1;
         }
-        WSTAMP(6);
         double n[3];
         colpiv_qr_5x3(A, b, n);
         const double negOA = 1 / sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
@@ -183,6 +181,38 @@ __device__ __forceinline__ void fit_factor(bool corner, const float4 po, const f
 constexpr int AG = 8;     // lanes per query of the scan-to-map registration (k_s2m_assoc); k_map_assoc: g_map_ag
 constexpr int ASSOC_BLOCKS = 512;   // fixed launch (graph-replayable); waves stride over the stacks
 constexpr int FIT_BLOCKS = 160;     // k_map_fit: 40960 lanes, one stack point each at C3 sizes
+
+// Per-query candidate cache of the registration rounds. A query's map-frame position moves little
+// between rounds (HDL-64 sequence, micro/round_stats.cpp: p99 7 cm after the first round, 2 cm after
+// the second, < 1 cm later), so the first round's search (and any later full search) also collects
+// the block points within 1 + MC_M of the query: the cache centre c. A later round whose query q has
+// |q - c| <= MC_M - eps and whose 1 m ball lies inside c's 3x3x3 block (the points the collection
+// saw) finds every point within the 1 m search radius in the cache, so the k-NN over the cached
+// list is exactly the grid search's result (same (d2, index) order). Otherwise the query searches
+// the grid again and re-centres its cache. A query whose 5 neighbours (in order) equal the previous
+// round's keeps its factor: the fit reads nothing but those 5 map points and the stack point.
+constexpr int MC_CAP = MC_CAP_PTS;  // cached points per query (p99 45, 1e-4 above 64 at MC_M = 0.1; more => full search)
+constexpr float MC_M = 0.1f;        // reuse radius (m)
+constexpr float MC_EPS = 2e-3f;     // fp32 slack of the distance and cell tests (coordinates << 2^13 m)
+struct MapCache {
+    float4* ctr;     // [cap_q] centre xyz, w = cached count (int bits; -1 = none)
+    float4* pts;     // [cap_q][MC_CAP] cached points (w = original index)
+    int* pos;        // [cap_q][MC_CAP] their grid positions
+    int* prev;       // [cap_q][5] last round's neighbour positions (-1: no factor)
+    int cap_q;       // queries with a cache slot (the rest always search)
+    int round;       // 0: search and collect for every query
+};
+// the 1 m ball (+ eps) around q inside the 3x3x3 cell block of c's cell (cells outside the grid hold no points)
+__device__ __forceinline__ bool ball_in_block(const GridDesc& gd, const float4 c, const float4 q) {
+    auto axis = [&gd](float cv, float qv, float o, int d) {
+        const int cc = (int)floorf((cv - o) * gd.inv_cell);
+        const float lo = cc - 1 <= 0 ? -INFINITY : o + (float)(cc - 1) * gd.cell;
+        const float hi = cc + 2 >= d ? INFINITY : o + (float)(cc + 2) * gd.cell;
+        return qv - (1.0f + MC_EPS) >= lo && qv + (1.0f + MC_EPS) <= hi;
+    };
+    return axis(c.x, q.x, gd.ox, gd.dx) && axis(c.y, q.y, gd.oy, gd.dy) && axis(c.z, q.z, gd.oz, gd.dz);
+}
+
 // slots [s0, s1) of the compact slot space (corner stack at [0, nc), surf stack at [nc, nc + ns) — the
 // reference's AddResidualBlock order), pose `par` (laserMapping.cpp:129 parameters)
 template <int G, int U>
@@ -191,12 +221,13 @@ __device__ __forceinline__ void assoc_slots(
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp, int (*tabs)[20],
-    int* __restrict__ nbr = nullptr) {
+    int* __restrict__ nbr = nullptr, const MapCache* mc = nullptr) {
     const bool lead = (lane_id() & (G - 1)) == 0;
     const int per_wave = WAVE / G;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
     int cnt_c = 0, cnt_s = 0;
     unsigned long long ncand_sum = 0;
+    const int round = mc ? mc->round : 0, wst_round = round;
     for (int base = s0 + wave * per_wave; base < s1; base += nwaves * per_wave) {   // wave-uniform trip count
         const int qi = base + (lane_id() / G);
         const bool live = qi < s1;
@@ -206,26 +237,112 @@ __device__ __forceinline__ void assoc_slots(
         const GridDesc gd = corner ? *gdc : *gds;
         const float4 sel = associate_to_map(par, po);
         const float4* sp = corner ? sp_c : sp_s;
+        const bool slot = mc && live && qi < mc->cap_q;
+        int ncache = -1;
+        bool cached = false;
+        if (slot && round > 0) {
+            const float4 c = mc->ctr[qi];
+            ncache = __float_as_int(c.w);
+            const float ex = sel.x - c.x, ey = sel.y - c.y, ez = sel.z - c.z;
+            cached = ncache >= 0 && ncache <= MC_CAP && ex * ex + ey * ey + ez * ez <= (MC_M - MC_EPS) * (MC_M - MC_EPS) &&
+                     ball_in_block(gd, c, sel);
+        }
         WSTAMP(2);
         int pos[5], idx[5], ncand = 0;
         float d2[5];
         int found = 5;
         if (exp & 1) { for (int k = 0; k < 5; k++) pos[k] = (li * 7 + k) % 64; }
-        else found = group_knn27<5, G, true, U>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
-                                                 corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, live, pos, d2, idx, &ncand,
-                                                 tabs[threadIdx.x / G], gd.n);
+        else {
+            found = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) pos[k] = -1;
+            const bool search = live && !cached;
+            if (mc && round > 0) {
+                // the few queries that left their cache: a whole wave per query (its latency bounds the
+                // launch: one group's search over a dense block streams hundreds of candidates per lane group)
+                unsigned long long todo = __ballot(search && lead);
+                while (todo) {
+                    const int src = __ffsll((long long)todo) - 1;
+                    todo &= todo - 1;
+                    const int q = __shfl(qi, src);
+                    const bool qc = __shfl((int)corner, src) != 0, qslot = __shfl((int)slot, src) != 0;
+                    const float qx = __shfl(sel.x, src), qy = __shfl(sel.y, src), qz = __shfl(sel.z, src);
+                    const GridDesc& g = qc ? *gdc : *gds;
+                    const KnnCollect col{(1.0f + MC_M) * (1.0f + MC_M), mc->pts + (size_t)q * MC_CAP, mc->pos + (size_t)q * MC_CAP,
+                                         qslot ? MC_CAP : 0};
+                    int p2[5], i2[5], ncol = 0;
+                    float e2[5];
+                    const int f2 = group_knn27<5, WAVE, true, 8, true>(g.ox, g.oy, g.oz, g.inv_cell, g.dx, g.dy, g.dz, qc ? cs_c : cs_s,
+                                                                       qc ? sp_c : sp_s, qc ? si_c : si_s, qx, qy, qz, 1.0f, true, p2,
+                                                                       e2, i2, nullptr, tabs[(threadIdx.x & ~(WAVE - 1)) / G], g.n,
+                                                                       col, &ncol);
+                    if (lane_id() == 0 && qslot) mc->ctr[q] = make_float4(qx, qy, qz, __int_as_float(ncol <= MC_CAP ? ncol : -1));
+                    if (lane_id() / G == src / G) {
+#pragma unroll
+                        for (int k = 0; k < 5; k++) pos[k] = p2[k];
+                        found = f2;
+                    }
+                }
+            } else if (__any(search)) {
+                if (mc) {   // search + collect: (re)centre the cache at this round's position
+                    const KnnCollect col{(1.0f + MC_M) * (1.0f + MC_M), mc->pts + (size_t)qi * MC_CAP, mc->pos + (size_t)qi * MC_CAP,
+                                         slot ? MC_CAP : 0};
+                    int ncol = 0;
+                    found = group_knn27<5, G, true, U, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz,
+                                                             corner ? cs_c : cs_s, sp, corner ? si_c : si_s, sel.x, sel.y, sel.z,
+                                                             1.0f, search, pos, d2, idx, &ncand, tabs[threadIdx.x / G], gd.n,
+                                                             col, &ncol);
+                    if (search && slot && lead) mc->ctr[qi] = make_float4(sel.x, sel.y, sel.z, __int_as_float(ncol <= MC_CAP ? ncol : -1));
+                } else {
+                    found = group_knn27<5, G, true, U>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
+                                                       corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, search, pos, d2, idx, &ncand,
+                                                       tabs[threadIdx.x / G], gd.n);
+                }
+            }
+            WSTAMP(6);
+            if (__any(cached)) {
+                int p2[5], i2[5];
+                float e2[5];
+                const size_t cb = cached ? (size_t)qi * MC_CAP : 0;
+                const int f2 = group_knn_list<5, G, (MC_CAP + G - 1) / G>(mc->pts + cb, mc->pos + cb, cached ? ncache : 0, sel.x,
+                                                                          sel.y, sel.z, 1.0f, p2, e2, i2);
+                if (cached) {
+#pragma unroll
+                    for (int k = 0; k < 5; k++) pos[k] = p2[k];
+                    found = f2;
+                }
+            }
+        }
         WSTAMP(3);
         if (live && lead) {
+            const bool use = found == 5 && !(exp & 2);
             if (nbr) {   // neighbours only: k_map_fit fits them one query per lane
 #pragma unroll
-                for (int k = 0; k < 5; k++) nbr[(size_t)qi * 5 + k] = (found == 5 && !(exp & 2)) ? pos[k] : -1;
+                for (int k = 0; k < 5; k++) nbr[(size_t)qi * 5 + k] = use ? pos[k] : -1;
             } else {
-                aloam_factor f;
-                f.type = -1; f.pad = 0;
-                if (found == 5 && !(exp & 2)) fit_factor(corner, po, sp, pos, f);
-                WSTAMP(7);
-                out[qi] = f;
-                if (f.type >= 0) { if (corner) cnt_c++; else cnt_s++; }
+                // unchanged neighbours since the last round: the factor in out[qi] is this round's
+                bool same = false;
+                if (slot) {
+                    int* pv = mc->prev + (size_t)qi * 5;
+                    same = round > 0;
+#pragma unroll
+                    for (int k = 0; k < 5; k++) same = same && pv[k] == (use ? pos[k] : -1);
+                    if (!same)
+#pragma unroll
+                        for (int k = 0; k < 5; k++) pv[k] = use ? pos[k] : -1;
+                }
+                int type;
+                if (same) {
+                    type = out[qi].type;
+                } else {
+                    aloam_factor f;
+                    f.type = -1; f.pad = 0;
+                    if (use) fit_factor(corner, po, sp, pos, f);
+                    WSTAMP(7);
+                    out[qi] = f;
+                    type = f.type;
+                }
+                if (type >= 0) { if (corner) cnt_c++; else cnt_s++; }
             }
             ncand_sum += ncand;
         }
@@ -254,8 +371,9 @@ __global__ void __launch_bounds__(256) k_map_assoc(
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     const MapState* __restrict__ m, aloam_factor* __restrict__ out, int* round_cnt, int* __restrict__ nbr,
-    unsigned long long* cand_count, int exp) {
+    unsigned long long* cand_count, int exp, const MapCache mc) {
     __shared__ int tabs[256 / G][20];
+    const int wst_round = mc.round;
     WSTAMP(0);
     // the solver reads nc + ns from the device
     if (!m->optimize) return;
@@ -265,7 +383,7 @@ __global__ void __launch_bounds__(256) k_map_assoc(
     for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
     WSTAMP(1);
     assoc_slots<G, U>(cstack, sstack, nc, 0, nc + ns, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, round_cnt,
-                      cand_count, exp, tabs, nbr);
+                      cand_count, exp, tabs, nbr, mc.ctr ? &mc : nullptr);
     WSTAMP(5);
 }
 
@@ -1181,6 +1299,7 @@ static const int g_assoc_blocks = getenv("ALOAM_ASSOC_BLOCKS") ? atoi(getenv("AL
 static const int g_fit_split = getenv("ALOAM_FIT_SPLIT") ? atoi(getenv("ALOAM_FIT_SPLIT")) : 0;   // tuning knob
 static const int g_map_ag = getenv("ALOAM_MAP_AG") ? atoi(getenv("ALOAM_MAP_AG")) : 8;   // tuning knob: lanes per query (C3, serial on 256 CUs: 8 / 16 / 32 = 25.5 / 19.9 / 29.0 us; pipeline on 128 CUs: 8 / 16 = 22.2 / 24.6 us)
 static const int g_map_u = getenv("ALOAM_MAP_U") ? atoi(getenv("ALOAM_MAP_U")) : 4;     // tuning knob: loads in flight
+static const bool g_map_cache = getenv("ALOAM_MAP_NOCACHE") == nullptr;   // A/B knob: the rounds' candidate cache
 __global__ void k_noop() {}
 // ALOAM_MAP_PHASES (profiling aid): GPU time of the frame's phases from events on the frame's stream,
 // read back two frames later (that frame is complete by then), means printed every 200 frames
@@ -1255,11 +1374,12 @@ void map_frame_launch(Ctx& C, int X) {
                 auto kern = g_map_ag == 16 ? (g_map_u == 8 ? k_map_assoc<16, 8> : k_map_assoc<16, 4>)
                           : g_map_ag == 32 ? (g_map_u == 8 ? k_map_assoc<32, 8> : k_map_assoc<32, 4>)
                                            : (g_map_u == 8 ? k_map_assoc<8, 8> : k_map_assoc<8, 4>);
+                const MapCache mc{g_map_cache ? C.d_mc_ctr : nullptr, C.d_mc_pts, C.d_mc_pos, C.d_mc_prev, C.cap_mq, it};
                 kern<<<g_assoc_blocks, 256, 0, st>>>(
                     in.cstack, in.sstack, stack_n,
                     C.g_map_corner.desc, C.g_map_corner.cell_start, C.g_map_corner.pts, C.g_map_corner.idx,
                     C.g_map_surf.desc, C.g_map_surf.cell_start, C.g_map_surf.pts, C.g_map_surf.idx, C.d_map, C.d_factors, cnt,
-                    g_fit_split ? C.d_nbr : nullptr, C.profiling ? C.d_cand : nullptr, g_exp);
+                    g_fit_split ? C.d_nbr : nullptr, C.profiling ? C.d_cand : nullptr, g_exp, mc);
                 if (g_fit_split)
                     k_map_fit<<<FIT_BLOCKS, 256, 0, st>>>(in.cstack, in.sstack, stack_n, C.g_map_corner.pts, C.g_map_surf.pts, C.d_map,
                                                          C.d_nbr, C.d_factors, cnt);
@@ -1286,6 +1406,13 @@ void map_frame_launch(Ctx& C, int X) {
         k_map_register<<<(in.nf + MB - 1) / MB, MB, 0, st>>>(in.full, in.nf, C.d_map, C.d_registered);
     if (g_map_phases) map_phase(C, 4);
     HIPCHK(hipGetLastError());
+}
+
+// ps_serial_std_sort calls of this translation unit's kernels (aloam_serial_sort_fallbacks)
+unsigned long long serial_sort_calls_map() {
+    unsigned long long v = 0;
+    HIPCHK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ps_serial_calls), sizeof(v)));
+    return v;
 }
 
 }  // namespace aloam

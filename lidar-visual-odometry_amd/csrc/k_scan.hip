@@ -984,4 +984,11 @@ void scan_registration_launch(Ctx& C, const float4* in, int n, bool side) {
     HIPCHK(hipGetLastError());
 }
 
+// ps_serial_std_sort calls of this translation unit's kernels (aloam_serial_sort_fallbacks)
+unsigned long long serial_sort_calls_scan() {
+    unsigned long long v = 0;
+    HIPCHK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ps_serial_calls), sizeof(v)));
+    return v;
+}
+
 }  // namespace aloam

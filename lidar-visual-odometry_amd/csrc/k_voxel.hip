@@ -248,4 +248,11 @@ void voxel_grid_sorted(Ctx& C, const float4* pts, const int* d_n, int cap_n, flo
     voxel_grid_sorted_on(C, lane ? C.stream2 : C.stream, C.ks[lane], pts, d_n, cap_n, leaf, out, d_nout);
 }
 
+// ps_serial_std_sort calls of this translation unit's kernels (aloam_serial_sort_fallbacks)
+unsigned long long serial_sort_calls_voxel() {
+    unsigned long long v = 0;
+    HIPCHK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ps_serial_calls), sizeof(v)));
+    return v;
+}
+
 }  // namespace aloam

@@ -241,6 +241,74 @@ __device__ inline void ws_sift(unsigned long long* H, const int hl, const unsign
         h = ((h + 1) << 6) - 1 + (r - 63);      // the hole went six levels down
     }
 }
+// The pops of __sort_heap on a heap in LDS. A wave's LDS operations complete in issue order, so no pop waits
+// for its stores: the next pop's loads see them. Per pop: the root is carried in registers (the previous
+// pop's new root), the re-inserted value H[hl] rides on lane 63 of the first six-level load, the popped
+// root goes straight to its final slot, then ws_sift's six-level steps without the store waits. The
+// result is std::__sort_heap's array (first npop pops).
+__device__ inline bool ps_in_lds(const void* p) {
+#if defined(PS_HOST_EMU)
+    (void)p;
+    return true;
+#elif defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p);
+#else
+    (void)p;
+    return false;
+#endif
+}
+__device__ inline void ws_sort_heap_lds(unsigned long long* H, const int len, const int npop) {
+    const int lane = lane_id();
+    const int dr = 31 - __builtin_clz((unsigned)(lane + 1));   // depth of subtree node `lane` (lane 63: the value)
+    const int o = lane + 1 - (1 << dr);
+    unsigned long long top = H[0];
+    for (int i = 0; i < npop; i++) {
+        const int hl = len - 1 - i;
+        unsigned long long v = 0ull;
+        unsigned vk = 0u;
+        int h = 0;
+        for (bool first = true;; first = false) {
+            int a = 0;
+            bool has = false, right = false;
+            unsigned long long e1 = 0ull, e2 = 0ull, vv = 0ull;
+            if (lane < 63) {
+                a = ((h + 1) << dr) - 1 + o;
+                const int c1 = 2 * a + 1;
+                if (c1 < hl) {
+                    has = true;
+                    e1 = H[c1];
+                    if (c1 + 1 < hl) { e2 = H[c1 + 1]; right = !(ps_key(e2) < ps_key(e1)); }
+                }
+            } else if (first) {
+                vv = H[hl];
+            }
+            if (first) {
+                v = ps_rl64(vv, 63);
+                vk = ps_key(v);
+                if (lane == 0) H[hl] = top;                 // after the load of H[hl] (issue order)
+            }
+            const unsigned long long w = right ? e2 : e1;
+            const bool go = has && ps_key(w) >= vk;
+            const unsigned long long mgo = __ballot(go), mr = __ballot(right);
+            int r = 0, steps = 0;
+            unsigned long long pm = 0ull;
+            while (steps < 6 && ((mgo >> r) & 1ull)) {
+                pm |= 1ull << r;
+                r = 2 * r + 1 + (int)((mr >> r) & 1ull);
+                steps++;
+            }
+            if ((pm >> lane) & 1ull) H[a] = w;
+            if (first) top = (mgo & 1ull) ? ps_rl64(w, 0) : v;   // the new root
+            if (steps < 6) {                                 // v fills the hole at subtree node r
+                const int ar = readlane_i(a, r);
+                if (lane == 0) H[ar] = v;
+                break;
+            }
+            h = ((h + 1) << 6) - 1 + (r - 63);               // the hole went six levels down
+        }
+        ps_wsync<false>();
+    }
+}
 // std::__partial_sort(E + f, E + l, E + l) (= __make_heap + __sort_heap) by one wave, E in LDS or global.
 // __make_heap adjusts the parents (len - 2) / 2 .. 0 in turn; parents of one depth have disjoint subtrees,
 // so each depth runs on the lanes at once, deepest first. With rel (rvg.hpp), only the order of the
@@ -344,6 +412,7 @@ __device__ inline void ws_heap_sort(unsigned long long* E, const int f, const in
         c = wave_sum_i(c);
         npop = ps_u(min(len - 1, c));
     }
+    const bool lds = ps_in_lds(H);
     const int P = (len - 2) / 2;
     const int D = 31 - __builtin_clz((unsigned)(P + 1));
     for (int d = D; d >= 0; d--) {
@@ -352,9 +421,13 @@ __device__ inline void ws_heap_sort(unsigned long long* E, const int f, const in
             const int node = base + lane;
             if (node <= a1) ps_adjust_heap(H, node, len, H[node]);
         }
-        ps_wsync<true>();
+        if (lds) ps_wsync<false>(); else ps_wsync<true>();
     }
     if (rel && len <= 16 * WAVE && ws_heap_postorder(H, len, npop, rel)) return;
+    if (lds) {
+        ws_sort_heap_lds(H, len, npop);
+        return;
+    }
     for (int i = 0; i < npop; i++) {
         const int hl = len - 1 - i;
         const unsigned long long v = H[hl], top = H[0];
@@ -444,7 +517,15 @@ __device__ inline bool ws_order_matters(const unsigned long long* E, int f, int 
 // The whole std::sort by one thread (arrays beyond NT * PS_MAX_CHUNK elements): introsort_loop with an
 // explicit stack (the right part is pushed, the left continued — disjoint ranges, same result), then
 // __final_insertion_sort.
+// Every call is counted (this translation unit's copy of the counter; aloam_serial_sort_fallbacks sums
+// them): the one-thread sort is exact but slow, and a workload that reaches it should show.
+#ifndef PS_HOST_EMU
+static __device__ unsigned long long g_ps_serial_calls;
+#endif
 __device__ __noinline__ void ps_serial_std_sort(unsigned long long* E, int n) {
+#ifndef PS_HOST_EMU
+    atomicAdd(&g_ps_serial_calls, 1ull);
+#endif
     if (n <= 1) return;
     int sf[64], sl[64], sd[64], sp = 0;
     sf[0] = 0; sl[0] = n; sd[0] = 2 * (31 - __builtin_clz((unsigned)n)); sp = 1;

@@ -58,10 +58,121 @@ __device__ __forceinline__ void rvg_positions(const unsigned long long* E, const
 // to 16 by a register sorting network, more by repeated selection). fpos == null: S is PCL's order itself
 // (every leaf summed in S order; payloads are then full 32-bit point indices). sc: 2 (NT / 64) + 2 ints of
 // LDS.
+// One relevant leaf S[q, e) (len >= 3) summed in fpos order.
+template <typename PtF>
+__device__ __forceinline__ float4 rvg_rel_sum(const unsigned long long* S, const int q, const int e, const int* fpos, PtF pt) {
+    const int len = e - q;
+    float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto add = [&](unsigned i) {
+        const float4 v = pt((int)i);
+        cc.x += v.x; cc.y += v.y; cc.z += v.z; cc.w += v.w;
+    };
+    if (len <= 16) {
+        unsigned v[16];                  // (position << 16) | point, sorted ascending = position order
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const unsigned i = u < len ? ((unsigned)S[q + u] & 0xffffu) : 0u;
+            v[u] = u < len ? (((unsigned)fpos[i] << 16) | i) : 0xffffffffu;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {   // odd-even transposition network
+#pragma unroll
+            for (int u = r & 1; u + 1 < 16; u += 2) {
+                const unsigned a = v[u], b = v[u + 1];
+                v[u] = a < b ? a : b;
+                v[u + 1] = a < b ? b : a;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (u < len) add(v[u] & 0xffffu);
+    } else {
+        int last = -1;
+        for (int m = 0; m < len; m++) {
+            int best = 0x7fffffff;
+            unsigned bi = 0;
+            for (int t = q; t < e; t++) {
+                const unsigned i = (unsigned)S[t] & 0xffffu;
+                const int fp = fpos[i];
+                if (fp > last && fp < best) { best = fp; bi = i; }
+            }
+            add(bi);
+            last = best;
+        }
+    }
+    return cc;
+}
+
+// The same leaf sums with the thread's chunk read in batches of RB entries: the batch's S entries and
+// their points are loaded together (independent loads in flight) and the leaves summed from registers
+// in S order; a relevant leaf (rel bit at its head, its points then in fpos order) and a leaf running
+// past the chunk take the per-leaf path. Same sums in the same order as rvg_reduce's loop.
+template <int NT, int RB, typename PtF, typename OutF>
+__device__ __forceinline__ int rvg_reduce_batched(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos,
+                                                  PtF pt, OutF out, int* sc) {
+    const int C = (n + NT - 1) / NT;
+    const int q0 = min(n, (int)threadIdx.x * C), q1 = min(n, q0 + C);
+    int nh = 0;
+    for (int qb = q0; qb < q1; qb += RB) {
+        unsigned k[RB];
+        const unsigned kp = qb > 0 ? ps_key(S[qb - 1]) : 0u;
+#pragma unroll
+        for (int j = 0; j < RB; j++) k[j] = qb + j < q1 ? ps_key(S[qb + j]) : 0u;
+#pragma unroll
+        for (int j = 0; j < RB; j++)
+            if (qb + j < q1) nh += (qb + j == 0 || k[j] != (j ? k[j - 1] : kp));
+    }
+    int run = nh, dummy = 0, tot, td;
+    ps_exscan2<NT>(run, dummy, sc, tot, td);
+    // the open leaf: its head, whether it is summed here (a <= 2-point leaf) and the sum so far
+    int head = -1;
+    bool plain = false;
+    float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto close = [&](int e) {            // the open leaf ends at e
+        const int len = e - head;
+        if (!plain) cc = rvg_rel_sum(S, head, e, fpos, pt);
+        out(run, div4_by_count(cc, len));
+        run++;
+    };
+    for (int qb = q0; qb < q1; qb += RB) {
+        unsigned long long s[RB];
+        float4 v[RB];
+        const unsigned kp = qb > 0 ? ps_key(S[qb - 1]) : 0u;
+#pragma unroll
+        for (int j = 0; j < RB; j++) s[j] = qb + j < q1 ? S[qb + j] : 0ull;
+#pragma unroll
+        for (int j = 0; j < RB; j++) v[j] = qb + j < q1 ? pt((int)((unsigned)s[j] & 0xffffu)) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < RB; j++) {
+            const int q = qb + j;
+            if (q >= q1) continue;
+            const unsigned kj = ps_key(s[j]);
+            if (q == 0 || kj != (j ? ps_key(s[j - 1]) : kp)) {   // a leaf starts at q
+                if (head >= 0) close(q);
+                head = q;
+                plain = !rvg_is_rel(rel, (unsigned)s[j] & 0xffffu);
+                cc = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            if (head >= 0 && plain) { cc.x += v[j].x; cc.y += v[j].y; cc.z += v[j].z; cc.w += v[j].w; }
+        }
+    }
+    if (head >= 0) {                     // the last leaf may run into the next chunk
+        int e = q1;
+        const unsigned kh = ps_key(S[head]);
+        while (e < n && ps_key(S[e]) == kh) {
+            if (plain) { const float4 w = pt((int)((unsigned)S[e] & 0xffffu)); cc.x += w.x; cc.y += w.y; cc.z += w.z; cc.w += w.w; }
+            e++;
+        }
+        close(e);
+    }
+    return tot;
+}
+
 template <int NT, typename PtF, typename OutF>
 __device__ __forceinline__ int rvg_reduce(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos, PtF pt,
                                           OutF out, int* sc) {
     const bool exact = fpos == nullptr;
+    if (!exact) return rvg_reduce_batched<NT, 8>(S, n, rel, fpos, pt, out, sc);
     const unsigned pm = exact ? 0xffffffffu : 0xffffu;
     const int C = (n + NT - 1) / NT;
     const int q0 = min(n, (int)threadIdx.x * C), q1 = min(n, q0 + C);

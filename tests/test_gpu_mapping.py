@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_binding as ob
-from lvo_amd_loader import abi, synth
+from lvo_amd_loader import abi, lvo, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -84,6 +84,7 @@ def test_map_bit_exact_after_sequence(gpu_ctx_factory, name, n_frames):
     inserted points."""
     ctx = gpu_ctx_factory(64)
     orc = ob.Oracle(abi.default_params(64))
+    serial0 = lvo.serial_sort_fallbacks()
     big = 0
     for k in range(n_frames):
         pts = synth.scan(name, k)
@@ -97,3 +98,5 @@ def test_map_bit_exact_after_sequence(gpu_ctx_factory, name, n_frames):
         nd = int(np.sum(np.any(bits(g) != bits(o), axis=1)))
         assert nd == 0, f"map {which}: {nd} of {len(o)} points differ"
     assert big > 10000, big
+    # every line, stack and cube sort stayed on the workgroup replay (no one-thread fallback)
+    assert lvo.serial_sort_fallbacks() == serial0

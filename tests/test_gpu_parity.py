@@ -162,12 +162,16 @@ def test_voxel_grid_matches_pcl_semantics(gpu_ctx_factory):
     ctx = gpu_ctx_factory(64)
     pts = synth.scan("hdl64", 4)
     pts[:, 3] = np.arange(len(pts)) % 64 * 0.01
+    serial0 = lvo.serial_sort_fallbacks()
     for n in (1, 2, 15, 16, 17, 300, 6144, 11264, 11265, 20000, 60000, len(pts)):
         for leaf in ((0.2, 0.4, 0.8) if n in (300, 20000) else (0.4,)):
             vg = ctx.voxel_grid(pts[:n], leaf)
             vp = ob.voxel_grid(pts[:n], leaf, order=1)
             assert vg.shape == vp.shape, (n, leaf)
             assert np.array_equal(bits(vg), bits(vp)), (n, leaf)
+    # exactly the one cloud beyond 65,536 points took the one-thread sort, and it is counted
+    assert len(pts) > 65536
+    assert lvo.serial_sort_fallbacks() - serial0 == 1
     rng = np.random.default_rng(11)
     for case in ("one_leaf", "two_leaves", "sorted", "descending", "few_leaves"):
         m = 5000
