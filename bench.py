@@ -543,7 +543,11 @@ def main():
                 "pipelined_3core": round(pipelined, 4) if pipelined else None,
                 "box": {"value": round(cb["box"]["scans_per_s"], 3), "cores": cb["box"]["cores"],
                         "note": f"{cb['box']['cores']} independent sequences, one pinned process per core, "
-                                f"{cb['box']['frames_per_sequence']} timed frames each"},
+                                f"{cb['box']['frames_per_sequence']} timed frames each",
+                        # SURVEY §8(d)'s P = nproc form, extrapolated from the measured per-core rate (context:
+                        # the box's host shares its cores with other jobs, so all of them were not timed)
+                        "host_nproc": os.cpu_count(),
+                        "full_host_est": round(cb["box"]["scans_per_s"] / max(1, cb["box"]["cores"]) * (os.cpu_count() or 1), 1)},
                 "tictoc_ms": cb["serial"]["tictoc_ms"],
             }
             otraj = cb["traj"]

@@ -692,23 +692,34 @@ __device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
     }
     return __hiloint2double(h2, l2);
 }
+// the partner's `v` (partner lane l^32, or l^16 with ROW16): the gfx950 lane swap of a register with
+// itself leaves this lane's value and the partner's in its two results; which one is the partner's is
+// read from the bits (where the two are equal, either is)
 template <bool ROW16>
-__device__ __forceinline__ double swap_add(double x, double y) {   // lane-swap step: keep x (low) or y (high) by lane bit
-    const unsigned xl = (unsigned)__double2loint(x), xh = (unsigned)__double2hiint(x);
-    const unsigned yl = (unsigned)__double2loint(y), yh = (unsigned)__double2hiint(y);
-    const auto a = ROW16 ? __builtin_amdgcn_permlane16_swap(xl, yl, false, false) : __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
-    const auto b = ROW16 ? __builtin_amdgcn_permlane16_swap(xh, yh, false, false) : __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
-    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+__device__ __forceinline__ double lane_xchg(double v) {
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto a = ROW16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false) : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = ROW16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false) : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const unsigned pl = (unsigned)a[0] == lo ? (unsigned)a[1] : (unsigned)a[0];
+    const unsigned ph = (unsigned)b[0] == hi ? (unsigned)b[1] : (unsigned)b[0];
+    return __hiloint2double((int)ph, (int)pl);
 }
 __device__ __forceinline__ double wave_transpose_sum(const double* acc) {
     double v[32];
 #pragma unroll
     for (int j = 0; j < 32; j++) v[j] = j < NACC ? acc[j] : 0.0;
     const int lane = threadIdx.x & 63;
+    const bool b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = swap_add<false>(v[j], v[j + 16]);   // bit 5
+    for (int j = 0; j < 16; j++) {                                          // bit 5: partner l^32
+        const double send = b5 ? v[j] : v[j + 16], keep = b5 ? v[j + 16] : v[j];
+        v[j] = keep + lane_xchg<false>(send);
+    }
 #pragma unroll
-    for (int j = 0; j < 8; j++) v[j] = swap_add<true>(v[j], v[j + 8]);      // bit 4
+    for (int j = 0; j < 8; j++) {                                           // bit 4: partner l^16
+        const double send = b4 ? v[j] : v[j + 8], keep = b4 ? v[j + 8] : v[j];
+        v[j] = keep + lane_xchg<true>(send);
+    }
 #pragma unroll
     for (int s = 0; s < 3; s++) {                                           // bits 3, 2, 1: partners l^15, l^7, l^2
         const int half = 4 >> s;

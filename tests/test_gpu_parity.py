@@ -647,6 +647,38 @@ def test_cu_mask_contexts_match(gpu_ctx_factory):
     assert lvo.lib().aloam_set_cu_mask(b.h, zero, 8) != 0
 
 
+def test_cu_mask_solver_with_a_busy_neighbour(gpu_ctx_factory):
+    """The persistent LM solver's workgroups exchange records across the grid, so they must all run at
+    once: a context restricted to 4 CUs (grid capped at 4 workgroups) keeps solving correctly while a
+    second context, masked to the same CUs, runs its own frames concurrently from another thread (its
+    kernels take those CUs' slots in between). Poses equal the same context's unshared run to 1e-9."""
+    import ctypes as C
+    import threading
+    frames = [synth.scan("vlp16", k) for k in range(6)]
+    mask = (C.c_uint * 8)(*([0xF] + [0] * 7))
+    ref_ctx = gpu_ctx_factory(16)
+    assert lvo.lib().aloam_set_cu_mask(ref_ctx.h, mask, 8) == 0
+    ref = [ref_ctx.process_scan(f)[1]["t_w_curr"] for f in frames]
+    a, b = gpu_ctx_factory(16), gpu_ctx_factory(16)
+    for c in (a, b):
+        assert lvo.lib().aloam_set_cu_mask(c.h, mask, 8) == 0
+    out, errs = {}, []
+
+    def run(ctx, key, seq):
+        try:
+            out[key] = [ctx.process_scan(f)[1]["t_w_curr"] for f in seq]
+        except Exception as e:   # surfaced below
+            errs.append(e)
+    busy = [synth.scan("hdl64", k) for k in range(4)]
+    t1 = threading.Thread(target=run, args=(a, "a", frames))
+    t2 = threading.Thread(target=run, args=(b, "b", busy))
+    t1.start(); t2.start(); t1.join(timeout=300); t2.join(timeout=300)
+    assert not errs, errs
+    assert len(out["a"]) == len(frames)
+    for x, y in zip(out["a"], ref):
+        np.testing.assert_allclose(x, y, rtol=1e-9, atol=1e-12)
+
+
 def test_c5_sequence_ate_vs_oracle(lvo):
     """BASELINE configs[4] stand-in (KITTI-04 is not on the box): the 271-frame synthetic straight road
     end to end through the native pipeline against the oracle run of the same frames. North-star bar:
