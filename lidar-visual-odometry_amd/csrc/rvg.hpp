@@ -53,12 +53,8 @@ __device__ __forceinline__ void rvg_positions(const unsigned long long* E, const
     }
 }
 
-// Leaf sums: thread t owns the leaves starting in its chunk of S; out(r, centroid) for the r-th leaf in key
-// order; returns the number of leaves (all threads). A relevant leaf's points are added in fpos order (up
-// to 16 by a register sorting network, more by repeated selection). fpos == null: S is PCL's order itself
-// (every leaf summed in S order; payloads are then full 32-bit point indices). sc: 2 (NT / 64) + 2 ints of
-// LDS.
-// One relevant leaf S[q, e) (len >= 3) summed in fpos order.
+// One relevant leaf S[q, e) (len >= 3) summed in fpos order (up to 16 points by a register sorting network,
+// more by repeated selection).
 template <typename PtF>
 __device__ __forceinline__ float4 rvg_rel_sum(const unsigned long long* S, const int q, const int e, const int* fpos, PtF pt) {
     const int len = e - q;
@@ -168,11 +164,15 @@ __device__ __forceinline__ int rvg_reduce_batched(const unsigned long long* S, c
     return tot;
 }
 
+// Leaf sums: thread t owns the leaves starting in its chunk of S; out(r, centroid) for the r-th leaf in key
+// order; returns the number of leaves (all threads). A relevant leaf's points are added in fpos order.
+// fpos == null: S is PCL's order itself (every leaf summed in S order; payloads are then full 32-bit point
+// indices). sc: 2 (NT / 64) + 2 ints of LDS. This is the leaf-at-a-time form (the exact mode's path, and
+// the batched form's reference in tests/ps_emu.cpp).
 template <int NT, typename PtF, typename OutF>
-__device__ __forceinline__ int rvg_reduce(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos, PtF pt,
-                                          OutF out, int* sc) {
+__device__ __forceinline__ int rvg_reduce_loop(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos, PtF pt,
+                                               OutF out, int* sc) {
     const bool exact = fpos == nullptr;
-    if (!exact) return rvg_reduce_batched<NT, 8>(S, n, rel, fpos, pt, out, sc);
     const unsigned pm = exact ? 0xffffffffu : 0xffffu;
     const int C = (n + NT - 1) / NT;
     const int q0 = min(n, (int)threadIdx.x * C), q1 = min(n, q0 + C);
@@ -230,6 +230,13 @@ __device__ __forceinline__ int rvg_reduce(const unsigned long long* S, const int
         run++;
     }
     return tot;
+}
+
+template <int NT, typename PtF, typename OutF>
+__device__ __forceinline__ int rvg_reduce(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos, PtF pt,
+                                          OutF out, int* sc) {
+    if (fpos) return rvg_reduce_batched<NT, 8>(S, n, rel, fpos, pt, out, sc);
+    return rvg_reduce_loop<NT>(S, n, rel, fpos, pt, out, sc);
 }
 
 }  // namespace aloam

@@ -269,7 +269,17 @@ template <class V> void hook(const V& in, float leaf, int kind) {
                         long pops = 0;
                         for (IV* p = first; p < last; p++) pops += p->idx >= kmin;
                         hs_pr += m / 2 * 2 + pops * lg2;
-                        if (getenv("CS_HEAPS")) printf("HEAP kind %d m %ld pops %ld n %zu\n", kind, m, pops, n);
+                        if (getenv("CS_HEAPS")) {
+                            std::map<unsigned, int> dk;
+                            for (IV* p = first; p < last; p++) dk[p->idx]++;
+                            int ng = 0, nm = 0, mx = 0, ge3 = 0;
+                            for (auto& kv : c) if (kv.second >= 2) { ng++; nm += kv.second; }
+                            for (auto& kv : dk) { mx = std::max(mx, kv.second); ge3 += kv.second >= 2; }
+                            long below = 0;   // segment elements below the smallest relevant key
+                            for (IV* p = first; p < last; p++) below += p->idx < kmin;
+                            printf("HEAP kind %d m %ld pops %ld n %zu groups %d members %d distinct %zu dupkeys %d maxmult %d below %ld\n",
+                                   kind, m, pops, n, ng, nm, dk.size(), ge3, mx, below);
+                        }
                         std::map<unsigned, int> relg;
                         for (auto& kv : c) if (kv.second >= 2) relg[kv.first] = kv.second;
                         heap_sort_check(first, last, less, relg, A);

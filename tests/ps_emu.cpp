@@ -118,6 +118,13 @@ static std::atomic<long> g_postorder{0};      // ws_heap_postorder hits (coverag
 #define PS_POSTORDER_COUNT g_postorder
 #include "../lidar-visual-odometry_amd/csrc/pcl_sort.hpp"
 #include "../lidar-visual-odometry_amd/csrc/ls_sort.hpp"
+struct float4 { float x, y, z, w; };
+static inline float4 make_float4(float x, float y, float z, float w) { return {x, y, z, w}; }
+static inline unsigned atomicOr(unsigned* p, unsigned v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
+namespace aloam {
+inline float4 div4_by_count(float4 v, int k) { const float d = (float)k; return {v.x / d, v.y / d, v.z / d, v.w / d}; }
+}
+#include "../lidar-visual-odometry_amd/csrc/rvg.hpp"
 
 // the level-synchronous sort (csrc/ls_sort.hpp) on one emulated workgroup of NT threads
 template <int NT, int CPW>
@@ -241,6 +248,64 @@ static int heap_trials(int trials, std::mt19937_64& rng) {
     return bad;
 }
 
+// csrc/rvg.hpp's leaf sums: the batched form (rvg_reduce_batched, the map filter's) against the
+// leaf-at-a-time loop on one emulated workgroup: S sorted by key (random tie order), rel = the points of
+// >= 3-point leaves, fpos a random position per point; identical centroids (bits) and leaf counts. Mode 5.
+static int reduce_trials(int trials, std::mt19937_64& rng) {
+    constexpr int NT = 128;
+    int bad = 0;
+    for (int t = 0; t < trials; t++) {
+        const int n = t % 7 == 0 ? (int)(rng() % 40) : 1 + (int)(rng() % 6000);
+        const unsigned kinds = 1 + (unsigned)(rng() % (unsigned)(t % 3 == 0 ? n / 4 + 1 : 2 * n + 1));
+        std::vector<unsigned long long> S(n);
+        for (int i = 0; i < n; i++) S[i] = ((unsigned long long)(unsigned)(rng() % kinds) << 32) | (unsigned)i;
+        std::shuffle(S.begin(), S.end(), rng);
+        std::stable_sort(S.begin(), S.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
+        std::vector<unsigned> rel(n / 32 + 2, 0u);
+        for (int i = 0; i < n;) {
+            int j = i;
+            while (j < n && (S[j] >> 32) == (S[i] >> 32)) j++;
+            if (j - i >= 3) for (int k = i; k < j; k++) { const unsigned x = (unsigned)S[k] & 0xffffu; rel[x >> 5] |= 1u << (x & 31); }
+            i = j;
+        }
+        std::vector<int> fpos(n + 1);
+        for (int i = 0; i < n; i++) fpos[i] = i;
+        std::shuffle(fpos.begin(), fpos.begin() + n, rng);
+        std::vector<float4> P(n + 1);
+        for (int i = 0; i < n; i++) P[i] = {(float)(rng() % 100000) * 0.013f, (float)(rng() % 100000) * -0.007f, (float)(rng() % 1000) * 0.1f, (float)(i % 7)};
+        std::vector<float4> out[2];
+        int tot[2];
+        for (int form = 0; form < 2; form++) {
+            out[form].assign(n + 1, float4{-1.f, -1.f, -1.f, -1.f});
+            std::vector<int> sc(2 * (NT / WAVE) + 2);
+            g_waves.clear();
+            for (int w = 0; w < NT / WAVE; w++) {
+                auto c = std::make_unique<WaveCtx>();
+                c->bar = std::make_unique<std::barrier<>>(WAVE);
+                g_waves.push_back(std::move(c));
+            }
+            g_block = std::make_unique<std::barrier<>>(NT);
+            std::vector<std::thread> th;
+            std::vector<int> r(NT);
+            for (int tt = 0; tt < NT; tt++)
+                th.emplace_back([&, tt] {
+                    threadIdx.x = tt; t_lane = tt % WAVE; t_wave = tt / WAVE;
+                    auto pt = [&](int i) { return P[i]; };
+                    auto of = [&](int q, float4 v) { out[form][q] = v; };
+                    r[tt] = form == 0 ? aloam::rvg_reduce_loop<NT>(S.data(), n, rel.data(), fpos.data(), pt, of, sc.data())
+                                      : aloam::rvg_reduce_batched<NT, 8>(S.data(), n, rel.data(), fpos.data(), pt, of, sc.data());
+                });
+            for (auto& x : th) x.join();
+            tot[form] = r[0];
+        }
+        if (tot[0] != tot[1] || std::memcmp(out[0].data(), out[1].data(), sizeof(float4) * (size_t)tot[0]) != 0) {
+            bad++;
+            std::printf("reduce mismatch trial %d n %d kinds %u leaves %d/%d\n", t, n, kinds, tot[0], tot[1]);
+        }
+    }
+    return bad;
+}
+
 #ifndef NTHREADS
 #define NTHREADS 128
 #endif
@@ -256,6 +321,11 @@ int main(int argc, char** argv) {
     // must equal std::sort's (heap sorts gated / queued / stopped early, other ties free)
     const bool relmode = argc > 5 && atoi(argv[5]) == 1;
     int bad = 0;
+    if (lsm == 5) {
+        bad = reduce_trials(trials, rng);
+        std::printf("trials %d mismatches %d\n", trials, bad);
+        return bad != 0;
+    }
     if (lsm == 4) {
         bad = heap_trials(trials, rng);
         std::printf("postorder segments %ld\n", (long)g_postorder.load());

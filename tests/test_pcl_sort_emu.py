@@ -75,3 +75,13 @@ def test_wave_heap_sort_orders_relevant_keys_like_libstdcxx(emu):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
     assert "postorder segments 0" not in r.stdout
+
+
+def test_batched_leaf_sums_match_the_leaf_loop(emu):
+    # csrc/rvg.hpp rvg_reduce_batched (the map filter's leaf sums: chunk entries and points loaded in batches,
+    # leaves summed from registers, relevant leaves in fpos order) against the leaf-at-a-time loop on one
+    # emulated 128-thread workgroup: the same centroids bit for bit and the same leaf count, across chunk
+    # boundaries, leaves running past a chunk, all-relevant and no-relevant inputs
+    r = subprocess.run([emu, "300", "29", "5"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
