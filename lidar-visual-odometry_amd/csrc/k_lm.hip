@@ -633,47 +633,7 @@ __device__ __forceinline__ void block_reduce_acc(const double* acc, double* rows
     reduce_rows(rows, NT / 4, part8, tot);
 }
 
-// Cross-workgroup exchange for the persistent solver: a tagged all-gather instead of a counter
-// barrier. Workgroup b writes its NACC partials into record b of this pass's buffer, waits for the
-// stores to complete, then writes the record's tag = epoch; every workgroup polls the G tags (one
-// lane each) until all equal the epoch and then reads the G records. There is no read-modify-write
-// on a shared word, so arrivals do not serialise at one address. All cross-workgroup data moves
-// through agent-scope RELAXED atomics (coherent across XCDs on their own), ordered by completion
-// (s_waitcnt vmcnt(0)); acquire/release would add an L2 writeback + invalidate per poll.
-// Epochs are unique per (launch, pass): seq (read at kernel start, bumped by workgroup 0 at the end)
-// * 256 + pass + 1, so records left by earlier launches never match and nothing is re-initialised.
-// Bounded spin: an exchange that does not complete flags an error instead of hanging the queue.
-constexpr int LM_REC = 32;   // u64 per record: NACC partials, tag at [LM_REC - 1]
-__device__ __forceinline__ bool gather_partials(unsigned long long* buf, unsigned long long epoch, const double* tot,
-                                                double* rows, unsigned G, int* err) {
-    __shared__ int ok;
-    unsigned long long* mine = buf + (size_t)blockIdx.x * LM_REC;
-    if (threadIdx.x < 64) {   // wave 0: publish, then poll
-        if (threadIdx.x < NACC)
-            __hip_atomic_store(&mine[threadIdx.x], (unsigned long long)__double_as_longlong(tot[threadIdx.x]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (threadIdx.x == 0) __hip_atomic_store(&mine[LM_REC - 1], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // lane l polls the tags of records l and l + 64 (G <= 128)
-        const unsigned long long* tag = buf + (size_t)threadIdx.x * LM_REC + (LM_REC - 1);
-        const unsigned long long* tag2 = tag + (size_t)64 * LM_REC;
-        int spins = 0, good = 1;
-        while (!__all((threadIdx.x >= G || __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) &&
-                      (threadIdx.x + 64 >= G || __hip_atomic_load(tag2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch))) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1 << 22)) { good = 0; break; }
-        }
-        if (threadIdx.x == 0) { ok = good; if (!good) atomicExch(err, 1); }
-    }
-    __syncthreads();
-    if (!ok) return false;
-    for (int i = threadIdx.x; i < (int)G * NACC; i += blockDim.x) {   // all records -> LDS in one round trip
-        const int b = i / NACC, c = i - b * NACC;
-        rows[i] = __longlong_as_double(__hip_atomic_load(&buf[(size_t)b * LM_REC + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();
-    return true;
-}
+constexpr int LM_REC = 32;   // u64 per record of the persistent solver's exchange (NACC partials + check word)
 
 // ---- k_lm_coop's per-pass reduction and exchange ---------------------------------------------------
 // Wave sum of NACC (<= 32) doubles by transposition: five halving steps, each exchanging half of the

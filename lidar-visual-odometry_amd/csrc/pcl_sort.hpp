@@ -437,72 +437,6 @@ __device__ inline void ws_heap_sort(unsigned long long* E, const int f, const in
         ws_sift(H, hl, v);
     }
 }
-// The pops of __sort_heap pipelined over the lanes of one wave: pop i runs on lane i % 64, one heap level
-// per step, in the top-down form of __adjust_heap (see ws_sift). Consecutive pops are two levels apart: in
-// a step every pop first writes the element it chose in the previous step into its hole's parent slot,
-// then reads its hole's children, so a pop reads a level only after the pop ahead of it (two levels
-// deeper) has finished writing it. Pop i starts no earlier than two steps after pop i - 1, and only once no
-// pop in flight still has slot hl_i (its value, the heap's last slot) below or at its hole: from then on
-// that slot is pop i's alone, so the popped root goes straight into it. The result is std::__sort_heap's
-// array; pops stop after npop (the early stop of ws_heap_sort).
-__device__ inline void ws_sort_heap_pipelined(unsigned long long* H, const int len, const int npop) {
-    const int lane = lane_id();
-    // this lane's pop (if any): hole h, its level, heap size hl, value v, the element to write next into
-    // slot par (par < 0: none), done flag
-    int h = 0, hl = 0, par = -1;
-    unsigned long long v = 0ull, pend = 0ull;
-    bool act = false, stop = false;
-    int next = 0, last_start = -2;             // next pop to start; step of the last start (uniform)
-    for (int t = 0;; t++) {
-        // phase 1: pending writes (the winner moved up into the parent slot, or v placed: pop done)
-        if (act && par >= 0) {
-            H[par] = pend;
-            if (stop) act = false;
-        }
-        // start the next pop: no pop in flight may still write its value slot hl = len - 1 - next
-        bool started = false;
-        if (next < npop && t - last_start >= 2) {
-            const int hn = len - 1 - next;
-            bool anc = false;
-            if (act) {                          // h an ancestor (or itself) of hn?
-                const int dh = 31 - __builtin_clz((unsigned)(h + 1)), dn = 31 - __builtin_clz((unsigned)(hn + 1));
-                anc = dn >= dh && (((hn + 1) >> (dn - dh)) - 1) == h;
-            }
-            if (!__ballot(anc)) {
-                started = true;
-                if (lane == (next & 63)) {
-                    act = true; stop = false; par = -1; h = 0; hl = hn;
-                    v = H[hn];
-                    H[hn] = H[0];               // the popped root into its final slot
-                }
-                next++;
-                last_start = t;
-            }
-        }
-        if (!__ballot(act) && next >= npop) break;
-        // phase 2: read the hole's children, choose (ties: the right one), decide
-        if (act) {
-            const int c1 = 2 * h + 1;
-            unsigned long long w = 0ull;
-            int wi = -1;
-            if (c1 < hl) {
-                const unsigned long long e1 = H[c1];
-                wi = c1; w = e1;
-                if (c1 + 1 < hl) {
-                    const unsigned long long e2 = H[c1 + 1];
-                    if (!(ps_key(e2) < ps_key(e1))) { wi = c1 + 1; w = e2; }
-                }
-            }
-            par = h;
-            if (wi >= 0 && ps_key(w) >= ps_key(v)) { pend = w; h = wi; stop = false; }
-            else { pend = v; stop = true; }
-        }
-        (void)started;
-        ps_wsync<true>();
-    }
-    ps_wsync<true>();
-}
-
 // ps_order_matters by a wave (all lanes get the answer)
 __device__ inline bool ws_order_matters(const unsigned long long* E, int f, int l, const unsigned* rel) {
     if (!rel) return true;

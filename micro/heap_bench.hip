@@ -11,21 +11,7 @@ __global__ void __launch_bounds__(64) k_heap(const unsigned long long* in, unsig
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     if (MODE == 0) { if (threadIdx.x == 0) ps_heap_sort(E, E + n); }
-    else if (MODE == 1) ws_heap_sort(E, 0, n, nullptr);
-    else {                                   // make_heap by levels, then the pipelined pops
-        const int len = n, lane = threadIdx.x;
-        const int P = (len - 2) / 2;
-        const int D = 31 - __builtin_clz((unsigned)(P + 1));
-        for (int d = D; d >= 0; d--) {
-            const int a0 = (1 << d) - 1, a1 = min((2 << d) - 2, P);
-            for (int base = a0; base <= a1; base += 64) {
-                const int node = base + lane;
-                if (node <= a1) ps_adjust_heap(E, node, len, E[node]);
-            }
-            ps_wsync<true>();
-        }
-        ws_sort_heap_pipelined(E, len, len - 1);
-    }
+    else ws_heap_sort(E, 0, n, nullptr);   // E in LDS: the store-wait-free pops
     __syncthreads();
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) *cyc = t1 - t0;
@@ -37,8 +23,7 @@ extern "C" int heap_run(const unsigned long long* h_in, unsigned long long* h_ou
     hipMemcpy(d_in, h_in, 8 * n, hipMemcpyHostToDevice);
     for (int r = 0; r < 3; r++) {
         if (mode == 0) k_heap<0><<<1, 64>>>(d_in, d_out, n, d_c);
-        else if (mode == 1) k_heap<1><<<1, 64>>>(d_in, d_out, n, d_c);
-        else k_heap<2><<<1, 64>>>(d_in, d_out, n, d_c);
+        else k_heap<1><<<1, 64>>>(d_in, d_out, n, d_c);
     }
     hipMemcpy(h_out, d_out, 8 * n, hipMemcpyDeviceToHost);
     hipMemcpy(cycles, d_c, 8, hipMemcpyDeviceToHost);
