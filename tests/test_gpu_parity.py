@@ -650,18 +650,20 @@ def test_cu_mask_contexts_match(gpu_ctx_factory):
 def test_cu_mask_solver_with_a_busy_neighbour(gpu_ctx_factory):
     """The persistent LM solver's workgroups exchange records across the grid, so they must all run at
     once: a context restricted to 4 CUs (grid capped at 4 workgroups) keeps solving correctly while a
-    second context, masked to the same CUs, runs its own frames concurrently from another thread (its
-    kernels take those CUs' slots in between). Poses equal the same context's unshared run to 1e-9."""
+    second context runs its own frames concurrently from another thread on the next 60 CUs (disjoint CU
+    sets, as the pipeline gives its stages: INTEGRATION.md). Poses equal the same context's unshared run
+    to 1e-9."""
     import ctypes as C
     import threading
     frames = [synth.scan("vlp16", k) for k in range(6)]
     mask = (C.c_uint * 8)(*([0xF] + [0] * 7))
+    other = (C.c_uint * 8)(*([0xFFFFFFF0, 0xFFFFFFFF] + [0] * 6))
     ref_ctx = gpu_ctx_factory(16)
     assert lvo.lib().aloam_set_cu_mask(ref_ctx.h, mask, 8) == 0
     ref = [ref_ctx.process_scan(f)[1]["t_w_curr"] for f in frames]
-    a, b = gpu_ctx_factory(16), gpu_ctx_factory(16)
-    for c in (a, b):
-        assert lvo.lib().aloam_set_cu_mask(c.h, mask, 8) == 0
+    a, b = gpu_ctx_factory(16), gpu_ctx_factory(64)
+    assert lvo.lib().aloam_set_cu_mask(a.h, mask, 8) == 0
+    assert lvo.lib().aloam_set_cu_mask(b.h, other, 8) == 0
     out, errs = {}, []
 
     def run(ctx, key, seq):
