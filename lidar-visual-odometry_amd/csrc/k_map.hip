@@ -1186,7 +1186,7 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubered(RbKinds P, const MapState*
     __syncthreads();
     const float4* B = K.B;
     float4* Cf = K.Cf;
-    const int tot = rvg_reduce<RBV_T>(rvg_S(G, n), n, rvg_rel(G, n), rvg_fpos(G, n), [&](int i) { return B[p0 + i]; },
+    const int tot = rvg_reduce<RBV_T, true>(rvg_S(G, n), n, rvg_rel(G, n), rvg_fpos(G, n), [&](int i) { return B[p0 + i]; },
                                       [&](int q, float4 v) { Cf[p0 + q] = v; }, sc);
     if (threadIdx.x == 0) K.a.seg_nout[c] = tot;
 }

@@ -201,6 +201,31 @@ __device__ inline void ps_heap_sort_rel(unsigned long long* E, int f, int l, con
 // of the hole's subtree node r (relative heap numbering, depths 0-5) and votes (child chosen, moves up),
 // the path is walked on the two ballots in scalar registers, and the path's lanes shift their winners up
 // with one store.
+// The hole's path through one six-level subtree from the two ballots (bit r: subtree node r's larger child
+// moves up / is the right one), without a data-dependent loop: the six candidate nodes follow the `right`
+// bits alone, the path length is the run of leading `go` bits along them. Returns the node where the path
+// stops (< 63: the value goes there; 63..126 after six steps), the path's nodes in *pm, its length in *steps.
+__device__ __forceinline__ int ws_path(const unsigned long long mgo, const unsigned long long mr, unsigned long long* pm, int* steps) {
+    int rk[7];
+    rk[0] = 0;
+    unsigned gom = 0u;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        gom |= (unsigned)((mgo >> rk[k]) & 1ull) << k;
+        rk[k + 1] = 2 * rk[k] + 1 + (int)((mr >> rk[k]) & 1ull);
+    }
+    const int st = __builtin_ctz(~gom);           // <= 6: gom < 64
+    unsigned long long m = 0ull;
+    int r = rk[0];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (k < st) m |= 1ull << rk[k];
+        if (k + 1 == st) r = rk[k + 1];
+    }
+    *pm = m;
+    *steps = st;
+    return r;
+}
 __device__ inline void ws_sift(unsigned long long* H, const int hl, const unsigned long long v) {
     const int lane = lane_id();
     const int dr = 31 - __builtin_clz((unsigned)(lane + 1));   // depth of subtree node `lane` (lane 63: unused)
@@ -223,13 +248,9 @@ __device__ inline void ws_sift(unsigned long long* H, const int hl, const unsign
             }
         }
         const unsigned long long mgo = __ballot(go), mr = __ballot(right);
-        int r = 0, steps = 0;
-        unsigned long long pm = 0ull;
-        while (steps < 6 && ((mgo >> r) & 1ull)) {
-            pm |= 1ull << r;
-            r = 2 * r + 1 + (int)((mr >> r) & 1ull);
-            steps++;
-        }
+        unsigned long long pm;
+        int steps;
+        const int r = ws_path(mgo, mr, &pm, &steps);
         if ((pm >> lane) & 1ull) H[a] = w;
         if (steps < 6) {                        // v fills the hole at subtree node r
             const int ar = readlane_i(a, r);
@@ -290,13 +311,9 @@ __device__ inline void ws_sort_heap_lds(unsigned long long* H, const int len, co
             const unsigned long long w = right ? e2 : e1;
             const bool go = has && ps_key(w) >= vk;
             const unsigned long long mgo = __ballot(go), mr = __ballot(right);
-            int r = 0, steps = 0;
-            unsigned long long pm = 0ull;
-            while (steps < 6 && ((mgo >> r) & 1ull)) {
-                pm |= 1ull << r;
-                r = 2 * r + 1 + (int)((mr >> r) & 1ull);
-                steps++;
-            }
+            unsigned long long pm;
+            int steps;
+            const int r = ws_path(mgo, mr, &pm, &steps);
             if ((pm >> lane) & 1ull) H[a] = w;
             if (first) top = (mgo & 1ull) ? ps_rl64(w, 0) : v;   // the new root
             if (steps < 6) {                                 // v fills the hole at subtree node r
@@ -393,7 +410,7 @@ __device__ inline bool ws_heap_postorder(unsigned long long* H, const int len, c
     return true;
 }
 
-__device__ inline void ws_heap_sort(unsigned long long* E, const int f, const int l, const unsigned* rel) {
+__device__ __noinline__ void ws_heap_sort(unsigned long long* E, const int f, const int l, const unsigned* rel) {
     const int len = l - f;
     if (len < 2) return;
     unsigned long long* H = E + f;

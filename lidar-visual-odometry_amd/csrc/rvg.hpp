@@ -232,10 +232,12 @@ __device__ __forceinline__ int rvg_reduce_loop(const unsigned long long* S, cons
     return tot;
 }
 
-template <int NT, typename PtF, typename OutF>
+// BATCHED: the batched form (S in global memory and registers to spare, k_rb_cubered); else the loop
+// (S in LDS, or a kernel whose other phases already fill the 1024-thread register budget)
+template <int NT, bool BATCHED = false, typename PtF, typename OutF>
 __device__ __forceinline__ int rvg_reduce(const unsigned long long* S, const int n, const unsigned* rel, const int* fpos, PtF pt,
                                           OutF out, int* sc) {
-    if (fpos) return rvg_reduce_batched<NT, 8>(S, n, rel, fpos, pt, out, sc);
+    if (BATCHED && fpos) return rvg_reduce_batched<NT, 8>(S, n, rel, fpos, pt, out, sc);
     return rvg_reduce_loop<NT>(S, n, rel, fpos, pt, out, sc);
 }
 
