@@ -221,13 +221,14 @@ __device__ __forceinline__ void assoc_slots(
     const GridDesc* __restrict__ gdc, const int* __restrict__ cs_c, const float4* __restrict__ sp_c, const int* __restrict__ si_c,
     const GridDesc* __restrict__ gds, const int* __restrict__ cs_s, const float4* __restrict__ sp_s, const int* __restrict__ si_s,
     aloam_factor* __restrict__ out, int* round_cnt, unsigned long long* cand_count, int exp, int (*tabs)[20],
-    int* __restrict__ nbr = nullptr, const MapCache* mc = nullptr) {
+    int* __restrict__ nbr = nullptr, const MapCache mc = MapCache{}) {
     const bool lead = (lane_id() & (G - 1)) == 0;
     const int per_wave = WAVE / G;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, nwaves = gridDim.x * (blockDim.x / WAVE);
     int cnt_c = 0, cnt_s = 0;
     unsigned long long ncand_sum = 0;
-    const int round = mc ? mc->round : 0, wst_round = round;
+    const bool has_mc = mc.ctr != nullptr;   // by value: no private copy of the struct
+    const int round = has_mc ? mc.round : 0, wst_round = round;
     for (int base = s0 + wave * per_wave; base < s1; base += nwaves * per_wave) {   // wave-uniform trip count
         const int qi = base + (lane_id() / G);
         const bool live = qi < s1;
@@ -237,11 +238,11 @@ __device__ __forceinline__ void assoc_slots(
         const GridDesc gd = corner ? *gdc : *gds;
         const float4 sel = associate_to_map(par, po);
         const float4* sp = corner ? sp_c : sp_s;
-        const bool slot = mc && live && qi < mc->cap_q;
+        const bool slot = has_mc && live && qi < mc.cap_q;
         int ncache = -1;
         bool cached = false;
         if (slot && round > 0) {
-            const float4 c = mc->ctr[qi];
+            const float4 c = mc.ctr[qi];
             ncache = __float_as_int(c.w);
             const float ex = sel.x - c.x, ey = sel.y - c.y, ez = sel.z - c.z;
             cached = ncache >= 0 && ncache <= MC_CAP && ex * ex + ey * ey + ez * ez <= (MC_M - MC_EPS) * (MC_M - MC_EPS) &&
@@ -257,7 +258,7 @@ __device__ __forceinline__ void assoc_slots(
 #pragma unroll
             for (int k = 0; k < 5; k++) pos[k] = -1;
             const bool search = live && !cached;
-            if (mc && round > 0) {
+            if (has_mc && round > 0) {
                 // the few queries that left their cache: a whole wave per query (its latency bounds the
                 // launch: one group's search over a dense block streams hundreds of candidates per lane group)
                 unsigned long long todo = __ballot(search && lead);
@@ -268,7 +269,7 @@ __device__ __forceinline__ void assoc_slots(
                     const bool qc = __shfl((int)corner, src) != 0, qslot = __shfl((int)slot, src) != 0;
                     const float qx = __shfl(sel.x, src), qy = __shfl(sel.y, src), qz = __shfl(sel.z, src);
                     const GridDesc& g = qc ? *gdc : *gds;
-                    const KnnCollect col{(1.0f + MC_M) * (1.0f + MC_M), mc->pts + (size_t)q * MC_CAP, mc->pos + (size_t)q * MC_CAP,
+                    const KnnCollect col{(1.0f + MC_M) * (1.0f + MC_M), mc.pts + (size_t)q * MC_CAP, mc.pos + (size_t)q * MC_CAP,
                                          qslot ? MC_CAP : 0};
                     int p2[5], i2[5], ncol = 0;
                     float e2[5];
@@ -276,7 +277,7 @@ __device__ __forceinline__ void assoc_slots(
                                                                        qc ? sp_c : sp_s, qc ? si_c : si_s, qx, qy, qz, 1.0f, true, p2,
                                                                        e2, i2, nullptr, tabs[(threadIdx.x & ~(WAVE - 1)) / G], g.n,
                                                                        col, &ncol);
-                    if (lane_id() == 0 && qslot) mc->ctr[q] = make_float4(qx, qy, qz, __int_as_float(ncol <= MC_CAP ? ncol : -1));
+                    if (lane_id() == 0 && qslot) mc.ctr[q] = make_float4(qx, qy, qz, __int_as_float(ncol <= MC_CAP ? ncol : -1));
                     if (lane_id() / G == src / G) {
 #pragma unroll
                         for (int k = 0; k < 5; k++) pos[k] = p2[k];
@@ -284,15 +285,15 @@ __device__ __forceinline__ void assoc_slots(
                     }
                 }
             } else if (__any(search)) {
-                if (mc) {   // search + collect: (re)centre the cache at this round's position
-                    const KnnCollect col{(1.0f + MC_M) * (1.0f + MC_M), mc->pts + (size_t)qi * MC_CAP, mc->pos + (size_t)qi * MC_CAP,
+                if (has_mc) {   // search + collect: (re)centre the cache at this round's position
+                    const KnnCollect col{(1.0f + MC_M) * (1.0f + MC_M), mc.pts + (size_t)qi * MC_CAP, mc.pos + (size_t)qi * MC_CAP,
                                          slot ? MC_CAP : 0};
                     int ncol = 0;
                     found = group_knn27<5, G, true, U, true>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz,
                                                              corner ? cs_c : cs_s, sp, corner ? si_c : si_s, sel.x, sel.y, sel.z,
                                                              1.0f, search, pos, d2, idx, &ncand, tabs[threadIdx.x / G], gd.n,
                                                              col, &ncol);
-                    if (search && slot && lead) mc->ctr[qi] = make_float4(sel.x, sel.y, sel.z, __int_as_float(ncol <= MC_CAP ? ncol : -1));
+                    if (search && slot && lead) mc.ctr[qi] = make_float4(sel.x, sel.y, sel.z, __int_as_float(ncol <= MC_CAP ? ncol : -1));
                 } else {
                     found = group_knn27<5, G, true, U>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, corner ? cs_c : cs_s, sp,
                                                        corner ? si_c : si_s, sel.x, sel.y, sel.z, 1.0f, search, pos, d2, idx, &ncand,
@@ -304,7 +305,7 @@ __device__ __forceinline__ void assoc_slots(
                 int p2[5], i2[5];
                 float e2[5];
                 const size_t cb = cached ? (size_t)qi * MC_CAP : 0;
-                const int f2 = group_knn_list<5, G, (MC_CAP + G - 1) / G>(mc->pts + cb, mc->pos + cb, cached ? ncache : 0, sel.x,
+                const int f2 = group_knn_list<5, G, (MC_CAP + G - 1) / G>(mc.pts + cb, mc.pos + cb, cached ? ncache : 0, sel.x,
                                                                           sel.y, sel.z, 1.0f, p2, e2, i2);
                 if (cached) {
 #pragma unroll
@@ -323,7 +324,7 @@ __device__ __forceinline__ void assoc_slots(
                 // unchanged neighbours since the last round: the factor in out[qi] is this round's
                 bool same = false;
                 if (slot) {
-                    int* pv = mc->prev + (size_t)qi * 5;
+                    int* pv = mc.prev + (size_t)qi * 5;
                     same = round > 0;
 #pragma unroll
                     for (int k = 0; k < 5; k++) same = same && pv[k] == (use ? pos[k] : -1);
@@ -383,7 +384,7 @@ __global__ void __launch_bounds__(256) k_map_assoc(
     for (int i = 0; i < 7; i++) par[i] = m->parameters[i];
     WSTAMP(1);
     assoc_slots<G, U>(cstack, sstack, nc, 0, nc + ns, par, gdc, cs_c, sp_c, si_c, gds, cs_s, sp_s, si_s, out, round_cnt,
-                      cand_count, exp, tabs, nbr, mc.ctr ? &mc : nullptr);
+                      cand_count, exp, tabs, nbr, mc);
     WSTAMP(5);
 }
 
