@@ -724,7 +724,7 @@ __device__ __forceinline__ unsigned long long xor32_lanes(unsigned long long v) 
 // when the hashes of what they read XOR to zero. A stale record (another epoch) or one whose stores
 // are still landing fails the check (up to 2^-64). Stores and loads are agent-scope relaxed atomics
 // (64-bit single-copy atomic, coherent across XCDs); no fence, no completion wait before a tag.
-constexpr int LM_COOP_MAX_RECS = 128;   // records per pass buffer (k_lm_coop's workgroup cap)
+constexpr int LM_COOP_MAX_RECS = 64;    // records per pass buffer = k_lm_coop's workgroup cap (128 measured slower in round 2)
 __device__ __forceinline__ void publish_record(unsigned long long* buf, unsigned long long epoch, double v) {
     const int lane = threadIdx.x & 63;   // wave 0 only; lane i < NACC holds partial i
     const unsigned long long w = lane < NACC ? (unsigned long long)__double_as_longlong(v) : 0ull;
