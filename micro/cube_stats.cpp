@@ -277,8 +277,19 @@ template <class V> void hook(const V& in, float leaf, int kind) {
                             for (auto& kv : dk) { mx = std::max(mx, kv.second); ge3 += kv.second >= 2; }
                             long below = 0;   // segment elements below the smallest relevant key
                             for (IV* p = first; p < last; p++) below += p->idx < kmin;
-                            printf("HEAP kind %d m %ld pops %ld n %zu groups %d members %d distinct %zu dupkeys %d maxmult %d below %ld\n",
-                                   kind, m, pops, n, ng, nm, dk.size(), ge3, mx, below);
+                            // refined: a group with exactly 2 points here and none of its points before the
+                            // segment has them as its leaf's first two terms (commutative): order free
+                            unsigned kref = ~0u;
+                            for (auto& kv : c) {
+                                if (kv.second < 2) continue;
+                                int before = 0;
+                                for (IV* p = w.data(); p < first; p++) before += p->idx == kv.first;
+                                if (kv.second >= 3 || before >= 1) kref = std::min(kref, kv.first);
+                            }
+                            long pref = 0;
+                            for (IV* p = first; p < last; p++) pref += kref != ~0u && p->idx >= kref;
+                            printf("HEAP kind %d m %ld pops %ld n %zu groups %d members %d distinct %zu dupkeys %d maxmult %d below %ld refined_pops %ld\n",
+                                   kind, m, pops, n, ng, nm, dk.size(), ge3, mx, below, pref);
                         }
                         std::map<unsigned, int> relg;
                         for (auto& kv : c) if (kv.second >= 2) relg[kv.first] = kv.second;
