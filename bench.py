@@ -153,9 +153,10 @@ def c4_search(lvo, torch, dev, launches):
             by.append(t["knn_bytes"])
             st.append(t["knn_streamed_bytes"])
     found = float((idx[:, 4] >= 0).float().mean().item())
+    kernel = ctx.knn_kernel()
     ctx.close()
     return {"map_points": len(m), "queries": len(q), "ms": float(np.mean(ms)), "bytes": float(np.mean(by)),
-            "streamed": float(np.mean(st)), "found5": found}
+            "streamed": float(np.mean(st)), "found5": found, "kernel": kernel}
 
 
 def c4_registration(lvo, torch, dev, dist, rank, world, steps, cpu_rounds):
@@ -477,8 +478,8 @@ def main():
         result["roofline_c3"] = result["roofline"]
         st_ach = c4["streamed"] / (c4["ms"] * 1e-3) / 1e9
         result["roofline"] = {
-            "kernel": "k_knn_2phase<5,8> (mapping 5-NN correspondence search, exact radius 1 m: fine 0.3 m block, "
-                      "then the 1.025 m block for unsettled queries)",
+            "kernel": f"{c4['kernel']} (as reported by aloam_knn_kernel; mapping 5-NN correspondence search, exact "
+                      "radius 1 m: fine 0.3 m block, then the 1.025 m block for unsettled queries)",
             "config": f"C4: 128-line sweep ({c4['queries']} queries) vs {c4['map_points']}-point local map (BASELINE configs[3])",
             "bound": "l2",
             "achieved": round(st_ach, 1),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ALOAM_ABI_VERSION 4
+#define ALOAM_ABI_VERSION 5
 
 /* error codes */
 #define ALOAM_OK             0
@@ -242,9 +242,14 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
  * local map): d_pts / d_queries are device float4 (x, y, z, w) arrays, d_idx / d_d2 device arrays
  * of nq * k; the index is built in context memory grown on demand. Synchronous. Two-phase: a fine
  * grid's 3x3x3 block first (exact when the k-th neighbour is closer than 0.99 fine cells), the
- * radius-edge block for the rest; ALOAM_KNN_FINE = fine cell / radius (default 0.3; 0 = one phase). */
+ * radius-edge block for the rest; ALOAM_KNN_FINE = fine cell / radius (default 0.3; 0 = one phase).
+ * Replaces the KdTreeFLANN::nearestKSearch calls of laserMapping.cpp:582,648 at C4 scale. */
 int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k,
                      float radius, int* d_idx, float* d_d2);
+/* Name of the search kernel the context's last aloam_knn_device call launched (e.g. "k_knn_2phase<5,8>";
+ * "" before the first call), so a timing of that call can be attributed to a kernel. ALOAM_KNN_TILE=1
+ * (read per call) selects the LDS-tiled phase 1 ("k_knn_tile<...>"). Valid until the next call. */
+const char* aloam_knn_kernel(const aloam_ctx* ctx);
 
 /* TicToc stage names of the reference (printf'ed per scan), as indices of aloam_timing.tictoc_ms */
 #define ALOAM_TT_PREPARE            0   /* "prepare time"              scanRegistration.cpp:128-254 */

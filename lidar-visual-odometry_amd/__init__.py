@@ -39,6 +39,8 @@ def _declare(L):
     L.aloam_destroy.argtypes = [vp]
     L.aloam_last_error.restype = C.c_char_p
     L.aloam_last_error.argtypes = [vp]
+    L.aloam_knn_kernel.restype = C.c_char_p
+    L.aloam_knn_kernel.argtypes = [vp]
     L.aloam_scan_registration.argtypes = [vp, C.c_void_p, C.c_int, C.c_int]
     L.aloam_feature_counts.argtypes = [vp, I]
     L.aloam_get_features.argtypes = [vp, C.POINTER(abi.Features)]
@@ -130,7 +132,7 @@ EXPORTED_SYMBOLS = [
     "aloam_scan_registration_pc2", "aloam_set_cu_mask", "aloam_serial_sort_fallbacks",
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
-    "aloam_map_high_freq_pose",
+    "aloam_map_high_freq_pose", "aloam_knn_kernel",
 ]
 
 
@@ -316,6 +318,10 @@ class Context:
         """aloam_knn_device on device pointers (ints, e.g. torch tensor .data_ptr())."""
         self._check(lib().aloam_knn_device(self.h, C.c_void_p(d_pts), int(n), C.c_void_p(d_queries), int(nq), int(k),
                                            float(radius), C.c_void_p(d_idx), C.c_void_p(d_d2)))
+
+    def knn_kernel(self):
+        """Name of the search kernel the last knn_device call launched (aloam_knn_kernel)."""
+        return lib().aloam_knn_kernel(self.h).decode()
 
     # ---- scan-to-map registration, sharded over ranks (laserMapping.cpp:556-727; BASELINE configs[3]) ----
     @staticmethod

@@ -1473,6 +1473,11 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
     API_END
 }
 
+const char* aloam_knn_kernel(const aloam_ctx* ctx) {
+    if (!ctx) return "";
+    return reinterpret_cast<const Ctx*>(ctx)->knn_kernel;
+}
+
 int aloam_serial_sort_fallbacks(unsigned long long* count) {
     if (!count) return ALOAM_E_ARG;
     try {

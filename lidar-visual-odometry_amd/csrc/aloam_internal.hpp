@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <chrono>
+#include <cstdio>
 #include <functional>
 #include <string>
 #include <mutex>
@@ -174,6 +175,7 @@ struct Ctx {
     Grid g_corner_fine, g_surf_fine;  // fine grids of the last clouds (first 1-NN phase, k_odom.hip)
     Grid g_knn;                     // aloam_knn_device (grown on demand): radius-edge cells
     Grid g_knn_fine;                // its fine grid (first search phase, k_knn_2phase)
+    char knn_kernel[48] = "";        // the search kernel the last aloam_knn_device call launched
     int* d_knn_n = nullptr;
     aloam_factor* d_factors = nullptr;
     int cap_factors = 0;

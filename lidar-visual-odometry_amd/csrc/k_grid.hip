@@ -489,7 +489,7 @@ __global__ void __launch_bounds__(256) k_knn_tile(const GridDesc* __restrict__ f
                                                   const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
                                                   const int* __restrict__ cstart, const float4* __restrict__ cpts,
                                                   const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
-                                                  float* __restrict__ d2, unsigned long long* cand) {
+                                                  float* __restrict__ d2, unsigned long long* cand, int max_pts) {
     constexpr int T = 256 / GS;
     __shared__ int tabs[T][20];
     __shared__ int lstart[KT_MAXC + 1];
@@ -537,7 +537,7 @@ __global__ void __launch_bounds__(256) k_knn_tile(const GridDesc* __restrict__ f
             const int len = tid < nrow ? rowg[tid] - rows0[tid] : 0;
             const int inc = wave_incl_scan(len);
             if (tid < nrow) rowoff[tid + 1] = inc;
-            if (tid == 0) { rowoff[0] = 0; tile_ok = readlane_i(inc, WAVE - 1) <= KT_MAXP; }
+            if (tid == 0) { rowoff[0] = 0; tile_ok = readlane_i(inc, WAVE - 1) <= max_pts; }
         }
         __syncthreads();
         ok = tile_ok != 0;
@@ -601,9 +601,18 @@ template <int GS>
 static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int nq, int k, float r2, int* idx, float* d2,
                               unsigned long long* cand) {
     const int blocks = (int)(((long long)nq * GS + 255) / 256);
-    static const bool tile = getenv("ALOAM_KNN_TILE") == nullptr || atoi(getenv("ALOAM_KNN_TILE")) != 0;   // A/B knob
+    // A/B knob, read per call (tests run both kernels in one process). Default: phase 1 from global memory —
+    // measured on one MI355X (C4, 50 launches): k_knn_2phase 91.5 us vs k_knn_tile 134.1 us per launch
+    // (profiles/r05_ab.txt): the tile's serial bbox -> row scan -> copy chain before any distance costs more
+    // than the L2 gathers it replaces.
+    const char* te = getenv("ALOAM_KNN_TILE");
+    const int tmode = te ? atoi(te) : 0;
+    const bool tile = tmode != 0;
+    // ALOAM_KNN_TILE=2 (tests): every tile takes the over-budget path (phase 1 from global memory in k_knn_tile)
+    const int max_pts = tmode == 2 ? -1 : KT_MAXP;
+    std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "%s<%d,%d>", tile ? "k_knn_tile" : "k_knn_2phase", k <= 5 ? 5 : 8, GS);
     if (tile) {
-#define KNNT(KK, CN) k_knn_tile<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+#define KNNT(KK, CN) k_knn_tile<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, max_pts)
         if (k <= 5) { if (cand) KNNT(5, true); else KNNT(5, false); }
         else { if (cand) KNNT(8, true); else KNNT(8, false); }
 #undef KNNT
@@ -643,6 +652,7 @@ void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float ra
     if (nq <= 0) return;
     const float r2 = radius * radius;
     static const int gs = getenv("ALOAM_KNN_GS") ? atoi(getenv("ALOAM_KNN_GS")) : 8;   // tuning knob
+    std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_group<%d,%d>", k <= 5 ? 5 : 8, gs);
     if (gs == 64) knn_group_launch<64>(C, g, q, nq, k, r2, idx, d2, cand);
     else if (gs == 32) knn_group_launch<32>(C, g, q, nq, k, r2, idx, d2, cand);
     else if (gs == 16) knn_group_launch<16>(C, g, q, nq, k, r2, idx, d2, cand);
