@@ -126,7 +126,9 @@ __device__ __forceinline__ unsigned ls_median_to_first(unsigned long long* E, in
 // RS[j] for j < k as lane gathers, the cut from k. Depth exhausted: heap sort (std::__partial_sort) of the
 // remaining > 16 sub-segments by one lane each. Then every final sub-segment of <= 16 is stably ranked (the
 // final insertion sort) and written back.
-__device__ __forceinline__ void ws_small(unsigned long long* E, const int f, const int m, int d, const unsigned* rel = nullptr) {
+// fb (may be null): LDS bytes at 2 x position free for the heap sorts' child flags (the RS region of the segment)
+__device__ __forceinline__ void ws_small(unsigned long long* E, const int f, const int m, int d, const unsigned* rel = nullptr,
+                                         unsigned char* fb = nullptr) {
     const int lane = lane_id();
     const unsigned long long lt = lanemask_lt64(), le = lt | (1ull << lane), gt = ~le;
     const unsigned long long all = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
@@ -155,7 +157,7 @@ __device__ __forceinline__ void ws_small(unsigned long long* E, const int f, con
                 const int a2 = __builtin_ctzll(hm);
                 hm &= hm - 1ull;
                 const int b2 = readlane_i(b, a2);
-                if (ws_order_matters(E, f + a2, f + b2, rel)) ws_heap_sort(E, f + a2, f + b2, rel);
+                if (ws_order_matters(E, f + a2, f + b2, rel)) ws_heap_sort(E, f + a2, f + b2, rel, fb ? fb + 2 * (f + a2) : nullptr);
             }
             ps_wsync<true>();
             e = in ? E[f + lane] : ~0ull;
@@ -287,11 +289,11 @@ __device__ __forceinline__ void ws_segment(unsigned long long* E, int f, int l, 
     for (;;) {
         for (;;) {
             if (l - f <= WAVE) {
-                if (l - f >= 2) ws_small(E, f, l - f, d, rel);
+                if (l - f >= 2) ws_small(E, f, l - f, d, rel, (unsigned char*)RS);
                 break;
             }
-            if (d == 0) {
-                if (ws_order_matters(E, f, l, rel)) ws_heap_sort(E, f, l, rel);
+            if (d == 0) {   // the child flags in this segment's part of RS (its partitions are done)
+                if (ws_order_matters(E, f, l, rel)) ws_heap_sort(E, f, l, rel, (unsigned char*)RS + 2 * f);
                 ps_wsync<false>();
                 break;
             }
@@ -545,7 +547,8 @@ __device__ __forceinline__ void ls_sort(unsigned long long* E, const int n, cons
         const int nh = min(S.hdr[6], LS_HQ);
         for (int i = wid; i < nh; i += W) {
             const int hf = ps_u(S.hq[2 * i]), hl2 = ps_u(S.hq[2 * i + 1]);
-            if (ws_order_matters(E, hf, hl2, rel)) ws_heap_sort(E, hf, hl2, rel);
+            // child flags in the heap's own part of RS_pos (2 bytes per position; the levels are over)
+            if (ws_order_matters(E, hf, hl2, rel)) ws_heap_sort(E, hf, hl2, rel, (unsigned char*)S.rs + 2 * hf);
         }
     }
     // final insertion sort (stable, whole array): every element ranked inside its leaf (<= 16 elements

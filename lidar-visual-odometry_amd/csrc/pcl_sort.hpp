@@ -326,6 +326,103 @@ __device__ inline void ws_sort_heap_lds(unsigned long long* H, const int len, co
         ps_wsync<false>();
     }
 }
+// ---- the pops with child flags (FH: len <= FH_MAX, heap and flags in LDS) -------------------------------
+// A pop of __sort_heap moves the hole from the root along the larger-child path (the right child on a tie)
+// to a leaf, then pushes the re-inserted value v = H[hl] up while its parent's key is < v's (pcl_sort.hpp
+// ps_adjust_heap). The path depends only on which child of each path node is the larger one, so that bit
+// is kept per node (1-based node m, children 2m and 2m + 1): F[m - 1] = !(key(right) < key(left)). A pop:
+//   1. the top six levels: lane j (1..63) loads node j's bit (0 unless both children are in the heap), a
+//      ballot gives the 63 bits, and the walk m <- 2m + bit(m) runs six steps (no branch: steps past the
+//      heap are cut off afterwards); 2. the next five levels the same way from the level-6 node's
+//      subtree; 3. the path's length L = the depths whose node lies in the heap (one ballot); lane t holds
+//      path node p_t and loads x_t = H[p_t] and its sibling, every lane loads v; 4. v lands at p_J,
+//      J = #{t >= 1: !(key(x_t) < key(v))} (path keys do not increase: a prefix), p_{t-1} <- x_t for t <= J,
+//      the popped root goes to H[hl]; the only bits that change are those of p_0..p_{J-1} (their path
+//      child got a new value): lane t recomputes p_{t-1}'s bit from p_t's new value and its sibling.
+// Three LDS round trips per pop, everything else straight-line vector code: on one wave a taken branch
+// costs ~32 cycles, a dependent scalar op ~8, a readlane -> scalar -> readlane link ~41 and a dependent
+// vector op ~5 (micro/heap_bench.py), so the walks run on vector registers (fh_v launders the ballots
+// there) and nothing branches inside a pop. Same array as std::__sort_heap (first npop pops). Bits of
+// nodes whose right child left the heap are stale but never read (the heap-size test masks them).
+constexpr int FH_MAX = 4095;            // depth <= 11: a six-level and a five-level walk; flag scratch: len bytes
+#if defined(PS_HOST_EMU)
+__device__ __forceinline__ unsigned fh_v(unsigned x) { return x; }
+#else
+// the value in a vector register (the compiler then keeps what is computed from it on the vector unit)
+__device__ __forceinline__ unsigned fh_v(unsigned x) { unsigned r; asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(x)); return r; }
+#endif
+__device__ __forceinline__ unsigned long long fh_v64(unsigned long long x) {
+    return ((unsigned long long)fh_v((unsigned)(x >> 32)) << 32) | fh_v((unsigned)x);
+}
+__device__ __forceinline__ unsigned long long fh_shl1(unsigned long long x) {   // lane l <- lane l + 1 (row of 16)
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)x, 0x101, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(x >> 32), 0x101, 0xF, 0xF, false);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PS_HOST_EMU)
+#define PS_LDSP(T) __attribute__((address_space(3))) T*      // LDS pointer: ds_* instructions, not flat ones
+#else
+#define PS_LDSP(T) T*
+#endif
+template <bool DEEP>
+__device__ __forceinline__ void fh_pops(PS_LDSP(unsigned long long) H, PS_LDSP(unsigned char) F, const int len, const int npop) {
+    const int lane = lane_id();
+    const unsigned dj = lane ? 31u - (unsigned)__builtin_clz((unsigned)lane) : 0u;   // lane j: subtree node j (1-based)
+    const unsigned oj = (unsigned)lane - (1u << dj);
+    for (int i = 0; i < npop; i++) {
+        const int hl = len - 1 - i;                 // the descent's heap: 1-based nodes 1..hl; v = H[hl]
+        // 1. top six levels
+        const int jt = lane ? lane : 1;
+        const unsigned char ft = F[min(jt, len) - 1];
+        const unsigned long long Ct = fh_v64(__ballot(lane >= 1 && 2 * lane + 1 <= hl && ft));
+        unsigned m = fh_v(1u);
+#pragma unroll
+        for (int k = 0; k < 6; k++) m = (m << 1) | (unsigned)((Ct >> m) & 1ull);   // m in [64, 127]
+        // 2. five more levels below the level-6 node m
+        unsigned md = 32u;
+        if (DEEP) {
+            const unsigned nd = (m << dj) | oj;         // lane j: node j of m's subtree
+            const unsigned char fd = F[min((int)nd, len) - 1];
+            const unsigned long long Cd = fh_v64(__ballot(lane >= 1 && lane < 32 && (int)(2 * nd + 1) <= hl && fd));
+            md = fh_v(1u);
+#pragma unroll
+            for (int k = 0; k < 5; k++) md = (md << 1) | (unsigned)((Cd >> md) & 1ull);   // md in [32, 63]
+        }
+        const unsigned me = (m << 5) | (md & 31u);    // the walk's node at depth 11
+        // 3. path length and path nodes
+        const int L = __popcll(__ballot(lane <= 11 && (int)(me >> (11 - min(lane, 11))) <= hl)) - 1;
+        const unsigned p = lane <= 11 ? me >> (11 - lane) : 1u;    // lane t <= L: path node p_t
+        const unsigned sb = p ^ 1u;                                  // its sibling (t >= 1)
+        const unsigned long long x = H[min((int)p, hl + 1) - 1];
+        const unsigned long long sv = H[max(min((int)sb, hl + 1), 1) - 1];
+        const unsigned long long v = H[hl], root = H[0];            // (every lane: broadcast reads)
+        const unsigned vk = ps_key(v);
+        // 4. v's slot, the moves, the bits
+        const int J = __popcll(__ballot(lane >= 1 && lane <= L && !(ps_key(x) < vk)));
+        const unsigned long long xs = fh_shl1(x);                   // x_{t+1} in lane t (every lane: a collective)
+        const unsigned long long nv = lane < J ? xs : v;            // p_t's new value (t <= J)
+        const unsigned sk = ps_key(sv), nk = ps_key(nv);
+        const unsigned char nf = (p & 1u) ? !(nk < sk) : !(sk < nk);   // p_{t-1}'s bit (p_t odd: the right child)
+        // every lane stores (no exec-mask branches): lanes t <= J their path node, the others the popped
+        // root into H[hl] (all the same value) and their bit into node hl + 1's byte, which no later pop
+        // reads (the heap only shrinks)
+        const bool wf = lane >= 1 && lane <= J && (int)sb <= hl;
+        F[wf ? (int)(p >> 1) - 1 : hl] = nf;
+        *(lane <= J ? H + (p - 1) : H + hl) = lane <= J ? nv : root;
+        ps_wsync<false>();
+    }
+}
+__device__ inline void fh_sort_heap_lds(unsigned long long* Hg, unsigned char* Fg, const int len_, const int npop_) {
+    PS_LDSP(unsigned long long) H = (PS_LDSP(unsigned long long))Hg;
+    PS_LDSP(unsigned char) F = (PS_LDSP(unsigned char))Fg;
+    const int len = ps_u(len_), npop = ps_u(npop_);
+    // the bits of every node with two children (1-based m: children 2m, 2m + 1 = 0-based 2m - 1, 2m)
+    for (int m = lane_id() + 1; 2 * m + 1 <= len; m += WAVE) F[m - 1] = !(ps_key(H[2 * m]) < ps_key(H[2 * m - 1]));
+    ps_wsync<false>();
+    if (len > 127) fh_pops<true>(H, F, len, npop);
+    else fh_pops<false>(H, F, len, npop);
+}
+
 // std::__partial_sort(E + f, E + l, E + l) (= __make_heap + __sort_heap) by one wave, E in LDS or global.
 // __make_heap adjusts the parents (len - 2) / 2 .. 0 in turn; parents of one depth have disjoint subtrees,
 // so each depth runs on the lanes at once, deepest first. With rel (rvg.hpp), only the order of the
@@ -410,10 +507,11 @@ __device__ inline bool ws_heap_postorder(unsigned long long* H, const int len, c
     return true;
 }
 
-__device__ __noinline__ void ws_heap_sort(unsigned long long* E, const int f, const int l, const unsigned* rel) {
-    const int len = l - f;
+__device__ __noinline__ void ws_heap_sort(unsigned long long* E, const int f, const int l, const unsigned* rel,
+                                          unsigned char* fscr = nullptr) {
+    const int len = ps_u(l - f);          // scalar (arguments arrive in VGPRs): uniform loops, no exec masks
     if (len < 2) return;
-    unsigned long long* H = E + f;
+    unsigned long long* H = E + ps_u(f);
     const int lane = lane_id();
     int npop = len - 1;
     if (rel) {
@@ -441,8 +539,12 @@ __device__ __noinline__ void ws_heap_sort(unsigned long long* E, const int f, co
         if (lds) ps_wsync<false>(); else ps_wsync<true>();
     }
     if (rel && len <= 16 * WAVE && ws_heap_postorder(H, len, npop, rel)) return;
+#ifdef PS_NO_FH                              // A/B builds: the six-level pops everywhere
+    fscr = nullptr;
+#endif
     if (lds) {
-        ws_sort_heap_lds(H, len, npop);
+        if (fscr && len <= FH_MAX) fh_sort_heap_lds(H, fscr, len, npop);   // fscr: len bytes of LDS
+        else ws_sort_heap_lds(H, len, npop);
         return;
     }
     for (int i = 0; i < npop; i++) {

@@ -88,6 +88,14 @@ static inline int __shfl(int v, int src, int) {
     return (int)wave_collect((unsigned long long)(unsigned)v, [src](const unsigned long long* s) { return s[src & 63]; });
 }
 static inline int __builtin_amdgcn_readfirstlane(int v) { return aloam::readlane_i(v, 0); }
+// DPP row_shl:N (ctrl 0x101..0x10f) only: lane l takes lane l + N of its row of 16, else `old`
+static inline int __builtin_amdgcn_update_dpp(int old, int src, int ctrl, int, int, bool) {
+    const int sh = ctrl - 0x100;
+    if (sh < 1 || sh > 15) std::abort();
+    return (int)wave_collect((unsigned long long)(unsigned)src, [&](const unsigned long long* s) {
+        return (t_lane & 15) + sh < 16 ? s[t_lane + sh] : (unsigned long long)(unsigned)old;
+    });
+}
 static inline void __builtin_amdgcn_wave_barrier() { wave_sync(); }
 static inline void __builtin_amdgcn_fence(int, const char*) { std::atomic_thread_fence(std::memory_order_seq_cst); }
 static inline void __builtin_amdgcn_s_sleep(int) { std::this_thread::yield(); }
@@ -203,10 +211,12 @@ static void run_ls_global(std::vector<unsigned long long>& E, int cap) {
 // csrc/pcl_sort.hpp's wave heap sort (ws_heap_sort: closed form or six-level pops, early stop) on one
 // emulated wave against libstdc++'s heap sort (std::partial_sort(f, l, l) = make_heap + sort_heap): every
 // >= 3-point key's points in the same order. Mode 4.
-static int heap_trials(int trials, std::mt19937_64& rng) {
+// Mode 6: the same with the child-flag pops (fh_sort_heap_lds, flag bytes passed as fscr) up to FH_MAX points;
+// every other trial without rel (all pops: the whole array must equal libstdc++'s).
+static int heap_trials(int trials, std::mt19937_64& rng, bool flags = false) {
     int bad = 0;
     for (int t = 0; t < trials; t++) {
-        const int n = 17 + (int)(rng() % 1000);
+        const int n = flags ? 2 + (int)(rng() % (t % 3 == 0 ? 200 : aloam::FH_MAX - 1)) : 17 + (int)(rng() % 1000);
         const unsigned kinds = 2 + (unsigned)(rng() % (unsigned)(t % 2 ? n / 3 + 1 : 4 * n));
         std::vector<unsigned long long> E(n);
         for (int i = 0; i < n; i++) E[i] = ((unsigned long long)(unsigned)(rng() % kinds) << 32) | (unsigned)i;
@@ -231,9 +241,15 @@ static int heap_trials(int trials, std::mt19937_64& rng) {
         g_waves.push_back(std::move(c));
         g_block = std::make_unique<std::barrier<>>(WAVE);
         std::vector<std::thread> th;
+        std::vector<unsigned char> F(n, 0xee);
+        const bool all = flags && t % 2 == 0;
         for (int l = 0; l < WAVE; l++)
-            th.emplace_back([&, l] { threadIdx.x = l; t_lane = l; t_wave = 0; aloam::ws_heap_sort(E.data(), 0, n, rel.data()); });
+            th.emplace_back([&, l] {
+                threadIdx.x = l; t_lane = l; t_wave = 0;
+                aloam::ws_heap_sort(E.data(), 0, n, all ? nullptr : rel.data(), flags ? F.data() : nullptr);
+            });
         for (auto& x : th) x.join();
+        if (all && E != A) { bad++; std::printf("heap (all pops) mismatch trial %d n %d kinds %u\n", t, n, kinds); continue; }
         auto order = [&](const std::vector<unsigned long long>& X) {
             std::vector<std::pair<unsigned, unsigned>> v;
             for (auto x : X) if (cnt[(unsigned)(x >> 32)] >= 3) v.push_back({(unsigned)(x >> 32), (unsigned)x & 0xffffu});
@@ -326,8 +342,8 @@ int main(int argc, char** argv) {
         std::printf("trials %d mismatches %d\n", trials, bad);
         return bad != 0;
     }
-    if (lsm == 4) {
-        bad = heap_trials(trials, rng);
+    if (lsm == 4 || lsm == 6) {
+        bad = heap_trials(trials, rng, lsm == 6);
         std::printf("postorder segments %ld\n", (long)g_postorder.load());
         std::printf("trials %d mismatches %d\n", trials, bad);
         return bad != 0;

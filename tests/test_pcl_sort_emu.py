@@ -77,6 +77,16 @@ def test_wave_heap_sort_orders_relevant_keys_like_libstdcxx(emu):
     assert "postorder segments 0" not in r.stdout
 
 
+def test_flag_heap_pops_match_libstdcxx(emu):
+    # csrc/pcl_sort.hpp fh_sort_heap_lds (the pops walked on per-node child flags: top six levels from a scalar
+    # copy, deeper ones six at a time by a ballot, path values moved by their lanes) on one emulated wave, up
+    # to FH_MAX = 4095 points: with every pop the whole array must equal libstdc++'s heap sort; with the
+    # relevance early stop every >= 3-point key's points must be in its order
+    r = subprocess.run([emu, "16", "71", "6"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
+
+
 def test_batched_leaf_sums_match_the_leaf_loop(emu):
     # csrc/rvg.hpp rvg_reduce_batched (the map filter's leaf sums: chunk entries and points loaded in batches,
     # leaves summed from registers, relevant leaves in fpos order) against the leaf-at-a-time loop on one
