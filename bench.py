@@ -409,6 +409,8 @@ def main():
             "tictoc_ms": {lvo.abi.TICTOC_NAMES[i]: round(float(tt2[i] / tn2[i]), 4) for i in range(8, NT) if tn2[i]},
             "map_total_points": int(last_mp["map_total_points"]) if last_mp is not None else None,
             "surround_points": int(last_mp["map_corner_num"] + last_mp["map_surf_num"]) if last_mp is not None else None,
+            # stack points without a round-cache slot (they search the grid every round; aloam_map_result)
+            "uncached_queries": int(last_mp["uncached_queries"]) if last_mp is not None else None,
         }
 
     value = lvo.replicas.aggregate_rate(K, world, elapsed)
@@ -545,10 +547,12 @@ def main():
                 "box": {"value": round(cb["box"]["scans_per_s"], 3), "cores": cb["box"]["cores"],
                         "note": f"{cb['box']['cores']} independent sequences, one pinned process per core, "
                                 f"{cb['box']['frames_per_sequence']} timed frames each",
-                        # SURVEY §8(d)'s P = nproc form, extrapolated from the measured per-core rate (context:
-                        # the box's host shares its cores with other jobs, so all of them were not timed)
-                        "host_nproc": os.cpu_count(),
-                        "full_host_est": round(cb["box"]["scans_per_s"] / max(1, cb["box"]["cores"]) * (os.cpu_count() or 1), 1)},
+                        # SURVEY §8(d)'s P = nproc form: NOT measured. The per-process rate of the pinned cores times
+                        # os.cpu_count(), which counts SMT hardware threads as full cores and assumes perfect scaling
+                        # (the box's host shares its cores with other jobs, so all of them were not timed): an upper
+                        # bound for context only; gpu_vs_cpu_box uses the measured value above
+                        "host_nproc_hw_threads": os.cpu_count(),
+                        "full_host_hw_thread_extrapolation": round(cb["box"]["scans_per_s"] / max(1, cb["box"]["cores"]) * (os.cpu_count() or 1), 1)},
                 "tictoc_ms": cb["serial"]["tictoc_ms"],
             }
             otraj = cb["traj"]

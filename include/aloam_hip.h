@@ -128,6 +128,8 @@ typedef struct aloam_map_result {
     int    frame_count;         /* frameCount of this frame: mapping frames processed before it      */
     int    pub_surround;        /* frameCount % 5 == 0: /laser_cloud_surround is published (:806)     */
     int    pub_map;             /* frameCount % 20 == 0: /laser_cloud_map is published (:823)         */
+    int    uncached_queries;    /* stack points beyond the rounds' candidate-cache slots (65,536): they
+                                 * search the map grid in every round (exact, slower); 0 on HDL-64       */
 } aloam_map_result;
 
 /* One residual block of lidarFactor.hpp, flattened.
@@ -297,7 +299,9 @@ int aloam_get_timing(aloam_ctx* ctx, aloam_timing* t);
 int aloam_set_cu_mask(aloam_ctx* ctx, const unsigned* mask, int nwords);
 /* Number of VoxelGrid / segment sorts (process-wide, all contexts on the current device) that exceeded
  * the workgroup replay's reach (n > 65,536) and ran the exact one-thread std::sort instead: correct but
- * slow, so a workload that reaches it is visible (bench.py reports it). */
+ * slow, so a workload that reaches it is visible (bench.py reports it). Blocking: it reads the device
+ * counters with a synchronous copy on the CALLING thread's current HIP device (call it between frames,
+ * with that device current). */
 int aloam_serial_sort_fallbacks(unsigned long long* count);
 
 /* ---- native pipeline: the reference's node split on one GPU ---------------------------------

@@ -100,6 +100,7 @@ class MapResult(C.Structure):
         ("map_total_points", C.c_int),
         ("q_wmap_wodom", C.c_double * 4), ("t_wmap_wodom", C.c_double * 3),
         ("frame_count", C.c_int), ("pub_surround", C.c_int), ("pub_map", C.c_int),
+        ("uncached_queries", C.c_int),
     ]
 
 
@@ -225,6 +226,7 @@ def map_to_dict(r):
         "map_total_points": r.map_total_points,
         "q_wmap_wodom": np.array(r.q_wmap_wodom[:]), "t_wmap_wodom": np.array(r.t_wmap_wodom[:]),
         "frame_count": r.frame_count, "pub_surround": r.pub_surround, "pub_map": r.pub_map,
+        "uncached_queries": r.uncached_queries,
     }
 
 

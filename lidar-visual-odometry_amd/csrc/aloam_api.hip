@@ -207,7 +207,9 @@ static void allocate(Ctx& C) {
     rebuild_init(C);                                              // map rebuild's run tables: reset
     grid_alloc(C, C.g_map_corner, M, 1.0f * 1.025f, 1, true);     // 5-NN within 1 m, 3x3x3 cells
     grid_alloc(C, C.g_map_surf, M, 1.0f * 1.025f, 1, true);
-    // candidate cache of the registration rounds: stack points beyond cap_mq always search the grid
+    // candidate cache of the registration rounds: stack points beyond cap_mq always search the grid (exact, but
+    // a full 27-cell search per round; reported per frame as aloam_map_result.uncached_queries). 65,536 slots
+    // hold every HDL-64 stack (~20k points); 1,280 B per slot
     C.cap_mq = std::min(C.cap_factors, 1 << 16);
     C.d_mc_ctr = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_mq);
     C.d_mc_pts = (float4*)dalloc(C, sizeof(float4) * (size_t)C.cap_mq * MC_CAP_PTS);
@@ -763,6 +765,7 @@ void mapping_complete(Ctx& C, aloam_map_result* R) {
     r.frame_count = C.m_frame[slot];
     r.pub_surround = r.frame_count % 5 == 0;      // laserMapping.cpp:806
     r.pub_map = r.frame_count % 20 == 0;          // :823
+    r.uncached_queries = std::max(0, stackn[0] + stackn[1] - C.cap_mq);   //  no cache slot: full search every round
     {
         std::lock_guard<std::mutex> g(C.hf_mu);
         std::memcpy(C.hf_q, r.q_wmap_wodom, sizeof(C.hf_q));

@@ -191,6 +191,11 @@ constexpr int FIT_BLOCKS = 160;     // k_map_fit: 40960 lanes, one stack point e
 // list is exactly the grid search's result (same (d2, index) order). Otherwise the query searches
 // the grid again and re-centres its cache. A query whose 5 neighbours (in order) equal the previous
 // round's keeps its factor: the fit reads nothing but those 5 map points and the stack point.
+// Invariant of that reuse: between the rounds of one mapping frame nothing else writes the
+// factor slots (C.d_factors). They are shared with the odometry rounds and the eval / solve test entry
+// points of the same context, but all of those run on the context's one stream (C.stream), and a frame's
+// rounds are issued back to back (one graph); round 0 searches every query and rewrites every slot, so no
+// factor of an earlier frame or call is ever reused.
 constexpr int MC_CAP = MC_CAP_PTS;  // cached points per query (p99 45, 1e-4 above 64 at MC_M = 0.1; more => full search)
 constexpr float MC_M = 0.1f;        // reuse radius (m)
 constexpr float MC_EPS = 2e-3f;     // fp32 slack of the distance and cell tests (coordinates << 2^13 m)
