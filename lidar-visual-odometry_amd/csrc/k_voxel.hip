@@ -15,7 +15,11 @@
 #ifdef ALOAM_PS_TIMING           // profiling builds only: per-level stamps of the sort of workgroup 0
 __device__ unsigned long long g_ps_ts[64][6];
 __device__ int g_ps_nseg[64];
-#define PS_TS(level, k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && (level) < 64) { g_ps_ts[level][k] = wall_clock64(); if ((k) == 0) g_ps_nseg[level] = hdr[(level) == 60 ? 2 : 0]; } } while (0)
+#define PS_TS(level, k) do { if (threadIdx.x == 0 && blockIdx.x == 1 && (level) < 64) { g_ps_ts[level][k] = wall_clock64(); if ((k) == 0) g_ps_nseg[level] = hdr[(level) == 60 ? 2 : 0]; } } while (0)
+// k_vox_pcl phases per job (blockIdx.x): start, bbox, keys, sort / split, reduce, and n in slot 7
+__device__ unsigned long long g_vx_ts[2][8];
+#define VX_TS(k) do { if (threadIdx.x == 0) g_vx_ts[blockIdx.x & 1][k] = wall_clock64(); } while (0)
+extern "C" int aloam_dbg_vx_ts(unsigned long long* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vx_ts), sizeof(g_vx_ts)); }
 __device__ unsigned long long g_ps_w[16][8];
 #define PS_CLK() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #define PS_WSTAT(slot, v) do { if (blockIdx.x == 0) { auto& w_ = g_ps_w[threadIdx.x / 64][slot]; w_ = w_ + (unsigned long long)(v); } } while (0)
@@ -30,6 +34,8 @@ extern "C" int aloam_dbg_ps_ts(unsigned long long* out, int* nseg) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ps_ts), sizeof(g_ps_ts)) != hipSuccess) return -1;
     return (int)hipMemcpyFromSymbol(nseg, HIP_SYMBOL(g_ps_nseg), sizeof(g_ps_nseg));
 }
+#else
+#define VX_TS(k) do { } while (0)
 #endif
 #include "ls_sort.hpp"
 
@@ -55,7 +61,10 @@ struct VoxJobs { VoxJob j[2]; };
 // g_vox_seg elements, k_vox_seg sorts the segments in parallel (VX_SEGW workgroups per cloud), k_vox_reduce
 // sums the leaves.
 constexpr int VX_SEGW = 16;
-static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(2048, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : 4096;   // tuning knob
+// tuning knob: split segments of at most this many elements (round 5, C3 pipeline, 2 x 20 / 50 steps on one box:
+// 10240 -> 846-850 / 936-937 scans/s vs 4096 -> 835-837 / 932-935, map prepare 0.17 vs 0.21 ms: fewer split
+// levels on one workgroup (~55 us each, micro/vx_stamps.py) for larger LDS sorts of the segments)
+static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(2048, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : VX_LDS_N;
 // tuning knob: clouds up to this size are sorted whole by their own workgroup, larger ones split
 static const int g_vox_fit = getenv("ALOAM_VOX_FIT") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_FIT")))) : VX_LDS_N;
 static_assert(ls_split_scratch_bytes(VX_T, VX_LDS_N) <= ls_global_scratch_bytes(VX_T, VX_LDS_N), "split scratch");
@@ -91,6 +100,10 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int 
     const int tid = threadIdx.x;
     // a hinted launch never reads past its launch size (the exact-size redo replaces the result)
     const int n = min(*J.d_n, J.cap);
+    VX_TS(0);
+#ifdef ALOAM_PS_TIMING
+    if (tid == 0) g_vx_ts[blockIdx.x & 1][7] = (unsigned long long)n;
+#endif
     if (n <= fit || n > VX_NMAX) { if (tid == 0) J.gseg[0] = 0; }   // done here (the others: split)
     if (n <= 0) { if (tid == 0) *J.d_nout = 0; return; }
     if (tid < 6) bb[tid] = tid < 3 ? 0xffffffffu : 0u;
@@ -110,6 +123,7 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int 
         }
     }
     __syncthreads();
+    VX_TS(1);
     bool ovf;
     int minb[3], mul1, mul2;
     voxel_params(bb, J.leaf, &ovf, minb, &mul1, &mul2);
@@ -122,15 +136,20 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int 
     if (n <= fit) {
         for (int t = tid; t < n; t += VX_T) EL[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
         lds_barrier();
+        VX_TS(2);
         ls_sort<VX_T, VX_CPW>(EL, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, VX_LDS_N);
+        VX_TS(3);
         vox_reduce(J, n, EL, sc);
+        VX_TS(4);
         return;
     }
     unsigned long long* E = J.gE;
     for (int t = tid; t < n; t += VX_T) E[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
     __syncthreads();
+    VX_TS(2);
     if (n <= VX_NMAX) {
         ls_split_to_list<VX_T>(E, n, seg_limit, J.gseg, (unsigned char*)sc);   // -> k_vox_seg, k_vox_reduce
+        VX_TS(3);
         return;
     }
     if (tid == 0) ps_serial_std_sort(E, n);   // beyond the parallel replay's reach: one thread (rare)
