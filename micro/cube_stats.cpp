@@ -22,6 +22,7 @@ struct Acc {
     long maxn = 0, heap_max = 0, matter_max = 0;
     long part_full = 0, part_pruned = 0, depth_full = 0, depth_pruned = 0;   // elements partitioned; max recursion depth
     long heap_steps_full = 0, heap_steps_pruned = 0, heap_steps_max_full = 0, heap_steps_max_pruned = 0;
+    long sw_pops = 0, sw_max = 0, sw_segs = 0, sw_ok = 0, sw_bad = 0, es_pops = 0, es_max = 0;   // safe-switch analysis
     long po_segs = 0, po_grab = 0, po_ok = 0, po_bad = 0, po_grab_g = 0, po_safe = 0, po_safe_ok = 0, po_noown = 0, po_noown_ok = 0;   // post-order closed form checks
 };
 Acc acc[5], frame_acc[5];
@@ -45,6 +46,7 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
     const long len = last - first;
     // make_heap
     if (len >= 2) { long parent = (len - 2) / 2; while (true) { T v = first[parent]; orc::adjust_heap(first, parent, len, v, less); if (parent == 0) break; parent--; } }
+    const std::vector<T> hcopy(first, first + len);
     // conservative no-grab check per group: no member of G in the last c_G slots after make_heap
     std::map<unsigned, bool> safe;
     for (auto& kv : rel) {
@@ -85,6 +87,43 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
         orc::adjust_heap(first, 0L, l, v, less);
     }
     A.po_segs++;
+    // safe-switch analysis (a device design's prototype): pops until no relevant group has a member in its
+    // danger window [len - c_G, h) (the window start stays fixed while G is popped: every pop takes an element
+    // >= K_G and shrinks the heap by one), then the post-order closed form of the CURRENT heap for the rest.
+    // Counts the pops simulated before the switch against the early-stop count, and checks the prediction.
+    {
+        std::vector<T> H(hcopy.begin(), hcopy.end());
+        std::map<unsigned, long> wG;
+        for (auto& kv : rel) { long cg = 0; for (long p = 0; p < len; p++) cg += H[p].idx >= kv.first; wG[kv.first] = len - cg; }
+        long h = len, isafe = -1;
+        for (long i = 0; h > 1; i++) {
+            bool danger = false;
+            for (long p = 0; p < h && !danger; p++) {
+                auto it = wG.find(H[p].idx);
+                if (it != wG.end() && p >= it->second) danger = true;
+            }
+            if (!danger) { isafe = i; break; }
+            --h; T v = H[h]; H[h] = H[0]; orc::adjust_heap(H.data(), 0L, h, v, less);
+        }
+        if (isafe < 0) isafe = len - 1;
+        isafe = std::min(isafe, std::min(len - 1, cmin));     // never more than the early stop's pops
+        A.sw_pops += isafe; A.sw_max = std::max(A.sw_max, isafe); A.sw_segs++;
+        A.es_pops += std::min(len - 1, cmin); A.es_max = std::max(A.es_max, std::min(len - 1, cmin));
+        // prediction: members still in [0, h) in post-order of their slots, then the popped ones in slot order
+        std::map<unsigned, std::vector<unsigned>> pr;
+        std::function<void(long)> post2 = [&](long x) {
+            if (x >= h) return;
+            post2(2 * x + 1); post2(2 * x + 2);
+            if (rel.count(H[x].idx)) pr[H[x].idx].push_back(H[x].ci);
+        };
+        post2(0);
+        for (long p = h; p < len; p++) if (rel.count(H[p].idx)) pr[H[p].idx].push_back(H[p].ci);
+        for (auto& kv : rel) {
+            std::vector<unsigned> got;
+            for (long p = 0; p < len; p++) if (first[p].idx == kv.first) got.push_back(first[p].ci);
+            if (got == pr[kv.first]) A.sw_ok++; else A.sw_bad++;
+        }
+    }
     bool anyg = false;
     for (auto& kv : rel) {
         std::vector<unsigned> got;
@@ -348,6 +387,8 @@ int main(int argc, char** argv) {
             t.heap_steps_max_full = std::max(t.heap_steps_max_full, a.heap_steps_max_full); t.heap_steps_max_pruned = std::max(t.heap_steps_max_pruned, a.heap_steps_max_pruned);
             t.po_safe += a.po_safe; t.po_safe_ok += a.po_safe_ok; t.po_noown += a.po_noown; t.po_noown_ok += a.po_noown_ok;
             t.po_segs += a.po_segs; t.po_grab += a.po_grab; t.po_ok += a.po_ok; t.po_bad += a.po_bad; t.po_grab_g += a.po_grab_g;
+            t.sw_pops += a.sw_pops; t.sw_max = std::max(t.sw_max, a.sw_max); t.sw_segs += a.sw_segs; t.sw_ok += a.sw_ok; t.sw_bad += a.sw_bad;
+            t.es_pops += a.es_pops; t.es_max = std::max(t.es_max, a.es_max);
             t.heap_matter_segs += a.heap_matter_segs; t.maxn = std::max(t.maxn, a.maxn); t.heap_max = std::max(t.heap_max, a.heap_max); t.matter_max = std::max(t.matter_max, a.matter_max);
             if ((k + 1) % every == 0)
                 printf("frame %3d %s: cubes %ld (unique-sorted %ld, with >=3 leaf %ld, heap %ld, heap-order-matters %ld) pts %ld max %ld | "
@@ -370,6 +411,8 @@ int main(int argc, char** argv) {
                t.heap_steps_pruned, t.heap_steps_max_pruned);
         printf("POSTORDER %s: relevant heap segments %ld (with a grab %ld) | groups predicted ok %ld wrong %ld grabbed %ld | safe %ld (post-order right %ld) | no own-member grab %ld (right %ld)\n",
                NM[w], t.po_segs, t.po_grab, t.po_ok, t.po_bad, t.po_grab_g, t.po_safe, t.po_safe_ok, t.po_noown, t.po_noown_ok);
+        printf("SWITCH %s: relevant heap segments %ld | pops: early stop %ld (max %ld), safe switch %ld (max %ld) | prediction right %ld wrong %ld\n",
+               NM[w], t.sw_segs, t.es_pops, t.es_max, t.sw_pops, t.sw_max, t.sw_ok, t.sw_bad);
     }
     if (getenv("CS_RVG")) printf("RVG: %ld cube filters, %ld differ from PCL order\n", stats::g_rvg_calls, stats::g_rvg_bad);
     oracle_destroy(o);
