@@ -61,6 +61,7 @@ struct LMState {
     double cost, initial_cost;
     double scale[6], diag[6];
     double radius, decrease_factor, x_norm, mcc, step_norm;
+    double inv_radius, inv_mcc;    // k_lm_coop's tail: 1 / radius (the step needs only that), 1 / mcc (lm_post)
     double delta[6];               // the last step in tangent space (k_lm_coop: its model cost change and
                                    // norm are computed off the critical path, lm_post)
     int reuse_diag, iteration, done, termination, successful, nres;

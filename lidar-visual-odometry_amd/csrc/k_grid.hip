@@ -367,7 +367,7 @@ __device__ __forceinline__ int block27_total(const GridDesc& gd, const int* __re
 // dense map (C4: the 5 neighbours within ~0.15 m, ~1000 points in the coarse block) phase 1 streams
 // ~10x fewer candidates. cand (profiling): [0] += C27(q) of the coarse block (SURVEY §8(d)'s
 // algorithmic count), [1] += candidates actually streamed by both phases.
-template <int K, int GS, bool CNT>
+template <int K, int GS, bool CNT, int U = 4>
 __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
                                                     const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
                                                     const int* __restrict__ cstart, const float4* __restrict__ cpts,
@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
     int pos[K], oi[K], nf = 0, nc = 0;
     float od[K];
     const GridDesc gf = *fgd;
-    int f = group_knn27<K, GS, true>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, nullptr,
+    int f = group_knn27<K, GS, true, U>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, nullptr,
                                      qq.x, qq.y, qq.z, r2, live, pos, od, oi, &nf, tabs[threadIdx.x / GS], gf.n);
     float dk = INFINITY;
 #pragma unroll
@@ -392,8 +392,8 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
     if (__any(need)) {                         // wave-uniform: every lane takes part in the group search
         int p2[K], i2[K];
         float e2[K];
-        const int f2 = group_knn27<K, GS, true>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, nullptr,
-                                                qq.x, qq.y, qq.z, r2, need, p2, e2, i2, &nc, tabs[threadIdx.x / GS], gc.n);
+        const int f2 = group_knn27<K, GS, true, U>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, nullptr,
+                                                   qq.x, qq.y, qq.z, r2, need, p2, e2, i2, &nc, tabs[threadIdx.x / GS], gc.n);
         if (need) {
 #pragma unroll
             for (int j = 0; j < K; j++) { od[j] = e2[j]; oi[j] = i2[j]; }
@@ -618,10 +618,19 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
 #undef KNNT
         return;
     }
-    // CNT: the candidate-counting instance (profiling), a separate symbol so kernel traces tell it apart
-#define KNN2(KK, CN) k_knn_2phase<KK, GS, CN><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
-    if (k <= 5) { if (cand) KNN2(5, true); else KNN2(5, false); }
-    else { if (cand) KNN2(8, true); else KNN2(8, false); }
+    // CNT: the candidate-counting instance (profiling), a separate symbol so kernel traces tell it apart.
+    // ALOAM_KNN_U (tuning knob, read per call): candidate loads in flight per lane, 4 (default) or 8
+    const char* ue = getenv("ALOAM_KNN_U");
+    const bool u8 = ue && atoi(ue) == 8;
+#define KNN2(KK, CN, UU) k_knn_2phase<KK, GS, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+    if (u8) {
+        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<%d,%d,U8>", k <= 5 ? 5 : 8, GS);
+        if (k <= 5) { if (cand) KNN2(5, true, 8); else KNN2(5, false, 8); }
+        else { if (cand) KNN2(8, true, 8); else KNN2(8, false, 8); }
+    } else {
+        if (k <= 5) { if (cand) KNN2(5, true, 4); else KNN2(5, false, 4); }
+        else { if (cand) KNN2(8, true, 4); else KNN2(8, false, 4); }
+    }
 #undef KNN2
 }
 

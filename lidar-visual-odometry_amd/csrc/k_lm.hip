@@ -167,9 +167,9 @@ __device__ __forceinline__ void plus7(const double* x, const double* d, double* 
     if (nd2 > 0.0) {
         double sdd, cs;
         if (nd2 < 0.0625) {
-            const double y = nd2;
-            sdd = 1.0 + y * (-1.0 / 6 + y * (1.0 / 120 + y * (-1.0 / 5040 + y * (1.0 / 362880 + y * (-1.0 / 39916800 + y * (1.0 / 6227020800.0))))));
-            cs = 1.0 + y * (-0.5 + y * (1.0 / 24 + y * (-1.0 / 720 + y * (1.0 / 40320 + y * (-1.0 / 3628800 + y * (1.0 / 479001600.0 + y * (-1.0 / 87178291200.0)))))));
+            const double y = nd2;   // Horner in fused multiply-adds: half the dependent fp64 ops
+            sdd = fma(y, fma(y, fma(y, fma(y, fma(y, fma(y, 1.0 / 6227020800.0, -1.0 / 39916800), 1.0 / 362880), -1.0 / 5040), 1.0 / 120), -1.0 / 6), 1.0);
+            cs = fma(y, fma(y, fma(y, fma(y, fma(y, fma(y, fma(y, -1.0 / 87178291200.0, 1.0 / 479001600.0), -1.0 / 3628800), 1.0 / 40320), -1.0 / 720), 1.0 / 24), -0.5), 1.0);
         } else {
             const double nd = sqrt(nd2);
             double sn;
@@ -211,10 +211,12 @@ __device__ __forceinline__ double Aget(const double* A, int a, int b) {   // upp
 // 1/sqrt(s) from the hardware estimate plus three Newton steps (quadratic convergence to full
 // precision); the Cholesky pivots take this instead of a sqrt and a division each, which are the
 // longest latency chain of the serial solver tail.
+// (v_rsq_f64 is good to ~2^-23: two steps reach full precision; NR = 3 keeps the older tails' rounding)
+template <int NR = 3>
 __device__ __forceinline__ double rsqrt_nr(double s) {
     double r = __builtin_amdgcn_rsq(s);
 #pragma unroll
-    for (int it = 0; it < 3; it++) {
+    for (int it = 0; it < NR; it++) {
         const double e = fma(-(s * r), r, 1.0);
         r = fma(0.5 * r, e, r);
     }
@@ -410,7 +412,7 @@ __device__ __forceinline__ void chol_solve6_packed(const double* Ml, const doubl
 #pragma unroll
         for (int k = 0; k < j; k++) s = fma(-L[j * (j + 1) / 2 + k], L[j * (j + 1) / 2 + k], s);
         ok = ok && (s > 0.0);
-        inv[j] = rsqrt_nr(s);
+        inv[j] = rsqrt_nr<2>(s);
         L[j * (j + 1) / 2 + j] = s * inv[j];
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
@@ -439,19 +441,20 @@ __device__ __forceinline__ void chol_solve6_packed(const double* Ml, const doubl
     for (int i = 0; i < 6; i++) ok = ok && isfinite(y[i]);
     *okp = ok;
 }
-__device__ __forceinline__ void lm_next_step_fast(LMState* st, aloam_lm_summary* out, int max_iter) {
-    double A[21], g[6], sc[6], x[7];
+// The next step from the state in registers (A, g: the current normal equations; the caller passes them
+// from where they already are, so an accepted pass's records never round-trip through the LDS state):
+// 1 / radius instead of radius (ceres' radius / x and x / radius become products: no fp64 division on
+// this serial path; a division is ~200 cycles on one lane, micro/lm_tail_bench.py).
+__device__ __forceinline__ void lm_next_step_fast(LMState* st, aloam_lm_summary* out, int max_iter, const double* A, const double* g,
+                                                  double inv_radius, double decrease, int reuse, int iteration) {
+    double sc[6], x[7], dg[6];
 #pragma unroll
-    for (int i = 0; i < 21; i++) A[i] = st->A[i];
-#pragma unroll
-    for (int i = 0; i < 6; i++) { g[i] = st->g[i]; sc[i] = st->scale[i]; }
+    for (int i = 0; i < 6; i++) { sc[i] = st->scale[i]; dg[i] = st->diag[i]; }
 #pragma unroll
     for (int i = 0; i < 7; i++) x[i] = st->x[i];
-    double radius = st->radius, decrease = st->decrease_factor;
-    int reuse = st->reuse_diag, iteration = st->iteration;
     while (true) {
         if (iteration >= max_iter) {
-            st->radius = radius; st->decrease_factor = decrease; st->reuse_diag = reuse; st->iteration = iteration;
+            st->inv_radius = inv_radius; st->decrease_factor = decrease; st->reuse_diag = reuse; st->iteration = iteration;
             lm_finish(st, out, 0);
             return;
         }
@@ -465,16 +468,15 @@ __device__ __forceinline__ void lm_next_step_fast(LMState* st, aloam_lm_summary*
         }
         if (!reuse)
 #pragma unroll
-            for (int a = 0; a < 6; a++) st->diag[a] = fmin(fmax(M[a * (a + 1) / 2 + a], 1e-6), 1e32);
-        const double inv_radius = 1.0 / radius;
+            for (int a = 0; a < 6; a++) dg[a] = fmin(fmax(M[a * (a + 1) / 2 + a], 1e-6), 1e32);
 #pragma unroll
-        for (int a = 0; a < 6; a++) M[a * (a + 1) / 2 + a] += st->diag[a] * inv_radius;   // D^2 = diag / radius
+        for (int a = 0; a < 6; a++) M[a * (a + 1) / 2 + a] += dg[a] * inv_radius;   // D^2 = diag / radius
         double y[6];
         bool ok;
         chol_solve6_packed(M, gs, y, &ok);
         reuse = 1;
         if (!ok) {                         // invalid step: StepIsInvalid() == StepRejected(0)
-            radius = radius / decrease;
+            inv_radius *= decrease;        // radius / decrease_factor
             decrease *= 2.0;
             continue;
         }
@@ -486,15 +488,15 @@ __device__ __forceinline__ void lm_next_step_fast(LMState* st, aloam_lm_summary*
 #pragma unroll
         for (int i = 0; i < 7; i++) st->cand[i] = cand[i];
 #pragma unroll
-        for (int a = 0; a < 6; a++) st->delta[a] = delta[a];
-        st->radius = radius; st->decrease_factor = decrease; st->reuse_diag = reuse; st->iteration = iteration;
+        for (int a = 0; a < 6; a++) { st->delta[a] = delta[a]; st->diag[a] = dg[a]; }
+        st->inv_radius = inv_radius; st->decrease_factor = decrease; st->reuse_diag = reuse; st->iteration = iteration;
         st->pending = 1;
         return;
     }
 }
 // off the critical path (another wave, during the next pass's exchange): model cost change of the last
-// step from the unscaled normal equations (mcc = -(g.d + d'Ad/2), d = the tangent step), its norm in the
-// ambient space, and the norm of x
+// step from the unscaled normal equations (mcc = -(g.d + d'Ad/2), d = the tangent step), its reciprocal
+// (the gain ratio is then a product), its norm in the ambient space, and the norm of x
 __device__ __forceinline__ void lm_post(LMState* st) {
     if (!st->pending || st->done) return;
     double d[6], x[7], c[7];
@@ -516,63 +518,68 @@ __device__ __forceinline__ void lm_post(LMState* st) {
 #pragma unroll
     for (int i = 0; i < 7; i++) dx[i] = x[i] - c[i];
     st->mcc = mcc;
+    st->inv_mcc = 1.0 / mcc;
     st->invalid = mcc < 0.0;
     st->step_norm = norm7(dx);
     st->x_norm = norm7(x);
     st->pending = 0;
 }
 __device__ __forceinline__ void lm_tail_fast(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+    double A[21], g[6];
+#pragma unroll
+    for (int i = 0; i < 21; i++) A[i] = tot[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) g[i] = tot[21 + i];
+    const double new_cost = tot[27];
     if (pass == 0) {
         #pragma unroll
         for (int i = 0; i < 7; i++) st->x[i] = xp[i];
         st->nres = (int)tot[28];
         st->iteration = 0; st->successful = 0; st->done = 0; st->pending = 0; st->invalid = 0;
-        st->cost = tot[27]; st->initial_cost = tot[27];
+        st->cost = new_cost; st->initial_cost = new_cost;
         if (st->nres == 0) { st->cost = 0; lm_finish(st, out, 4); return; }
         #pragma unroll
-        for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        for (int i = 0; i < 21; i++) st->A[i] = A[i];
         #pragma unroll
-        for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        for (int i = 0; i < 6; i++) st->g[i] = g[i];
         #pragma unroll
-        for (int a = 0; a < 6; a++) st->scale[a] = 1.0 / (1.0 + sqrt(Aget(tot, a, a)));
-        st->radius = 1e4; st->decrease_factor = 2.0; st->reuse_diag = 0;
-        if (grad_max_norm(st->x, st->g) <= 1e-10) { lm_finish(st, out, 3); return; }
-        lm_next_step_fast(st, out, max_iter);
+        for (int a = 0; a < 6; a++) st->scale[a] = 1.0 / (1.0 + sqrt(Aget(A, a, a)));
+        st->decrease_factor = 2.0; st->reuse_diag = 0;
+        if (grad_max_norm(st->x, g) <= 1e-10) { st->inv_radius = 1e-4; lm_finish(st, out, 3); return; }
+        lm_next_step_fast(st, out, max_iter, A, g, 1e-4, 2.0, 0, 0);   // initial radius 1e4
         return;
     }
-    if (st->invalid) {                     // the step evaluated in this pass was invalid: not a candidate
+    // the state this pass needs, loaded together (independent LDS reads)
+    const int invalid = st->invalid, iteration = st->iteration;
+    const double inv_radius = st->inv_radius, decrease = st->decrease_factor, cost = st->cost;
+    const double step_norm = st->step_norm, x_norm = st->x_norm, inv_mcc = st->inv_mcc;
+    if (invalid) {                         // the step evaluated in this pass was invalid: not a candidate
         st->invalid = 0;
-        st->radius = st->radius / st->decrease_factor;
-        st->decrease_factor *= 2.0;
-        st->reuse_diag = 1;
-        lm_next_step_fast(st, out, max_iter);
+        lm_next_step_fast(st, out, max_iter, st->A, st->g, inv_radius * decrease, 2.0 * decrease, 1, iteration);
         return;
     }
-    const double new_cost = tot[27];
-    if (st->step_norm <= 1e-8 * (st->x_norm + 1e-8)) { lm_finish(st, out, 2); return; }
-    const double cost_change = st->cost - new_cost;
-    if (fabs(cost_change) <= 1e-6 * st->cost) { lm_finish(st, out, 1); return; }
-    const double rel = cost_change / st->mcc;
+    if (step_norm <= 1e-8 * (x_norm + 1e-8)) { lm_finish(st, out, 2); return; }
+    const double cost_change = cost - new_cost;
+    if (fabs(cost_change) <= 1e-6 * cost) { lm_finish(st, out, 1); return; }
+    const double rel = cost_change * inv_mcc;
     if (rel > 1e-3) {
+        double x[7];
         #pragma unroll
-        for (int i = 0; i < 7; i++) { st->x[i] = st->cand[i]; xp[i] = st->cand[i]; }
+        for (int i = 0; i < 7; i++) { x[i] = st->cand[i]; st->x[i] = x[i]; xp[i] = x[i]; }
         #pragma unroll
-        for (int i = 0; i < 21; i++) st->A[i] = tot[i];
+        for (int i = 0; i < 21; i++) st->A[i] = A[i];
         #pragma unroll
-        for (int i = 0; i < 6; i++) st->g[i] = tot[21 + i];
+        for (int i = 0; i < 6; i++) st->g[i] = g[i];
         st->cost = new_cost;
         st->successful++;
         const double t = 2.0 * rel - 1.0;
-        st->radius = fmin(1e16, st->radius / fmax(1.0 / 3.0, 1.0 - t * t * t));
-        st->decrease_factor = 2.0;
-        st->reuse_diag = 0;
-        if (grad_max_norm(st->x, st->g) <= 1e-10) { lm_finish(st, out, 3); return; }
+        // radius = min(1e16, radius / max(1/3, 1 - t^3)) in reciprocal form
+        const double ir = fmax(1e-16, inv_radius * fmax(1.0 / 3.0, 1.0 - t * t * t));
+        if (grad_max_norm(x, g) <= 1e-10) { st->inv_radius = ir; st->decrease_factor = 2.0; st->reuse_diag = 0; lm_finish(st, out, 3); return; }
+        lm_next_step_fast(st, out, max_iter, A, g, ir, 2.0, 0, iteration);
     } else {
-        st->radius = st->radius / st->decrease_factor;
-        st->decrease_factor *= 2.0;
-        st->reuse_diag = 1;
+        lm_next_step_fast(st, out, max_iter, st->A, st->g, inv_radius * decrease, 2.0 * decrease, 1, iteration);
     }
-    lm_next_step_fast(st, out, max_iter);
 }
 
 // The same tail on a register copy of the state (one LDS read/write burst instead of dependent LDS

@@ -723,6 +723,25 @@ static_assert(4 * (size_t)RVG_OLD + 16 * (size_t)RVG_NEW <= RBV_LDS - RBV_HDR, "
 static_assert(8 * (size_t)RVG_FIT <= ls_global_scratch_bytes(RBV_T, RBV_CAP), "merge-sort buffer in the scratch");
 struct RbvShared { unsigned bb[6]; int bad; int nrel; };
 
+// whether this thread's pairs (E[t], E[t + 1]), t = tid, tid + NT, ..., have strictly increasing keys: loads 8
+// pairs at a time and no short-circuit (a `up && load` loop waits for every load in turn: ~1 us each on global memory)
+template <int NT>
+__device__ __forceinline__ bool keys_increasing(const unsigned long long* E, int n) {
+    bool up = true;
+    for (int t0 = threadIdx.x; t0 + 1 < n; t0 += 8 * NT) {
+        unsigned a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int t = t0 + u * NT;
+            a[u] = t + 1 < n ? ps_keyat(E, t) : 0u;
+            b[u] = t + 1 < n ? ps_keyat(E, t + 1) : 1u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) up &= a[u] < b[u];
+    }
+    return up;
+}
+
 // global layout of a split cube's scratch region G = gscr + 4 p0 (4 n u64, n > RVG_FIT >= 512)
 __device__ __forceinline__ unsigned long long* rvg_S(unsigned long long* G, int n) { return G + n; }
 __device__ __forceinline__ unsigned long long* rvg_T(unsigned long long* G, int n) { return G + 2 * (size_t)n + 64; }
@@ -742,8 +761,7 @@ __device__ __forceinline__ void rvg_sort_big(unsigned char* smem, unsigned long 
     if (tid == 0) SH.bad = !(n_old <= RVG_OLD && n_new <= RVG_NEW);
     __syncthreads();
     if (!SH.bad) {
-        bool up = true;
-        for (int i = tid; i + 1 < n_old; i += RBV_T) up = up && ps_key(E[i]) < ps_key(E[i + 1]);
+        const bool up = keys_increasing<RBV_T>(E, n_old);
         if (__ballot(!up) && lane_id() == 0) SH.bad = 1;
     }
     __syncthreads();
@@ -762,7 +780,9 @@ __device__ __forceinline__ void rvg_sort_big(unsigned char* smem, unsigned long 
     unsigned long long* X = (unsigned long long*)(smem + RBV_HDR + 4 * (size_t)RVG_OLD);
     unsigned long long* Y = X + RVG_NEW;
     const int m64 = (n_new + WAVE - 1) / WAVE * WAVE;
-    for (int i = tid; i < n_old; i += RBV_T) OK[i] = ps_key(E[i]);
+#pragma unroll 8
+    for (int i = tid; i < n_old; i += RBV_T) OK[i] = ps_keyat(E, i);
+#pragma unroll 4
     for (int j = tid; j < m64; j += RBV_T) X[j] = j < n_new ? E[n_old + j] : ~0ull;
     lds_barrier();
     const unsigned long long* Xs = m64 ? block_merge_sort<unsigned long long, 16>(X, Y, m64) : X;
@@ -888,8 +908,7 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     if (new_count(a, c) == 0) {
         if (tid == 0) SH.bad = 0;
         if (FITS) lds_barrier(); else __syncthreads();
-        bool up = true;
-        for (int t = tid; t + 1 < n; t += RBV_T) up = up && ps_key(E[t]) < ps_key(E[t + 1]);
+        const bool up = keys_increasing<RBV_T>(E, n);
         if (__ballot(!up) && lane_id() == 0) SH.bad = 1;
         __syncthreads();
         if (SH.bad == 0) {
@@ -944,10 +963,13 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
     }
     unsigned long long* S = rvg_S(G, n);
     unsigned* rel = rvg_rel(G, n);
-    for (int i = tid; i < (n + 31) / 32; i += RBV_T) rel[i] = 0u;
     rvg_sort_big(smem, E, n, old_count(a, c), S, rvg_T(G, n));
     RBSTAMP(3);
-    rvg_mark<RBV_T>(S, n, rel, &SH.nrel);
+    // relevance as one byte per point in the (now free) merge buffer, then packed to bits: no global atomics
+    unsigned char* relB = (unsigned char*)rvg_T(G, n);
+    rvg_mark_bytes<RBV_T>(S, n, relB, &SH.nrel);
+    __syncthreads();
+    rvg_pack_bits<RBV_T>(relB, n, rel);
     __syncthreads();
 #ifdef RVG_EXP_NOREPLAY
     if (tid == 0) SH.nrel = 0;
@@ -955,7 +977,7 @@ __device__ __forceinline__ void rbv_cube(unsigned char* smem, const float4* __re
 #endif
     RBSTAMP(2);
     if (SH.nrel == 0) {                       // no leaf of >= 3 points: no replay
-        const int tot = rvg_reduce<RBV_T>(S, n, rel, rvg_fpos(G, n), ptf, outf, rsc);
+        const int tot = rvg_reduce<RBV_T, true>(S, n, rel, rvg_fpos(G, n), ptf, outf, rsc);   // S in global memory: batched
         if (tid == 0) a.seg_nout[c] = tot;
         RBSTAMP(5);
         return;
@@ -1119,7 +1141,9 @@ __global__ void k_rb_scatter(RbKinds P) {
     }
 }
 
-__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState* __restrict__ m, int seg_limit, int fit) {
+// part: 0 every cube; 1 the cubes above `fit` (and the empty ones), 2 the others (run concurrently on a second
+// stream, so the split cubes' segment sorts need not wait for the longest in-LDS cube)
+__global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState* __restrict__ m, int seg_limit, int fit, int part) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RbKind& K = P.k[blockIdx.y];
     const int r = blockIdx.x;
@@ -1128,10 +1152,13 @@ __global__ void __launch_bounds__(RBV_T) k_rb_cubevox(RbKinds P, const MapState*
     const CubeArrays& a = K.a;
     const int p0 = a.off[c], n = a.off[c + 1] - p0;
     int* segl = K.segl + (size_t)r * LS_SEGL;
+    if (part == 2 && (n == 0 || n > fit)) return;
     // finished here unless split below; reset before any early return, or k_rb_cubeseg / k_rb_cubered would
-    // read the list a split cube left in this slot in an earlier frame
-    if (threadIdx.x == 0) segl[0] = 0;
+    // read the list a split cube left in this slot in an earlier frame (part 1 resets every slot: k_rb_cubeseg
+    // follows it on its stream)
+    if (threadIdx.x == 0 && part != 2) segl[0] = 0;
     if (n == 0) { if (threadIdx.x == 0) a.seg_nout[c] = 0; return; }
+    if (part == 1 && n <= fit) return;
     int fbv[3];
     const int* fb = nullptr;
     if (K.fast_keys) {                    // leaf base below the cube's box (cube_coord: x in [50 (ci - cen) - 25, +50])
@@ -1268,10 +1295,18 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     // whole by their own workgroup, larger ones split
     static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(2048, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
     static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(512, std::min(RVG_FIT, atoi(getenv("ALOAM_CUBE_FIT")))) : RVG_FIT;
-    k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit);
+    // the cubes sorted in LDS on stream2 beside the split cubes' chain (split, segment sorts, sums) on the frame's
+    // stream (ALOAM_RB_FORK=0: one launch for both, the segment sorts after the slowest cube)
+    static const bool fork = !(getenv("ALOAM_RB_FORK") && atoi(getenv("ALOAM_RB_FORK")) == 0);
+    if (fork) {
+        fork_lane1(C);
+        k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, C.stream2>>>(P, C.d_map, seg_limit, fit, 2);
+    }
+    k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map, seg_limit, fit, fork ? 1 : 0);
     if (seg_limit <= RBQ_CAP) k_rb_cubeseg_s<<<dim3(125 * RBQ_SEGW, 2), RBQ_T, RBQ_LDS, st>>>(P, C.d_map);
     else k_rb_cubeseg<<<dim3(125 * RBV_SEGW, 2), RBV_T, RBV_LDS, st>>>(P, C.d_map);
     k_rb_cubered<<<dim3(125, 2), RBV_T, 0, st>>>(P, C.d_map);
+    if (fork) join_lane1(C);
     k_rb_final_scan<<<2, 1024, 0, st>>>(P, C.d_cube_valid);
     k_rb_final<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P, C.d_cube_valid);
     prof_phase(C, Ctx::PM_MAP_FILTER);

@@ -108,14 +108,24 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int 
     if (n <= 0) { if (tid == 0) *J.d_nout = 0; return; }
     if (tid < 6) bb[tid] = tid < 3 ? 0xffffffffu : 0u;
     __syncthreads();
+    // the cloud's points, 8 per thread and pass with their loads in flight together
+    auto pass = [&](auto f) {
+        for (int t0 = tid; t0 < n; t0 += 8 * VX_T) {
+            float4 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) q[u] = t0 + u * VX_T < n ? J.pts[t0 + u * VX_T] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (t0 + u * VX_T < n) f(t0 + u * VX_T, q[u]);
+        }
+    };
     {
         unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-        for (int t = tid; t < n; t += VX_T) {
-            const float4 p = J.pts[t];
+        pass([&](int, float4 p) {
             const unsigned v[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
 #pragma unroll
             for (int d = 0; d < 3; d++) { mn[d] = min(mn[d], v[d]); mx[d] = max(mx[d], v[d]); }
-        }
+        });
 #pragma unroll
         for (int d = 0; d < 3; d++) {
             const unsigned long long lo = wave_min_u64(mn[d]), hi = wave_max_u64(mx[d]);
@@ -134,7 +144,7 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int 
     }
     const float inv = 1.0f / J.leaf;
     if (n <= fit) {
-        for (int t = tid; t < n; t += VX_T) EL[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
+        pass([&](int t, float4 p) { EL[t] = ((unsigned long long)voxel_index(p, inv, minb, mul1, mul2) << 32) | (unsigned)t; });
         lds_barrier();
         VX_TS(2);
         ls_sort<VX_T, VX_CPW>(EL, n, 2 * (31 - __builtin_clz((unsigned)n)), (unsigned char*)sc, VX_LDS_N);
@@ -144,7 +154,7 @@ __global__ void __launch_bounds__(VX_T) k_vox_pcl(VoxJobs P, int seg_limit, int 
         return;
     }
     unsigned long long* E = J.gE;
-    for (int t = tid; t < n; t += VX_T) E[t] = ((unsigned long long)voxel_index(J.pts[t], inv, minb, mul1, mul2) << 32) | (unsigned)t;
+    pass([&](int t, float4 p) { E[t] = ((unsigned long long)voxel_index(p, inv, minb, mul1, mul2) << 32) | (unsigned)t; });
     __syncthreads();
     VX_TS(2);
     if (n <= VX_NMAX) {
@@ -191,8 +201,18 @@ __global__ void __launch_bounds__(VX_T) k_vox_reduce(VoxJobs P) {
     const int R = (n + gridDim.x - 1) / gridDim.x;
     const int q0 = min(n, (int)blockIdx.x * R), q1 = min(n, q0 + R);
     const unsigned long long* E = J.gE;
-    int before = 0;
-    for (int p = tid; p < q0; p += VX_T) before += (p == 0 || ps_key(E[p]) != ps_key(E[p - 1]));
+    int before = 0;                              // (8 positions per thread in flight)
+    for (int p0 = tid; p0 < q0; p0 += 8 * VX_T) {
+        unsigned k[8], kp[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + u * VX_T;
+            k[u] = p < q0 ? ps_keyat(E, p) : 0u;
+            kp[u] = p < q0 && p > 0 ? ps_keyat(E, p - 1) : ~k[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) before += p0 + u * VX_T < q0 && k[u] != kp[u];
+    }
     const int C = (q1 - q0 + VX_T - 1) / VX_T;
     const int p0 = min(q1, q0 + tid * C), p1 = min(q1, p0 + C);
     int nh = 0;

@@ -351,9 +351,12 @@ __device__ __forceinline__ unsigned fh_v(unsigned x) { return x; }
 // the value in a vector register (the compiler then keeps what is computed from it on the vector unit)
 __device__ __forceinline__ unsigned fh_v(unsigned x) { unsigned r; asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(x)); return r; }
 #endif
-__device__ __forceinline__ unsigned long long fh_v64(unsigned long long x) {
-    return ((unsigned long long)fh_v((unsigned)(x >> 32)) << 32) | fh_v((unsigned)x);
-}
+// bit (k & 31) of x (v_bfe_u32: one instruction, the offset taken mod 32 like the hardware's)
+#if defined(PS_HOST_EMU)
+__device__ __forceinline__ unsigned fh_bit(unsigned x, unsigned k) { return (x >> (k & 31u)) & 1u; }
+#else
+__device__ __forceinline__ unsigned fh_bit(unsigned x, unsigned k) { return __builtin_amdgcn_ubfe(x, k, 1u); }
+#endif
 __device__ __forceinline__ unsigned long long fh_shl1(unsigned long long x) {   // lane l <- lane l + 1 (row of 16)
     const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)x, 0x101, 0xF, 0xF, false);
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(x >> 32), 0x101, 0xF, 0xF, false);
@@ -374,19 +377,21 @@ __device__ __forceinline__ void fh_pops(PS_LDSP(unsigned long long) H, PS_LDSP(u
         // 1. top six levels
         const int jt = lane ? lane : 1;
         const unsigned char ft = F[min(jt, len) - 1];
-        const unsigned long long Ct = fh_v64(__ballot(lane >= 1 && 2 * lane + 1 <= hl && ft));
+        const unsigned long long Cb = __ballot(lane >= 1 && 2 * lane + 1 <= hl && ft);
+        const unsigned Ctl = fh_v((unsigned)Cb), Cth = fh_v((unsigned)(Cb >> 32));
         unsigned m = fh_v(1u);
 #pragma unroll
-        for (int k = 0; k < 6; k++) m = (m << 1) | (unsigned)((Ct >> m) & 1ull);   // m in [64, 127]
+        for (int k = 0; k < 5; k++) m = (m << 1) | fh_bit(Ctl, m);   // nodes < 32: the low word (one bfe per step)
+        m = (m << 1) | fh_bit(Cth, m);                                   // m in [32, 63]: bit m - 32 = m & 31 -> [64, 127]
         // 2. five more levels below the level-6 node m
         unsigned md = 32u;
         if (DEEP) {
             const unsigned nd = (m << dj) | oj;         // lane j: node j of m's subtree
             const unsigned char fd = F[min((int)nd, len) - 1];
-            const unsigned long long Cd = fh_v64(__ballot(lane >= 1 && lane < 32 && (int)(2 * nd + 1) <= hl && fd));
+            const unsigned Cd = fh_v((unsigned)__ballot(lane >= 1 && lane < 32 && (int)(2 * nd + 1) <= hl && fd));
             md = fh_v(1u);
 #pragma unroll
-            for (int k = 0; k < 5; k++) md = (md << 1) | (unsigned)((Cd >> md) & 1ull);   // md in [32, 63]
+            for (int k = 0; k < 5; k++) md = (md << 1) | fh_bit(Cd, md);   // md in [32, 63]
         }
         const unsigned me = (m << 5) | (md & 31u);    // the walk's node at depth 11
         // 3. path length and path nodes
@@ -679,10 +684,28 @@ __device__ __forceinline__ int ps_prev_stop(const unsigned long long* mask, int 
     return t * C + ps_msb(rest);
 }
 
+// A[s] += c summed over the wave's lanes with the same s (s < 0 or c == 0: nothing); every lane calls it
+__device__ __forceinline__ void ps_wave_add(int* A, int s, int c) {
+    bool pend = s >= 0 && c != 0;
+    for (;;) {
+        const unsigned long long m = __ballot(pend);
+        if (!m) break;
+        const int lead = __builtin_ctzll(m);
+        const int sl = readlane_i(s, lead);
+        const bool mine = pend && s == sl;
+        const int sum = wave_sum_i(mine ? c : 0);
+        if (lane_id() == lead) atomicAdd(&A[sl], sum);
+        pend = pend && !mine;
+    }
+}
+
 // Split every segment listed in U's big list (Bf/Bl/Bd, sorted by f, hdr[0] entries) that is longer
 // than `limit`, level by level, over positions [0, n): children > limit stay listed, the others are
 // pushed to the sink queue (tail/pend/Qs/qcap; segments of <= 16 too: the wave phase sorts leaves).
-// Elements stay in E (LDS, or global with G: loads are batched 8 at a time).
+// Elements stay in E (LDS, or global with G). limit >= 64: a 64-position word of the stop flags meets at most
+// two listed segments. Per level (round 5, micro/split_bench.py): the flags by coalesced wave passes, the
+// swaps by groups of 64 consecutive pairs per wave (both were per-thread chunks: one cache line per lane and
+// load, bound by the CU's line rate on global memory), k summed per wave.
 template <int NT, bool G>
 __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const int limit, int* tail, int* pend, int* Qs,
                             const int qcap, const unsigned* rel = nullptr) {
@@ -703,6 +726,8 @@ __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const i
     int* Bcut = Bd + 3 * PS_WGSEG;
     const int C = (n + NT - 1) / NT;
     const int nch = (n + C - 1) / C;
+    constexpr int NW = NT / WAVE;
+    const int lane = lane_id();
     for (int lvl = 0;; lvl++) {
         (void)lvl;
         const int nbig = ps_u(hdr[0]);
@@ -713,6 +738,41 @@ __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const i
             if (Bd[s] == 0) ps_heap_sort_rel(E, Bf[s], Bl[s], rel);
         if (tid < nbig && Bd[tid] > 0) { Bk[tid] = ps_median_to_first(E, Bf[tid], Bl[tid]); Bkk[tid] = 0; }
         ps_bar<G>();
+        // A: the stop flags by ballot, 64 consecutive positions per wave pass (coalesced key loads, 4 passes in
+        // flight); the 64-position words go to maskL / maskR and are read back below into each thread's
+        // C-position masks (thread t: positions [t C, t C + C)) before those overwrite them
+        const int nch64 = (n + 63) >> 6;
+        for (int c0 = ps_u(tid / WAVE); c0 < nch64; c0 += 4 * NW) {
+            unsigned kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = (c0 + u * NW) * 64 + lane;
+                kk[u] = p < n ? ps_keyat(E, p) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int c = c0 + u * NW;
+                if (c >= nch64) break;
+                const int p = c * 64 + lane;
+                int lo = 0, hi = nbig;                   // the last segment with f <= 64 c, then this lane's
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (Bf[mid] <= c * 64) lo = mid + 1;
+                    else hi = mid;
+                }
+                int s = lo - 1;
+                if (s + 1 < nbig && Bf[s + 1] <= p) s++;
+                bool isL = false, isR = false;
+                if (s >= 0 && p < n) {
+                    const int cf = Bf[s], ce = Bd[s] > 0 ? Bl[s] : cf;
+                    const unsigned ck = Bk[s];
+                    if (p >= cf && p < ce) { isL = p > cf && kk[u] >= ck; isR = kk[u] <= ck; }
+                }
+                const unsigned long long bl = __ballot(isL), br = __ballot(isR);
+                if (lane == 0) { maskL[c] = bl; maskR[c] = br; }
+            }
+        }
+        lds_barrier();
         int cl = 0, cr = 0;
         unsigned long long mL = 0, mR = 0;
         const int p0 = tid * C;
@@ -725,97 +785,95 @@ __device__ void ps_wg_split(unsigned long long* E, const int n, int* sc, const i
                 if (Bf[mid] <= p0) lo = mid + 1;
                 else hi = mid;
             }
-            int s = lo - 1;
-            s0 = s;
-            // the current segment in registers: f, l (l = f: inactive), K, and the next segment's f
-            int cf = 0, ce = 0, nf = s + 1 < nbig ? Bf[s + 1] : 0x7fffffff;
-            unsigned ck = 0;
-            if (s >= 0) { cf = Bf[s]; ce = Bd[s] > 0 ? Bl[s] : cf; ck = Bk[s]; }
-            for (int pb = p0; pb < p1; pb += 8) {
-                unsigned kk[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) kk[i] = pb + i < p1 ? ps_keyat(E, pb + i) : 0u;
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int p = pb + i;
-                    if (p < p1) {
-                        while (p >= nf) {
-                            s++;
-                            cf = Bf[s]; ce = Bd[s] > 0 ? Bl[s] : cf; ck = Bk[s];
-                            nf = s + 1 < nbig ? Bf[s + 1] : 0x7fffffff;
-                        }
-                        if (p >= cf && p < ce) {
-                            if (p > cf && kk[i] >= ck) mL |= 1ull << (p - p0);
-                            if (kk[i] <= ck) mR |= 1ull << (p - p0);
-                        }
-                    }
-                }
-            }
+            s0 = lo - 1;
+            const int w0 = p0 >> 6, o = p0 & 63, len = p1 - p0;
+            unsigned long long wl = maskL[w0] >> o, wr = maskR[w0] >> o;
+            if (o && w0 + 1 < nch64) { wl |= maskL[w0 + 1] << (64 - o); wr |= maskR[w0 + 1] << (64 - o); }
+            const unsigned long long keep = len >= 64 ? ~0ull : (1ull << len) - 1ull;
+            mL = wl & keep;
+            mR = wr & keep;
             cl = __popcll(mL);
             cr = __popcll(mR);
         }
         int tl, tr;
-        ps_exscan2<NT>(cl, cr, ws, tl, tr);
+        ps_exscan2<NT>(cl, cr, ws, tl, tr);              // (its barrier orders the reads above before the writes)
         if (tid < nch) { prefL[tid] = cl; prefR[tid] = cr; maskL[tid] = mL; maskR[tid] = mR; sidx[tid] = s0; }
         if (tid == 0) { prefL[nch] = tl; prefR[nch] = tr; maskL[nch] = 0ull; maskR[nch] = 0ull; }
         lds_barrier();
         PS_TS(lvl, 1);
         // k per segment: left stops with more right stops after them than left stops before them (this
-        // thread's stops in registers; the segment's bounds once per segment)
-        if (tid < nch && mL) {
-            int s = s0, cur = -1, bL = 0, eR = 0, cnt = 0, j = 0;
-            for (unsigned long long m = mL; m; m &= m - 1ull) {
-                const int b = __builtin_ctzll(m), p = p0 + b;
-                while (s + 1 < nbig && Bf[s + 1] <= p) s++;
-                if (s != cur) {
-                    if (cur >= 0 && cnt) atomicAdd(&Bkk[cur], cnt);
-                    cur = s; cnt = 0;
-                    bL = ps_count_before(prefL, maskL, Bf[s], C);
-                    eR = ps_count_before(prefR, maskR, Bl[s], C);
+        // thread's stops in registers; the segment's bounds once per segment); a chunk meets at most two
+        // segments (listed segments are longer than `limit` >= 64), summed per wave before the LDS atomic
+        {
+            int sA = -1, cA = 0, sB = -1, cB = 0;
+            if (tid < nch && mL) {
+                int s = s0, cur = -1, bL = 0, eR = 0, cnt = 0, j = 0;
+                for (unsigned long long m = mL; m; m &= m - 1ull) {
+                    const int b = __builtin_ctzll(m), p = p0 + b;
+                    while (s + 1 < nbig && Bf[s + 1] <= p) s++;
+                    if (s != cur) {
+                        if (cur >= 0 && cnt) {
+                            if (sA < 0) { sA = cur; cA = cnt; }
+                            else if (sB < 0) { sB = cur; cB = cnt; }
+                            else atomicAdd(&Bkk[cur], cnt);
+                        }
+                        cur = s; cnt = 0;
+                        bL = ps_count_before(prefL, maskL, Bf[s], C);
+                        eR = ps_count_before(prefR, maskR, Bl[s], C);
+                    }
+                    j = cl + __popcll(mL & ((1ull << b) - 1ull)) - bL;
+                    const int after = eR - (cr + __popcll(mR & ((2ull << b) - 1ull)));
+                    cnt += j < after;
                 }
-                j = cl + __popcll(mL & ((1ull << b) - 1ull)) - bL;
-                const int after = eR - (cr + __popcll(mR & ((2ull << b) - 1ull)));
-                cnt += j < after;
+                if (cur >= 0 && cnt) {
+                    if (sA < 0) { sA = cur; cA = cnt; }
+                    else if (sB < 0) { sB = cur; cB = cnt; }
+                    else atomicAdd(&Bkk[cur], cnt);
+                }
             }
-            if (cur >= 0 && cnt) atomicAdd(&Bkk[cur], cnt);
+            ps_wave_add(Bkk, sA, cA);
+            ps_wave_add(Bkk, sB, cB);
         }
         lds_barrier();
         PS_TS(lvl, 2);
-        // the swaps, 8 pairs in flight: partners from one select, then walking down the right stops
-        if (tid < nch && mL) {
-            int s = s0, cur = -1, bL = 0, eR = 0, k = 0, q = 0;
-            unsigned long long m = mL;
-            while (m) {
-                int pp[8], qq[8];
-                bool v[8];
+        // the swaps: segment s's pairs (left stop j, right stop j from the right), j < k_s, in groups of 64
+        // consecutive j per wave pass (lane = j: neighbouring lanes touch neighbouring stops, so the loads
+        // and stores coalesce), 4 groups in flight; a lane finds its pair by two rank selects in the masks
+        {
+            const int ks = lane < nbig && Bd[lane] > 0 ? Bkk[lane] : 0;
+            const int gs = (ks + 63) >> 6;
+            const int gincl = wave_incl_scan(gs);
+            const int gtot = ps_u(readlane_i(gincl, WAVE - 1));
+            for (int g0 = ps_u(tid / WAVE); g0 < gtot; g0 += 4 * NW) {
+                int pp[4], qq[4];
+                bool v[4];
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    v[i] = false;
-                    while (m && !v[i]) {
-                        const int b = __builtin_ctzll(m), p = p0 + b;
-                        m &= m - 1ull;
-                        while (s + 1 < nbig && Bf[s + 1] <= p) s++;
-                        if (s != cur) {
-                            cur = s;
-                            bL = ps_count_before(prefL, maskL, Bf[s], C);
-                            eR = ps_count_before(prefR, maskR, Bl[s], C);
-                            k = Bkk[s];
-                            q = -1;
+                for (int u = 0; u < 4; u++) {
+                    const int g = g0 + u * NW;
+                    v[u] = false;
+                    pp[u] = qq[u] = 0;
+                    if (g < gtot) {
+                        const int sg = ps_u(__popcll(__ballot(lane < nbig && gincl <= g)));
+                        const int gb = ps_u(readlane_i(gincl - gs, sg)), kseg = ps_u(readlane_i(ks, sg));
+                        const int f = ps_u(Bf[sg]), l = ps_u(Bl[sg]);
+                        const int j = (g - gb) * 64 + lane;
+                        if (j < kseg) {
+                            const int bL = ps_count_before(prefL, maskL, f, C), eR = ps_count_before(prefR, maskR, l, C);
+                            pp[u] = ps_select(prefL, maskL, bL + j, f / C, (l - 1) / C, C);
+                            qq[u] = ps_select(prefR, maskR, eR - 1 - j, f / C, (l - 1) / C, C);
+                            v[u] = true;
+                            PS_CHECK(pp[u] > f && pp[u] < l && qq[u] > pp[u] && qq[u] < l, "ps wg swap: f %d l %d p %d q %d\n", f, l,
+                                     pp[u], qq[u]);
                         }
-                        const int j = cl + __popcll(mL & ((1ull << b) - 1ull)) - bL;
-                        if (j >= k) continue;
-                        q = q < 0 ? ps_select(prefR, maskR, eR - 1 - j, Bf[s] / C, (Bl[s] - 1) / C, C) : ps_prev_stop(maskR, q, C);
-                        PS_CHECK(p > Bf[s] && p < Bl[s] && q > p && q < Bl[s], "ps wg swap: f %d l %d p %d q %d\n", Bf[s], Bl[s], p, q);
-                        pp[i] = p; qq[i] = q; v[i] = true;
                     }
                 }
-                unsigned long long ep[8], eq[8];
+                unsigned long long ep[4], eq[4];
 #pragma unroll
-                for (int i = 0; i < 8; i++)
-                    if (v[i]) { ep[i] = E[pp[i]]; eq[i] = E[qq[i]]; }
+                for (int u = 0; u < 4; u++)
+                    if (v[u]) { ep[u] = E[pp[u]]; eq[u] = E[qq[u]]; }
 #pragma unroll
-                for (int i = 0; i < 8; i++)
-                    if (v[i]) { E[pp[i]] = eq[i]; E[qq[i]] = ep[i]; }
+                for (int u = 0; u < 4; u++)
+                    if (v[u]) { E[pp[u]] = eq[u]; E[qq[u]] = ep[u]; }
             }
         }
         if (tid < nbig && Bd[tid] > 0) {

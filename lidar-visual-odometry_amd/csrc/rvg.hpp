@@ -22,34 +22,86 @@ namespace aloam {
 __device__ __forceinline__ bool rvg_is_rel(const unsigned* rel, unsigned i) { return (rel[i >> 5] >> (i & 31u)) & 1u; }
 
 // S (n pairs sorted by key, any tie order) -> rel bits (zeroed by the caller) for the points of >= 3-point
-// leaves; *nrel (zeroed by the caller) += their count. Thread t walks the leaves that start in its chunk.
+// leaves; *nrel (zeroed by the caller) += their count. Position q lies in such a leaf exactly when one of the
+// three windows of 3 around it is constant; S is sorted, so a window is constant when its ends are equal:
+// key[q-2] == key[q], key[q-1] == key[q+1] or key[q] == key[q+2]. One position per lane, consecutive lanes
+// on consecutive positions (S in global memory: coalesced, no dependent loads; the leaf-walking form spent
+// ~45 us of dependent loads on a 16k-point cube).
 template <int NT>
 __device__ __forceinline__ void rvg_mark(const unsigned long long* S, const int n, unsigned* rel, int* nrel) {
-    const int C = (n + NT - 1) / NT;
-    const int q0 = min(n, (int)threadIdx.x * C), q1 = min(n, q0 + C);
     int mine = 0;
-    for (int q = q0; q < q1; q++) {
-        const unsigned k = ps_key(S[q]);
-        if (q > 0 && ps_key(S[q - 1]) == k) continue;
-        int e = q + 1;
-        while (e < n && ps_key(S[e]) == k) e++;
-        if (e - q >= 3) {
-            for (int t = q; t < e; t++) {
-                const unsigned i = (unsigned)S[t] & 0xffffu;
-                atomicOr(&rel[i >> 5], 1u << (i & 31u));
-            }
-            mine += e - q;
+    for (int q = threadIdx.x; q < n; q += NT) {
+        const unsigned k = ps_keyat(S, q);
+        const unsigned km2 = q >= 2 ? ps_keyat(S, q - 2) : ~k, km1 = q >= 1 ? ps_keyat(S, q - 1) : 0u;
+        const unsigned kp1 = q + 1 < n ? ps_keyat(S, q + 1) : 0u, kp2 = q + 2 < n ? ps_keyat(S, q + 2) : ~k;
+        const bool r = km2 == k || (q >= 1 && q + 1 < n && km1 == kp1) || kp2 == k;
+        if (r) {
+            const unsigned i = (unsigned)S[q] & 0xffffu;
+            atomicOr(&rel[i >> 5], 1u << (i & 31u));
+            mine++;
         }
     }
-    if (mine) atomicAdd(nrel, mine);
+    mine = wave_sum_i(mine);
+    if (lane_id() == 0 && mine) atomicAdd(nrel, mine);
+}
+
+// The same marks as bytes, relB[point] = 0 / 1 (every point's byte written, S holds each point once), for S and
+// relB in global memory: plain byte stores instead of contended atomics on the bit words; rvg_pack_bits then
+// builds the bit words (after a workgroup barrier). relB: 16-byte aligned, n + 31 bytes readable.
+template <int NT>
+__device__ __forceinline__ void rvg_mark_bytes(const unsigned long long* S, const int n, unsigned char* relB, int* nrel) {
+    int mine = 0;
+    for (int q0 = threadIdx.x; q0 < n; q0 += 4 * NT) {     // 4 positions per lane in flight
+        unsigned kk[4][5], pi[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u * NT;
+#pragma unroll
+            for (int d = 0; d < 5; d++) kk[u][d] = q + d - 2 >= 0 && q + d - 2 < n ? ps_keyat(S, q + d - 2) : 0xffffffffu - (unsigned)d;
+            pi[u] = q < n ? (unsigned)S[q] & 0xffffu : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u * NT;
+            if (q >= n) continue;
+            // (out-of-range neighbours hold distinct sentinels no key window can match with its ends)
+            const bool r = kk[u][0] == kk[u][2] || (q >= 1 && q + 1 < n && kk[u][1] == kk[u][3]) || kk[u][4] == kk[u][2];
+            relB[pi[u]] = r ? 1 : 0;
+            mine += r;
+        }
+    }
+    mine = wave_sum_i(mine);
+    if (lane_id() == 0 && mine) atomicAdd(nrel, mine);
+}
+template <int NT>
+__device__ __forceinline__ void rvg_pack_bits(const unsigned char* relB, const int n, unsigned* rel) {
+    const int nw = (n + 31) >> 5;
+    for (int w = threadIdx.x; w < nw; w += NT) {
+        const unsigned* src = (const unsigned*)__builtin_assume_aligned(relB + 32 * (size_t)w, 16);
+        unsigned x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) x[u] = src[u];
+        unsigned m = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) m |= ((x[u] | x[u] >> 7 | x[u] >> 14 | x[u] >> 21) & 0xfu) << (4 * u);   // bytes 0 / 1 -> 4 bits
+        const int valid = n - 32 * w;
+        rel[w] = valid >= 32 ? m : m & ((1u << valid) - 1u);
+    }
 }
 
 // the final array E of the exact replay -> fpos[point] = position, for the relevant points
+// (8 positions per thread in flight: E, then the relevance words, then the stores)
 template <int NT>
 __device__ __forceinline__ void rvg_positions(const unsigned long long* E, const int n, const unsigned* rel, int* fpos) {
-    for (int p = threadIdx.x; p < n; p += NT) {
-        const unsigned i = (unsigned)E[p] & 0xffffu;
-        if (rvg_is_rel(rel, i)) fpos[i] = p;
+    for (int p0 = threadIdx.x; p0 < n; p0 += 8 * NT) {
+        unsigned i[8], w[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) i[u] = p0 + u * NT < n ? (unsigned)E[p0 + u * NT] & 0xffffu : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; u++) w[u] = p0 + u * NT < n ? rel[i[u] >> 5] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if ((w[u] >> (i[u] & 31u)) & 1u) fpos[i[u]] = p0 + u * NT;
     }
 }
 
