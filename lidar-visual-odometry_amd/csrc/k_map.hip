@@ -1295,9 +1295,11 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     // whole by their own workgroup, larger ones split
     static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(2048, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
     static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(512, std::min(RVG_FIT, atoi(getenv("ALOAM_CUBE_FIT")))) : RVG_FIT;
-    // the cubes sorted in LDS on stream2 beside the split cubes' chain (split, segment sorts, sums) on the frame's
-    // stream (ALOAM_RB_FORK=0: one launch for both, the segment sorts after the slowest cube)
-    static const bool fork = !(getenv("ALOAM_RB_FORK") && atoi(getenv("ALOAM_RB_FORK")) == 0);
+    // ALOAM_RB_FORK=1: the cubes sorted in LDS on stream2 beside the split cubes' chain (split, segment sorts,
+    // sums) on the frame's stream. Off by default: measured slower (C3 20 steps 867-870 vs 881-882 scans/s,
+    // steady state 798-801 vs 819-821, profiles/r05_fork_ab.txt; the mapping rounds of the next frames ran
+    // ~25 us longer, and both launches hold one workgroup per CU for their LDS)
+    static const bool fork = getenv("ALOAM_RB_FORK") && atoi(getenv("ALOAM_RB_FORK")) == 1;
     if (fork) {
         fork_lane1(C);
         k_rb_cubevox<<<dim3(125, 2), RBV_T, RBV_LDS, C.stream2>>>(P, C.d_map, seg_limit, fit, 2);
