@@ -219,7 +219,7 @@ static void allocate(Ctx& C) {
         m.corner = (float4*)dalloc(C, sizeof(float4) * capLS);
         m.surf = (float4*)dalloc(C, sizeof(float4) * N);
         m.full = (float4*)dalloc(C, sizeof(float4) * N);
-        m.n = (int*)dalloc(C, sizeof(int) * 2);
+        m.n = (int*)dalloc(C, sizeof(int) * 4);
         m.pose = (double*)dalloc(C, sizeof(double) * 8);
         m.cstack = (float4*)dalloc(C, sizeof(float4) * capLS);
         m.sstack = (float4*)dalloc(C, sizeof(float4) * N);
@@ -268,6 +268,7 @@ static void allocate(Ctx& C) {
     }
     HIPCHK(hipEventCreateWithFlags(&C.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_join, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&C.ev_stkn, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_handoff, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_scan, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&C.ev_lf, hipEventDisableTiming));
@@ -416,6 +417,7 @@ static void do_scan_registration(Ctx& C, const float* xyzr, int n, int flags, bo
     const bool side = defer && !C.profiling;
     scan_registration_launch(C, in, n, side);
     if (side) C.lf_pending = true;
+    C.lf_side = side;
     if (g_front_phases) front_phase(C, 1);
     prof_mark(C, 1);
     if (side) {
@@ -461,6 +463,12 @@ static void build_last_grids(Ctx& C, bool flags_preset = false, int cap_c = -1, 
 // completion (the scan's one sync, then the host-side bookkeeping). aloam_odometry runs both; the
 // 2-stage pipeline returns between them (front_issue / front_complete), so the caller's round trip
 // to the next scan overlaps this scan's GPU work.
+// scanRegistration's less-sharp / less-flat counts (ScanMeta::counts[2], [4]) -> the early stacks' own copy
+__global__ void k_stack_counts(const int* __restrict__ counts, int* __restrict__ dst) {
+    dst[0] = counts[2];
+    dst[1] = counts[4];
+}
+
 static void do_odometry_issue(Ctx& C) {
     if (!C.have_features) throw ApiError{ALOAM_E_STATE, "odometry before any features"};
     if (C.fp_active) throw ApiError{ALOAM_E_STATE, "an issued odometry scan has not been completed"};
@@ -581,10 +589,26 @@ static void do_odometry_issue(Ctx& C) {
             // clouds, which takes them off the mapping stage's critical path
             hint_c = pend ? std::min(cap_c, C.stack_hint[0] > 0 ? C.stack_hint[0] : cap_c) : cap_c;   // (exact when known)
             hint_s = pend ? std::min(cap_s, C.stack_hint[1] > 0 ? C.stack_hint[1] : cap_s) : cap_s;
-            fork_lane1(C);
-            voxel_grid_pair_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, hint_c, C.P.mapping_line_resolution, m.cstack,
-                               C.d_out->stack_n + 2 * t + 0, m.surf, m.n + 1, hint_s, C.P.mapping_plane_resolution, m.sstack,
-                               C.d_out->stack_n + 2 * t + 1);
+            static const bool early = !(getenv("ALOAM_EARLY_STACKS") && atoi(getenv("ALOAM_EARLY_STACKS")) == 0);
+            if (pend && early && C.lf_side) {
+                // The stacks read the clouds where scanRegistration left them (the last clouds since the swap
+                // above) with its device counts, so stream2 needs nothing of this scan's odometry: it follows its
+                // own less-flat VoxelGrid (queued there) and the set's hand-off wait (pre_publish), and the stacks
+                // are ready ~one odometry earlier (ALOAM_EARLY_STACKS=0: after the publish copy, as before)
+                // (their counts copied first: the next registration rewrites the less-sharp count on the stream,
+                // which waits for that copy)
+                k_stack_counts<<<1, 1, 0, C.stream2>>>(C.d_meta->counts, m.n + 2);
+                HIPCHK(hipEventRecord(C.ev_stkn, C.stream2));
+                HIPCHK(hipStreamWaitEvent(st, C.ev_stkn, 0));
+                voxel_grid_pair_on(C, C.stream2, C.ks[1], C.d_corner_last, m.n + 2, hint_c, C.P.mapping_line_resolution, m.cstack,
+                                   C.d_out->stack_n + 2 * t + 0, C.d_surf_last, m.n + 3, hint_s, C.P.mapping_plane_resolution,
+                                   m.sstack, C.d_out->stack_n + 2 * t + 1);
+            } else {
+                fork_lane1(C);
+                voxel_grid_pair_on(C, C.stream2, C.ks[1], m.corner, m.n + 0, hint_c, C.P.mapping_line_resolution, m.cstack,
+                                   C.d_out->stack_n + 2 * t + 0, m.surf, m.n + 1, hint_s, C.P.mapping_plane_resolution, m.sstack,
+                                   C.d_out->stack_n + 2 * t + 1);
+            }
             HIPCHK(hipEventRecord(m.ready, C.stream2));
             m.stacks_pub = true;
         } else {
@@ -1048,6 +1072,7 @@ void aloam_destroy(aloam_ctx* ctx) {
     for (auto& g : C->graphs) if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (C->ev_fork) (void)hipEventDestroy(C->ev_fork);
     if (C->ev_join) (void)hipEventDestroy(C->ev_join);
+    if (C->ev_stkn) (void)hipEventDestroy(C->ev_stkn);
     if (C->ev_handoff) (void)hipEventDestroy(C->ev_handoff);
     if (C->ev_scan) (void)hipEventDestroy(C->ev_scan);
     if (C->ev_lf) (void)hipEventDestroy(C->ev_lf);

@@ -120,6 +120,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;   // mapping: the surf half of the per-kind work runs here (fork/join)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_stkn = nullptr;    // stream2: the early stacks took their input counts (aloam_api.hip publish)
     hipEvent_t ev_handoff = nullptr; // device-to-device hand-offs: the source stream waits on it
     hipEvent_t ev_scan = nullptr, ev_lf = nullptr;   // per-line VoxelGrid on stream2: after the line kernel / done
     bool profiling = false;
@@ -152,6 +153,7 @@ struct Ctx {
     ScanMeta* h_meta_pin = nullptr;  // pinned landing slot of the async meta copy
     bool meta_pending = false;       // scanRegistration's counts are in flight to h_meta_pin (no sync yet)
     bool lf_pending = false;         // the per-line VoxelGrid runs on stream2 (stream waits on ev_lf before its results)
+    bool lf_side = false;            // the last registration ran its per-line VoxelGrid on stream2
     bool meta_deferred = false;      // the counts copy is queued later (queue_meta, behind the ev_lf wait)
     int last_nslots = 0;             // the previous scan's odometry factor count (LM grid hint)
     int stack_hint[2] = {0, 0};      // launch / sort sizes of the next publish's stack VoxelGrids (0: caps)
@@ -212,7 +214,7 @@ struct Ctx {
     // frame k does not read; the current set is mset[in_cur], aliased by the d_map_*_in / n_map_*_in fields
     struct MapInSet {
         float4 *corner = nullptr, *surf = nullptr, *full = nullptr;
-        int* n = nullptr;                  // device [2]: corner / surf counts
+        int* n = nullptr;                  // device [4]: corner / surf counts; [2..3] the early stacks' input counts
         double* pose = nullptr;            // device [8]: q_wodom[4], t_wodom[3] (laser_odom_to_init)
         float4 *cstack = nullptr, *sstack = nullptr;   // the frame's VoxelGrid'ed stacks (:542-550)
         int nc = 0, ns = 0, nf = 0;        // host counts

@@ -438,7 +438,9 @@ int aloam_pipeline_push(aloam_pipeline* P, const float* xyzr, int n, int flags, 
                 while (S.issued.load(std::memory_order_acquire) < seq - 1) std::this_thread::yield();
                 if (g_pipe_timing) S.t_wiss += now_us() - tw0;
                 std::lock_guard<std::mutex> lk(((aloam::Ctx*)P->back)->capture_mu);   // not while mapping captures
-                const hipError_t e = hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0);
+                hipError_t e = hipStreamWaitEvent(F.stream, S.copied[seq & 1], 0);
+                // (the stacks of this publish may run on stream2 ahead of the publish copy: the same wait there)
+                if (e == hipSuccess && F.publish_stacks) e = hipStreamWaitEvent(F.stream2, S.copied[seq & 1], 0);
                 if (e != hipSuccess)
                     throw aloam::HipError(std::string("hipStreamWaitEvent failed: ") + hipGetErrorName(e) + " (hand-off " +
                                           std::to_string(seq - 2) + ", server rc " + std::to_string(S.rc[(seq - 2) % MapServer::NRES]) +

@@ -61,10 +61,10 @@ struct VoxJobs { VoxJob j[2]; };
 // g_vox_seg elements, k_vox_seg sorts the segments in parallel (VX_SEGW workgroups per cloud), k_vox_reduce
 // sums the leaves.
 constexpr int VX_SEGW = 16;
-// tuning knob: split segments of at most this many elements (round 5, C3 pipeline, 2 x 20 / 50 steps on one box:
-// 10240 -> 846-850 / 936-937 scans/s vs 4096 -> 835-837 / 932-935, map prepare 0.17 vs 0.21 ms: fewer split
-// levels on one workgroup (~55 us each, micro/vx_stamps.py) for larger LDS sorts of the segments)
-static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(2048, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : VX_LDS_N;
+// tuning knob: split segments of at most this many elements. Round 5, C3 pipeline, 20 steps on one box: with the
+// split's levels at ~55 us, 10240 won (846-850 vs 835-837 scans/s for 4096); with the coalesced split (~30 us a
+// level) 4096 wins (891-894 vs 880-885, profiles/r05_tune_ab.txt): more, shorter segment sorts in parallel
+static const int g_vox_seg = getenv("ALOAM_VOX_SEG") ? std::max(2048, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_SEG")))) : 4096;
 // tuning knob: clouds up to this size are sorted whole by their own workgroup, larger ones split
 static const int g_vox_fit = getenv("ALOAM_VOX_FIT") ? std::max(256, std::min(VX_LDS_N, atoi(getenv("ALOAM_VOX_FIT")))) : VX_LDS_N;
 static_assert(ls_split_scratch_bytes(VX_T, VX_LDS_N) <= ls_global_scratch_bytes(VX_T, VX_LDS_N), "split scratch");

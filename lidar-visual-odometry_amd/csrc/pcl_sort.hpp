@@ -615,13 +615,15 @@ __device__ __noinline__ void ps_serial_std_sort(unsigned long long* E, int n) {
 }
 
 // __move_median_to_first(first, first + 1, mid, last - 1): returns the pivot key
+// (the four elements loaded together: one round trip on global memory)
 __device__ __forceinline__ unsigned ps_median_to_first(unsigned long long* E, int f, int l) {
     const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
-    const unsigned ka = ps_key(E[a]), kb = ps_key(E[b]), kc = ps_key(E[c]);
+    const unsigned long long ef = E[f], ea = E[a], eb = E[b], ec = E[c];
+    const unsigned ka = ps_key(ea), kb = ps_key(eb), kc = ps_key(ec);
     int pick;
     if (ka < kb) pick = kb < kc ? b : (ka < kc ? c : a);
     else pick = ka < kc ? a : (kb < kc ? c : b);
-    const unsigned long long ef = E[f], ep = E[pick];
+    const unsigned long long ep = pick == a ? ea : (pick == b ? eb : ec);
     E[f] = ep;
     E[pick] = ef;
     return ps_key(ep);

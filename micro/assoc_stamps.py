@@ -30,17 +30,27 @@ for k in range(frames):
         continue
     live &= t[:, 0] > t[live, 0].max() - 100000
     w = t[live]
-    spans.append((w[:, 5].max() - w[:, 0].min()) / 100.0)
-    act = w[w[:, 4] > 0]
-    nw.append(len(act))
-    d = lambda a, b, x=act: (x[:, b] - x[:, a]) / 100.0
-    ph["pose"].append(d(0, 1).max() if len(act) else 0)
+    # a slot counts only if this launch wrote it: not before the wave's start stamp and within the launch's
+    # window (slots a wave skips keep an earlier frame's value, which the round-4 version mixed in)
+    t0 = w[:, 0:1]
+    cur = (w >= t0) & (w <= w[:, 0].max() + 100000)
+    spans.append((np.where(cur[:, 5], w[:, 5], 0).max() - w[:, 0].min()) / 100.0)
+    act = cur[:, 4]
+    nw.append(int(act.sum()))
+
+    def d(a, b):
+        ok = act & cur[:, a] & cur[:, b] & (w[:, b] >= w[:, a])
+        return (w[ok, b] - w[ok, a]) / 100.0
+
+    v = d(0, 1)
+    ph["pose"].append(v.max() if len(v) else 0)
     for name, a, b in (("query", 1, 2), ("search", 2, 6), ("list", 6, 3), ("post", 3, 4), ("end", 4, 5)):
         v = d(a, b)
         ph[name].append((v.mean(), v.max()) if len(v) else (0, 0))
-    fit = act[act[:, 7] > act[:, 3]]
-    nfit.append(len(fit))
-    ph["fit"].append(((fit[:, 7] - fit[:, 3]).mean() / 100.0, (fit[:, 7] - fit[:, 3]).max() / 100.0) if len(fit) else (0, 0))
+    v = d(3, 7)
+    v = v[v > 0]                                  # waves that fitted
+    nfit.append(len(v))
+    ph["fit"].append((v.mean(), v.max()) if len(v) else (0, 0))
     nsearch.append(int((d(2, 6) > 1.0).sum()))
 print(f"frames {frames // 2}..{frames - 1}: launch span mean {np.mean(spans):.1f} us max {np.max(spans):.1f}; active waves {np.mean(nw):.0f}, "
       f"waves with a grid search > 1 us {np.mean(nsearch):.1f}, waves fitting {np.mean(nfit):.0f}")

@@ -3,7 +3,7 @@ output, cycles per pop (s_memtime ticks) and kernel time per pop (HIP events). F
 dependent v_fma_f32 (about 4 cycles each for one wave alone, MI355X_MICROARCH.md) timed both ways."""
 import ctypes as C, os, sys
 import numpy as np
-L = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "heap_bench.so"))
+L = C.CDLL(os.environ.get("HEAP_SO") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "heap_bench.so"))
 L.heap_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_ulonglong), C.POINTER(C.c_float)]
 for n in (100000, 1000000):
     buf = np.zeros(64, np.uint64); c = C.c_ulonglong(0); ms = C.c_float(0)

@@ -1,0 +1,16 @@
+#!/bin/bash
+# heap pops (top bits in registers) vs HEAD's, split (one-trip median) vs HEAD's, full GPU suite, A/B bench vs the
+# listed library, early stacks on / off
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+HEAP_SO=micro/heap_bench_head.so timeout -k 10 120 python micro/heap_bench.py 300 1000 3000 > gpurun_out/r5_pops.txt 2>&1 || { cat gpurun_out/r5_pops.txt; exit 1; }
+timeout -k 10 120 python micro/heap_bench.py 300 1000 3000 >> gpurun_out/r5_pops.txt 2>&1 || { cat gpurun_out/r5_pops.txt; exit 1; }
+grep "^n " gpurun_out/r5_pops.txt
+timeout -k 10 60 python micro/split_bench.py micro/split_bench_base.so base > gpurun_out/r5_split3.txt 2>&1 || { cat gpurun_out/r5_split3.txt; exit 1; }
+timeout -k 10 60 python micro/split_bench.py micro/split_bench.so new base >> gpurun_out/r5_split3.txt 2>&1 || { cat gpurun_out/r5_split3.txt; exit 1; }
+grep -v "per level" gpurun_out/r5_split3.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_gpu_tests.txt 2>&1 || { tail -40 gpurun_out/r5_gpu_tests.txt; exit 1; }
+tail -2 gpurun_out/r5_gpu_tests.txt
+STEPS="20" bash micro/r5_var_ab.sh "$@" || exit 1
+STEPS="20" bash micro/r5_env_ab.sh "early:ALOAM_EARLY_STACKS=1" "late:ALOAM_EARLY_STACKS=0"
