@@ -183,7 +183,8 @@ def c4_registration(lvo, torch, dev, dist, rank, world, steps, cpu_rounds):
         "value": round(steps / elapsed, 3), "unit": "registrations/s", "n_gpus": world, "steps": steps,
         "ms_per_registration": round(elapsed / steps * 1e3, 4), "scaling": "strong",
         "parallelism": f"query slots sharded x{world} ({g['slot_end'] - g['slot_begin']} on rank {rank}), map replicated",
-        "exchange": "RCCL all-gather of 256 x 32 fp64 normal-equation records per LM pass" if world > 1 else "none (1 rank)",
+        "exchange": "RCCL all-gather of 256 x 32 fp64 normal-equation records per LM pass" if world > 1 else
+                    "none (1 rank)",
         "pose_err_m": float(np.linalg.norm(g["x"][4:] - x_true[4:])),
         "surf_correspondences_last_round": g["surf_num"][-1],
     }

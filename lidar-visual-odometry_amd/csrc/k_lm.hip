@@ -1034,6 +1034,119 @@ __global__ void __launch_bounds__(CB) k_s2m_final(const double* __restrict__ pre
     }
 }
 
+// One Solve of the sharded registration at world 1 as ONE launch: the same records, reductions and tails as
+// the max_iter + 1 pass launches and the final launch above, bit for bit (k_s2m_pass's block record code
+// and k_s2m_final's tail). G co-resident workgroups compute the nrec block records of a pass (workgroup w:
+// blocks w, w + G, ...) into a double-buffered record array, meet at a grid barrier (agent-scope counter
+// `bar`: S2M_BARS counters, zeroed before the launch), then every workgroup reduces the nrec records in block order and runs
+// the tail on its LDS copy of the state; a Solve that terminated stops in every workgroup at the same pass.
+constexpr int S2M_BARS = 16;                 // k_s2m_solve's barrier counters (32 unsigned apart)
+__global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict__ f, int nslots, int per, int nrec,
+                                                  double* __restrict__ recs, unsigned* bar, int* err, double* x, LMState* st_out,
+                                                  aloam_lm_summary* sum, int max_iter, int* round_cnt) {
+    __shared__ double rows[CB / 4 * NACC];
+    __shared__ double part8[8 * NACC];
+    __shared__ double tot[NACC];
+    __shared__ LMState ls;
+    __shared__ double xl[7], x0s[7];
+    __shared__ int cnt[2];
+    __shared__ int done, fail;
+    const unsigned G = gridDim.x;
+    if (threadIdx.x < 7) x0s[threadIdx.x] = x[threadIdx.x];
+    if (threadIdx.x == 0) { done = 0; fail = 0; }
+    __syncthreads();
+    for (int pass = 0; pass <= max_iter; pass++) {
+        const double* xs = pass == 0 ? x0s : ls.cand;
+        const dquat q{xs[0], xs[1], xs[2], xs[3]};
+        const double t[3] = {xs[4], xs[5], xs[6]};
+        double* rb = recs + (size_t)(pass & 1) * nrec * S2M_REC;
+        for (int g = blockIdx.x; g < nrec; g += G) {                   // this workgroup's blocks (k_s2m_pass)
+            if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+            __syncthreads();
+            double acc[NACC];
+#pragma unroll
+            for (int i = 0; i < NACC; i++) acc[i] = 0;
+            int ne = 0, np = 0;
+            const int f0 = g * per, f1 = min(nslots, f0 + per);
+            for (int i = f0 + threadIdx.x; i < f1; i += CB) {
+                const aloam_factor fi = f[i];
+                ne += fi.type == 0;
+                np += fi.type == 1 || fi.type == 2;
+                accumulate(fi, q, t, acc);
+            }
+            __syncthreads();
+            if (pass == 0) {
+                const int se = wave_sum_i(ne), sp = wave_sum_i(np);
+                if ((threadIdx.x & 63) == 0 && (se | sp)) { atomicAdd(&cnt[0], se); atomicAdd(&cnt[1], sp); }
+            }
+            block_reduce_acc<CB>(acc, rows, part8, tot);
+            double* rec = rb + (size_t)g * S2M_REC;
+            if (threadIdx.x < NACC) rec[threadIdx.x] = tot[threadIdx.x];
+            if (threadIdx.x == 0) { rec[NACC] = cnt[0]; rec[NACC + 1] = cnt[1]; rec[NACC + 2] = 0.0; }
+        }
+        // grid barrier: this pass's records of every workgroup stored. Arrivals spread over S2M_BARS counters
+        // (workgroup w on counter w % S2M_BARS, one cache line each), polled by as many lanes of wave 0: one
+        // counter for all 256 workgroups serialised their atomics (measured slower than the pass launches)
+        __syncthreads();
+        if (threadIdx.x < WAVE) {
+            if (threadIdx.x == 0) {
+                __threadfence();
+                atomicAdd(&bar[(blockIdx.x % S2M_BARS) * 32], 1u);
+            }
+            const int lane = threadIdx.x;
+            const unsigned mine = lane < S2M_BARS ? (G / S2M_BARS + ((unsigned)lane < G % S2M_BARS ? 1u : 0u)) * (unsigned)(pass + 1) : 0u;
+            int spins = 0;
+            while (true) {
+                const unsigned v = lane < S2M_BARS ? __hip_atomic_load(&bar[lane * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                if (!__ballot(v < mine)) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 22)) {
+                    if (lane == 0) { atomicExch(err, 1); fail = 1; }
+                    break;
+                }
+            }
+            __threadfence();
+        }
+        __syncthreads();
+        if (fail) return;
+        s2m_reduce_records(rb, nrec, rows, part8, tot);
+        if (pass == 0 && blockIdx.x == 0 && round_cnt) {              // this round's correspondences (pass-0 records)
+            int a = 0, b = 0;
+            for (int r = threadIdx.x; r < nrec; r += CB) { a += (int)rb[(size_t)r * S2M_REC + NACC]; b += (int)rb[(size_t)r * S2M_REC + NACC + 1]; }
+            a = wave_sum_i(a);
+            b = wave_sum_i(b);
+            if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+            __syncthreads();
+            if ((threadIdx.x & 63) == 0) { atomicAdd(&cnt[0], a); atomicAdd(&cnt[1], b); }
+            __syncthreads();
+            if (threadIdx.x < 2) round_cnt[threadIdx.x] = cnt[threadIdx.x];
+        }
+        if (threadIdx.x == 0) {
+            const double* xsrc = pass == 0 ? x0s : ls.x;
+            for (int i = 0; i < 7; i++) xl[i] = xsrc[i];
+            lm_tail_reg(&ls, tot, pass, xl, blockIdx.x == 0 ? sum : nullptr, max_iter);
+            done = ls.done;
+        }
+        __syncthreads();
+        if (done) break;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int i = 0; i < 7; i++) x[i] = ls.x[i];
+        *st_out = ls;
+    }
+}
+
+void s2m_solve_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int nrec, double* recs, unsigned* bar, double* x,
+                      LMState* st_out, aloam_lm_summary* sum, int* round_cnt) {
+    // every workgroup co-resident (<= 1 per CU, like k_lm_coop), each with nrec / G blocks (one block each on
+    // a full MI355X: the blocks' evaluations are the Solve's work, 64 workgroups x 4 blocks measured slower)
+    static const int gcap = getenv("ALOAM_S2M_SOLVE_G") ? std::max(1, atoi(getenv("ALOAM_S2M_SOLVE_G"))) : 256;
+    const int G = std::max(1, std::min(std::min(gcap, C.n_cus), nrec));
+    k_s2m_solve<<<G, CB, 0, C.stream>>>(f, nslots, per, nrec, recs, bar, C.d_bar_err, x, st_out, sum,
+                                        std::min(C.P.max_solver_iterations, 200), round_cnt);
+    HIPCHK(hipGetLastError());
+}
+
 void s2m_pass_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const double* prev,
                      const LMState* st_in, LMState* st_out, const double* x0, int pass, aloam_lm_summary* sum, int* round_cnt,
                      double* send) {

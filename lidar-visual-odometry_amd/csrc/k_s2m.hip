@@ -29,6 +29,8 @@ void s2m_pass_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec
                      const LMState* st_in, LMState* st_out, const double* x0, int pass, aloam_lm_summary* sum, int* round_cnt,
                      double* send);
 void s2m_final_launch(Ctx& C, const double* prev, int nrec, const LMState* st_in, double* x, int last_pass, aloam_lm_summary* sum);
+void s2m_solve_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int nrec, double* recs, unsigned* bar, double* x,
+                      LMState* st_out, aloam_lm_summary* sum, int* round_cnt);
 
 constexpr int S2M_REC = 32;                     // doubles per record (k_lm.hip)
 constexpr int NREC = ALOAM_S2M_RECORDS;
@@ -52,6 +54,7 @@ struct S2M {
     double* d_x = nullptr;                      // [8] parameters (laserMapping.cpp:129)
     double* d_send = nullptr;                   // 2 x NREC records (pass parity: group-mode reuse guard)
     double* d_recv = nullptr;                   // RECV_CAP records
+    unsigned* d_bar = nullptr;                  // [ALOAM_MAX_ROUNDS][16 x 32] grid-barrier counters of the one-launch Solves
     S2MOut* d_out = nullptr;
     S2MOut* h_out = nullptr;                    // pinned
     hipEvent_t ev[2] = {nullptr, nullptr};      // group mode: records of this rank ready (per parity)
@@ -114,6 +117,7 @@ static S2M& s2m_of(Ctx& C) {
         S->d_send = (double*)dalloc(C, sizeof(double) * 2 * NREC * S2M_REC);
         S->d_recv = (double*)dalloc(C, sizeof(double) * RECV_CAP * S2M_REC);
         S->d_out = (S2MOut*)dalloc(C, sizeof(S2MOut));
+        S->d_bar = (unsigned*)dalloc(C, sizeof(unsigned) * ALOAM_MAX_ROUNDS * 512);
         HIPCHK(hipHostMalloc((void**)&S->h_out, sizeof(S2MOut), hipHostMallocDefault));
         for (auto& e : S->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipMemsetAsync(S->d_recv, 0, sizeof(double) * RECV_CAP * S2M_REC, C.stream));
@@ -216,6 +220,10 @@ static void finish(Ctx& C, int rank, int world, double* x, aloam_s2m_result* out
     HIPCHK(hipMemcpyAsync(xo, S.d_x, sizeof(double) * 7, hipMemcpyDeviceToHost, C.stream));
     HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, sizeof(S2MOut), hipMemcpyDeviceToHost, C.stream));
     HIPCHK(hipStreamSynchronize(C.stream));
+    if (*(volatile int*)C.h_bar_err) {          // a one-launch Solve's grid barrier timed out (results void)
+        *(volatile int*)C.h_bar_err = 0;
+        throw ApiError{ALOAM_E_HIP, "s2m solve: grid barrier timed out"};
+    }
     if (copy_x) std::memcpy(x, xo, sizeof(xo));
     if (!out) return;
     aloam_s2m_result r{};
@@ -244,12 +252,23 @@ void s2m_register(Ctx& C, double* x, aloam_s2m_result* out) {
     const int Q = S.nqc + S.nqs;
     const Slice sl = slice_of(Q, rank, world);
     begin(C, x);
+    // ALOAM_S2M_PERSIST=1, world 1 without a communicator: each Solve is one launch with its exchange on the
+    // device (k_s2m_solve). Off by default: measured slower than the stream-ordered pass launches (C4, 2.18-2.21
+    // vs 2.04 ms per registration, profiles/r05_s2m_persist.txt): a grid barrier per pass costs ~3 us more
+    // than the boundary between two queued launches
+    static const bool persist = getenv("ALOAM_S2M_PERSIST") && atoi(getenv("ALOAM_S2M_PERSIST")) == 1;
+    const bool one_launch = persist && world == 1 && !rccl_exchange;
     if (s2m_gate(S)) {
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
         const int max_iter = std::min(C.P.max_solver_iterations, 200);
+        if (one_launch) HIPCHK(hipMemsetAsync(S.d_bar, 0, sizeof(unsigned) * ALOAM_MAX_ROUNDS * 512, C.stream));
         for (int it = 0; it < rounds; it++) {
             s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
                              S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
+            if (one_launch) {
+                s2m_solve_launch(C, S.d_f, Q, sl.per, NREC, S.d_send, S.d_bar + 512 * it, S.d_x, S.d_st, &S.d_out->lm[it], S.d_out->cnt[it]);
+                continue;
+            }
             const double* prev = nullptr;   // the exchanged records of the previous pass
             for (int pass = 0; pass <= max_iter; pass++) {
                 double* send = S.d_send + (size_t)(pass & 1) * NREC * S2M_REC;

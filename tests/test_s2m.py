@@ -179,3 +179,46 @@ def test_s2m_assoc_paths_bit_identical(gpu_ctx_factory, monkeypatch, batch_min, 
         o = ob.s2m_register(abi.default_params(128), cm, sm, cq, sq, x0)
         assert rel(g["x"], o["x"]) <= POSE_RTOL
         assert g["surf_num"] == o["surf_num"] and g["corner_num"] == o["corner_num"]
+
+
+_PERSIST_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from lvo_amd_loader import lvo
+import test_s2m as T
+wl = T.small_workload()
+x0 = wl[4]
+cm, sm, cq, sq, _, _ = wl
+p = lvo.abi.default_params(128)
+p.max_scan_points, p.max_map_points = max(len(cq) + len(sq), 1024), 1024
+ctx = lvo.Context(p)
+ctx.s2m_set_map(cm, sm)
+ctx.s2m_set_queries(cq, sq)
+g = ctx.s2m_register(x0)
+ctxs = []
+for _ in range(2):
+    c = lvo.Context(p)
+    c.s2m_set_map(cm, sm)
+    c.s2m_set_queries(cq, sq)
+    ctxs.append(c)
+res = lvo.s2m_register_group(ctxs, x0)
+assert np.array_equal(g["x"].view(np.uint64), res[0]["x"].view(np.uint64)), (g["x"], res[0]["x"])
+assert g["lm"] == res[0]["lm"] and g["surf_num"] == res[0]["surf_num"] and g["corner_num"] == res[0]["corner_num"]
+print("ok", list(g["x"]))
+"""
+
+
+def test_s2m_one_launch_solve_bit_identical():
+    """ALOAM_S2M_PERSIST=1 (read once per process, so in a child): at world 1 each Solve is one launch
+    (k_s2m_solve: grid barrier per pass, records on the device); the pose, summaries and correspondence
+    counts are bit-identical to the pass launches of a 2-rank group run."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ALOAM_S2M_PERSIST="1")
+    out = subprocess.run([sys.executable, "-c", _PERSIST_SCRIPT, here], env=env, capture_output=True, text=True,
+                         timeout=110, cwd=here)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert out.stdout.strip().splitlines()[-1].startswith("ok")
