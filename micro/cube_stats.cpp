@@ -24,6 +24,7 @@ struct Acc {
     long heap_steps_full = 0, heap_steps_pruned = 0, heap_steps_max_full = 0, heap_steps_max_pruned = 0;
     long sw_pops = 0, sw_max = 0, sw_segs = 0, sw_ok = 0, sw_bad = 0, es_pops = 0, es_max = 0;   // safe-switch analysis
     long po_segs = 0, po_grab = 0, po_ok = 0, po_bad = 0, po_grab_g = 0, po_safe = 0, po_safe_ok = 0, po_noown = 0, po_noown_ok = 0;   // post-order closed form checks
+    long seg_safe_small = 0, seg_safe_big = 0, seg_unsafe = 0, pops_safe_small = 0, pops_safe_big = 0, pops_unsafe = 0, pops_safe_big_max = 0, pops_unsafe_max = 0;
 };
 Acc acc[5], frame_acc[5];
 template <class V> void hook(const V& in, float leaf, int kind);
@@ -87,6 +88,14 @@ static void heap_sort_check(T* first, T* last, Less less, const std::map<unsigne
         orc::adjust_heap(first, 0L, l, v, less);
     }
     A.po_segs++;
+    {   // segment-level closed form (ws_heap_postorder: every relevant group safe) by length, with its early-stop pops
+        bool all = true;
+        for (auto& kv : rel) all = all && safe[kv.first];
+        const long pops = std::min(len - 1, cmin);
+        if (all && len <= 1024) { A.seg_safe_small++; A.pops_safe_small += pops; }
+        else if (all) { A.seg_safe_big++; A.pops_safe_big += pops; A.pops_safe_big_max = std::max(A.pops_safe_big_max, pops); }
+        else { A.seg_unsafe++; A.pops_unsafe += pops; A.pops_unsafe_max = std::max(A.pops_unsafe_max, pops); }
+    }
     // safe-switch analysis (a device design's prototype): pops until no relevant group has a member in its
     // danger window [len - c_G, h) (the window start stays fixed while G is popped: every pop takes an element
     // >= K_G and shrinks the heap by one), then the post-order closed form of the CURRENT heap for the rest.
@@ -389,6 +398,9 @@ int main(int argc, char** argv) {
             t.po_segs += a.po_segs; t.po_grab += a.po_grab; t.po_ok += a.po_ok; t.po_bad += a.po_bad; t.po_grab_g += a.po_grab_g;
             t.sw_pops += a.sw_pops; t.sw_max = std::max(t.sw_max, a.sw_max); t.sw_segs += a.sw_segs; t.sw_ok += a.sw_ok; t.sw_bad += a.sw_bad;
             t.es_pops += a.es_pops; t.es_max = std::max(t.es_max, a.es_max);
+            t.seg_safe_small += a.seg_safe_small; t.seg_safe_big += a.seg_safe_big; t.seg_unsafe += a.seg_unsafe;
+            t.pops_safe_small += a.pops_safe_small; t.pops_safe_big += a.pops_safe_big; t.pops_unsafe += a.pops_unsafe;
+            t.pops_safe_big_max = std::max(t.pops_safe_big_max, a.pops_safe_big_max); t.pops_unsafe_max = std::max(t.pops_unsafe_max, a.pops_unsafe_max);
             t.heap_matter_segs += a.heap_matter_segs; t.maxn = std::max(t.maxn, a.maxn); t.heap_max = std::max(t.heap_max, a.heap_max); t.matter_max = std::max(t.matter_max, a.matter_max);
             if ((k + 1) % every == 0)
                 printf("frame %3d %s: cubes %ld (unique-sorted %ld, with >=3 leaf %ld, heap %ld, heap-order-matters %ld) pts %ld max %ld | "
@@ -413,6 +425,9 @@ int main(int argc, char** argv) {
                NM[w], t.po_segs, t.po_grab, t.po_ok, t.po_bad, t.po_grab_g, t.po_safe, t.po_safe_ok, t.po_noown, t.po_noown_ok);
         printf("SWITCH %s: relevant heap segments %ld | pops: early stop %ld (max %ld), safe switch %ld (max %ld) | prediction right %ld wrong %ld\n",
                NM[w], t.sw_segs, t.es_pops, t.es_max, t.sw_pops, t.sw_max, t.sw_ok, t.sw_bad);
+        printf("SEGSAFE %s: all groups safe, <= 1024: %ld segs %ld pops | all safe, > 1024: %ld segs %ld pops (max %ld) | unsafe: %ld segs %ld pops (max %ld)\n",
+               NM[w], t.seg_safe_small, t.pops_safe_small, t.seg_safe_big, t.pops_safe_big, t.pops_safe_big_max, t.seg_unsafe, t.pops_unsafe,
+               t.pops_unsafe_max);
     }
     if (getenv("CS_RVG")) printf("RVG: %ld cube filters, %ld differ from PCL order\n", stats::g_rvg_calls, stats::g_rvg_bad);
     oracle_destroy(o);
