@@ -543,7 +543,9 @@ __device__ __noinline__ void ws_heap_sort(unsigned long long* E, const int f, co
         }
         if (lds) ps_wsync<false>(); else ps_wsync<true>();
     }
+#ifndef PS_NO_POSTORDER                      // A/B parity builds: the pops everywhere
     if (rel && len <= 16 * WAVE && ws_heap_postorder(H, len, npop, rel)) return;
+#endif
 #ifdef PS_NO_FH                              // A/B builds: the six-level pops everywhere
     fscr = nullptr;
 #endif

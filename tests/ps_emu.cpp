@@ -213,14 +213,43 @@ static void run_ls_global(std::vector<unsigned long long>& E, int cap) {
 // >= 3-point key's points in the same order. Mode 4.
 // Mode 6: the same with the child-flag pops (fh_sort_heap_lds, flag bytes passed as fscr) up to FH_MAX points;
 // every other trial without rel (all pops: the whole array must equal libstdc++'s).
-static int heap_trials(int trials, std::mt19937_64& rng, bool flags = false) {
+// Mode 7 (fuzz): inputs aimed at the post-order closed form's edges (ws_heap_postorder, len <= 1024): lengths
+// close to 1024, many duplicates, several relevant groups per segment, groups whose keys are the largest (popped
+// first), the smallest or in the middle, and group members placed at the input's end (after make_heap they tend
+// to sit in the last slots, the danger zone).
+static void fuzz_input(std::vector<unsigned long long>& E, std::mt19937_64& rng, int t) {
+    const int n = (int)E.size();
+    const int style = t % 5;
+    const unsigned kinds = style == 0 ? 2 + (unsigned)(n / 8) : 7u * (unsigned)n;
+    for (int i = 0; i < n; i++) E[i] = ((unsigned long long)(unsigned)(style == 0 ? rng() % kinds : 7u * (unsigned)i + 3u) << 32);
+    if (style != 0) std::shuffle(E.begin(), E.end(), rng);
+    const int groups = 1 + (int)(rng() % 5);
+    for (int g = 0; g < groups; g++) {
+        unsigned kg;
+        switch ((style + g) % 4) {
+            case 0: kg = 7u * (unsigned)n + 100u + (unsigned)g; break;          // larger than every other key
+            case 1: kg = 1u + (unsigned)g; break;                               // smaller than the others
+            default: kg = (unsigned)(E[rng() % (unsigned)n] >> 32); break;      // an existing key
+        }
+        const int sz = 3 + (int)(rng() % 4);
+        for (int j = 0; j < sz; j++) {
+            // members at the input's end (style 3, 4) or anywhere
+            const int p = style >= 3 && j % 2 == 0 ? n - 1 - (int)(rng() % (unsigned)std::max(1, n / 16)) : (int)(rng() % (unsigned)n);
+            E[p] = ((unsigned long long)kg << 32);
+        }
+    }
+    for (int i = 0; i < n; i++) E[i] = (E[i] & ~0xffffffffull) | (unsigned)i;
+}
+static int heap_trials(int trials, std::mt19937_64& rng, bool flags = false, bool fuzz = false) {
     int bad = 0;
     for (int t = 0; t < trials; t++) {
-        const int n = flags ? 2 + (int)(rng() % (t % 3 == 0 ? 200 : aloam::FH_MAX - 1)) : 17 + (int)(rng() % 1000);
+        const int n = fuzz ? 1024 - (int)(rng() % (t % 3 == 0 ? 1000 : 130))
+                           : flags ? 2 + (int)(rng() % (t % 3 == 0 ? 200 : aloam::FH_MAX - 1)) : 17 + (int)(rng() % 1000);
         const unsigned kinds = 2 + (unsigned)(rng() % (unsigned)(t % 2 ? n / 3 + 1 : 4 * n));
         std::vector<unsigned long long> E(n);
         for (int i = 0; i < n; i++) E[i] = ((unsigned long long)(unsigned)(rng() % kinds) << 32) | (unsigned)i;
-        if (t % 4 == 3) {                         // distinct keys but one group of 3-5 (few relevant points)
+        if (fuzz) fuzz_input(E, rng, t);
+        if (!fuzz && t % 4 == 3) {                // distinct keys but one group of 3-5 (few relevant points)
             for (int i = 0; i < n; i++) E[i] = ((unsigned long long)(unsigned)(7 * i + 3) << 32) | (unsigned)i;
             std::shuffle(E.begin(), E.end(), rng);
             const int g = 3 + (int)(rng() % 3);
@@ -228,7 +257,7 @@ static int heap_trials(int trials, std::mt19937_64& rng, bool flags = false) {
             for (int j = 0; j < g; j++) { const int p = (int)(rng() % n); E[p] = ((unsigned long long)kg << 32) | (E[p] & 0xffffffffull); }
             for (int i = 0; i < n; i++) E[i] = (E[i] & ~0xffffffffull) | (unsigned)i;
         }
-        if (t % 3 == 2) std::sort(E.begin(), E.begin() + n * 3 / 4);     // mostly ascending input
+        if (!fuzz && t % 3 == 2) std::sort(E.begin(), E.begin() + n * 3 / 4);     // mostly ascending input
         std::vector<unsigned long long> A = E;
         std::partial_sort(A.begin(), A.end(), A.end(), [](unsigned long long a, unsigned long long b) { return (a >> 32) < (b >> 32); });
         std::map<unsigned, int> cnt;
@@ -242,7 +271,7 @@ static int heap_trials(int trials, std::mt19937_64& rng, bool flags = false) {
         g_block = std::make_unique<std::barrier<>>(WAVE);
         std::vector<std::thread> th;
         std::vector<unsigned char> F(n, 0xee);
-        const bool all = flags && t % 2 == 0;
+        const bool all = flags && !fuzz && t % 2 == 0;
         for (int l = 0; l < WAVE; l++)
             th.emplace_back([&, l] {
                 threadIdx.x = l; t_lane = l; t_wave = 0;
@@ -342,8 +371,8 @@ int main(int argc, char** argv) {
         std::printf("trials %d mismatches %d\n", trials, bad);
         return bad != 0;
     }
-    if (lsm == 4 || lsm == 6) {
-        bad = heap_trials(trials, rng, lsm == 6);
+    if (lsm == 4 || lsm == 6 || lsm == 7) {
+        bad = heap_trials(trials, rng, lsm == 6 || lsm == 7, lsm == 7);
         std::printf("postorder segments %ld\n", (long)g_postorder.load());
         std::printf("trials %d mismatches %d\n", trials, bad);
         return bad != 0;
