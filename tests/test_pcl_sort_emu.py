@@ -103,7 +103,7 @@ def test_heap_postorder_fuzz_edges(emu, seed):
     relevant groups per segment with the largest / smallest / existing keys, members placed at the input's end
     (the danger zone after make_heap); the closed form or the pops (child flags) must leave every >= 3-point
     key's points in libstdc++'s heap-sort order, and the closed form must be taken in some trials."""
-    r = subprocess.run([emu, "24", str(seed), "7"], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([emu, "40", str(seed), "7"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
     assert "postorder segments 0" not in r.stdout
