@@ -1,14 +1,16 @@
 // tests/ps_emu.cpp — host emulation of HIP workgroups running csrc/ls_sort.hpp (+ pcl_sort.hpp's pieces).
 //
-// Every lane is a std::thread; the wave collectives the sort uses (ballot, shfl, readlane /
-// readfirstlane, DPP scans, all-reduces, the wave barrier) are a wave-wide std::barrier around a shared
-// exchange slot, lds_barrier / __syncthreads a workgroup-wide one, the LDS atomics host atomics. The
-// device code is compiled unchanged (PS_HOST_EMU skips its HIP include), so its partition arithmetic,
-// work queue and workgroup phase are checked against libstdc++'s std::sort on the CPU.
+// Every lane is a fiber (ucontext stacks, switched by _setjmp/_longjmp on one OS thread, round robin); the
+// wave collectives the sort uses (ballot, shfl, readlane / readfirstlane, DPP scans, all-reduces, the wave
+// barrier) are a wave-wide fiber barrier around a shared exchange slot, lds_barrier / __syncthreads a
+// workgroup-wide one, the LDS atomics host atomics. The device code is compiled unchanged (PS_HOST_EMU skips
+// its HIP include), so its partition arithmetic, work queue and workgroup phase are checked against
+// libstdc++'s std::sort on the CPU. (Lanes as OS threads spent most of the run in futex wake-ups.)
 // Test infrastructure: built and run by tests/test_pcl_sort_emu.py.
+#undef _FORTIFY_SOURCE        // longjmp between fiber stacks: the fortified check rejects a jump to another stack
 #include <algorithm>
 #include <atomic>
-#include <barrier>
+#include <csetjmp>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -17,7 +19,7 @@
 #include <map>
 #include <memory>
 #include <random>
-#include <thread>
+#include <ucontext.h>
 #include <vector>
 
 #define __device__
@@ -27,16 +29,80 @@
 #define WAVE 64
 
 struct Dim3 { unsigned x = 0, y = 0, z = 0; };
-static thread_local Dim3 threadIdx;
-static thread_local int t_lane = 0, t_wave = 0;
+static Dim3 threadIdx;
+static int t_lane = 0, t_wave = 0;
+
+// ---- fibers: one per emulated lane, all on the calling thread ----
+struct Fiber {
+    ucontext_t uc;
+    jmp_buf jb;
+    char* stack = nullptr;
+    bool started = false, done = false;
+};
+static constexpr size_t FIBER_STACK = 1u << 20;
+static std::vector<Fiber> g_fib;
+static int g_cur = 0, g_live = 0;
+static jmp_buf g_main_jb;
+static std::function<void(int)> g_body;
+
+static void set_ids(int t) { threadIdx.x = (unsigned)t; t_lane = t % WAVE; t_wave = t / WAVE; }
+static void enter(int next) {         // leave the current context for fiber `next` (never returns)
+    g_cur = next;
+    set_ids(next);
+    Fiber& f = g_fib[next];
+    if (!f.started) { f.started = true; setcontext(&f.uc); }
+    _longjmp(f.jb, 1);
+}
+__attribute__((noinline)) static void fiber_yield() {
+    const int n = (int)g_fib.size();
+    int next = g_cur;
+    do next = (next + 1) % n; while (g_fib[next].done && next != g_cur);
+    if (next == g_cur) return;
+    if (_setjmp(g_fib[g_cur].jb)) return;     // resumed by another fiber (ids already set for us)
+    enter(next);
+}
+static void fiber_entry() {
+    g_body(g_cur);
+    g_fib[g_cur].done = true;
+    if (--g_live == 0) _longjmp(g_main_jb, 1);
+    fiber_yield();                            // a done fiber is never resumed
+    std::abort();
+}
+// run body(t) for t in [0, nt) as nt lanes; returns when every lane has returned
+static void run_group(int nt, std::function<void(int)> body) {
+    g_fib = std::vector<Fiber>(nt);
+    g_body = std::move(body);
+    g_live = nt;
+    for (auto& f : g_fib) {
+        f.stack = (char*)std::malloc(FIBER_STACK);
+        getcontext(&f.uc);
+        f.uc.uc_stack.ss_sp = f.stack;
+        f.uc.uc_stack.ss_size = FIBER_STACK;
+        f.uc.uc_link = nullptr;
+        makecontext(&f.uc, fiber_entry, 0);
+    }
+    if (!_setjmp(g_main_jb)) enter(0);
+    for (auto& f : g_fib) std::free(f.stack);
+    g_fib.clear();
+}
+struct FBarrier {
+    int n, count = 0;
+    volatile unsigned gen = 0;
+    explicit FBarrier(int n_) : n(n_) {}
+    void arrive_and_wait() {
+        const unsigned g = gen;
+        if (++count == n) { count = 0; gen = g + 1; return; }
+        while (gen == g) fiber_yield();
+    }
+};
 
 struct WaveCtx {
-    std::unique_ptr<std::barrier<>> bar;
+    std::unique_ptr<FBarrier> bar;
     unsigned long long slot[WAVE];
     unsigned long long out;
 };
 static std::vector<std::unique_ptr<WaveCtx>> g_waves;
-static std::unique_ptr<std::barrier<>> g_block;
+static std::unique_ptr<FBarrier> g_block;
 
 static inline WaveCtx& W() { return *g_waves[t_wave]; }
 static inline void wave_sync() { W().bar->arrive_and_wait(); }
@@ -98,7 +164,7 @@ static inline int __builtin_amdgcn_update_dpp(int old, int src, int ctrl, int, i
 }
 static inline void __builtin_amdgcn_wave_barrier() { wave_sync(); }
 static inline void __builtin_amdgcn_fence(int, const char*) { std::atomic_thread_fence(std::memory_order_seq_cst); }
-static inline void __builtin_amdgcn_s_sleep(int) { std::this_thread::yield(); }
+static inline void __builtin_amdgcn_s_sleep(int) { fiber_yield(); }
 static inline void __syncthreads() { g_block->arrive_and_wait(); }
 static inline int __popc(unsigned x) { return __builtin_popcount(x); }
 static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
@@ -142,20 +208,12 @@ static void run_ls(std::vector<unsigned long long>& E, const unsigned* rel = nul
     g_waves.clear();
     for (int w = 0; w < NT / WAVE; w++) {
         auto c = std::make_unique<WaveCtx>();
-        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        c->bar = std::make_unique<FBarrier>(WAVE);
         g_waves.push_back(std::move(c));
     }
-    g_block = std::make_unique<std::barrier<>>(NT);
+    g_block = std::make_unique<FBarrier>(NT);
     const int d0 = n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0;
-    std::vector<std::thread> th;
-    for (int t = 0; t < NT; t++)
-        th.emplace_back([&, t] {
-            threadIdx.x = t;
-            t_lane = t % WAVE;
-            t_wave = t / WAVE;
-            aloam::ls_sort<NT, CPW>(E.data(), n, d0, (unsigned char*)scr.data(), nmax, rel);
-        });
-    for (auto& x : th) x.join();
+    run_group(NT, [&](int) { aloam::ls_sort<NT, CPW>(E.data(), n, d0, (unsigned char*)scr.data(), nmax, rel); });
 }
 // csrc/ls_sort.hpp's split-to-list + ls_sort_list: one emulated workgroup splits, then nw = 2 workgroups
 // (run one after the other) sort their share of the segments
@@ -168,20 +226,14 @@ static void run_ls_list(std::vector<unsigned long long>& E, int limit, const uns
         g_waves.clear();
         for (int w = 0; w < NT / WAVE; w++) {
             auto c = std::make_unique<WaveCtx>();
-            c->bar = std::make_unique<std::barrier<>>(WAVE);
+            c->bar = std::make_unique<FBarrier>(WAVE);
             g_waves.push_back(std::move(c));
         }
-        g_block = std::make_unique<std::barrier<>>(NT);
-        std::vector<std::thread> th;
-        for (int t = 0; t < NT; t++)
-            th.emplace_back([&, t] {
-                threadIdx.x = t;
-                t_lane = t % WAVE;
-                t_wave = t / WAVE;
+        g_block = std::make_unique<FBarrier>(NT);
+        run_group(NT, [&](int) {
                 if (phase == 0) aloam::ls_split_to_list<NT>(E.data(), n, limit, gseg.data(), (unsigned char*)scr.data(), rel);
                 else aloam::ls_sort_list<NT, CPW>(E.data(), gseg.data(), phase - 1, 2, EL.data(), cap, (unsigned char*)scr.data(), rel);
             });
-        for (auto& x : th) x.join();
     }
 }
 // csrc/ls_sort.hpp's global sort: split in "global" memory by the workgroup phase of pcl_sort.hpp, segments
@@ -193,19 +245,11 @@ static void run_ls_global(std::vector<unsigned long long>& E, int cap) {
     g_waves.clear();
     for (int w = 0; w < NT / WAVE; w++) {
         auto c = std::make_unique<WaveCtx>();
-        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        c->bar = std::make_unique<FBarrier>(WAVE);
         g_waves.push_back(std::move(c));
     }
-    g_block = std::make_unique<std::barrier<>>(NT);
-    std::vector<std::thread> th;
-    for (int t = 0; t < NT; t++)
-        th.emplace_back([&, t] {
-            threadIdx.x = t;
-            t_lane = t % WAVE;
-            t_wave = t / WAVE;
-            aloam::ls_sort_global<NT, CPW>(E.data(), n, EL.data(), cap, (unsigned char*)scr.data());
-        });
-    for (auto& x : th) x.join();
+    g_block = std::make_unique<FBarrier>(NT);
+    run_group(NT, [&](int) { aloam::ls_sort_global<NT, CPW>(E.data(), n, EL.data(), cap, (unsigned char*)scr.data()); });
 }
 
 // csrc/pcl_sort.hpp's wave heap sort (ws_heap_sort: closed form or six-level pops, early stop) on one
@@ -266,18 +310,12 @@ static int heap_trials(int trials, std::mt19937_64& rng, bool flags = false, boo
         for (auto x : E) if (cnt[(unsigned)(x >> 32)] >= 3) { const unsigned i = (unsigned)x & 0xffffu; rel[i >> 5] |= 1u << (i & 31); }
         g_waves.clear();
         auto c = std::make_unique<WaveCtx>();
-        c->bar = std::make_unique<std::barrier<>>(WAVE);
+        c->bar = std::make_unique<FBarrier>(WAVE);
         g_waves.push_back(std::move(c));
-        g_block = std::make_unique<std::barrier<>>(WAVE);
-        std::vector<std::thread> th;
+        g_block = std::make_unique<FBarrier>(WAVE);
         std::vector<unsigned char> F(n, 0xee);
         const bool all = flags && !fuzz && t % 2 == 0;
-        for (int l = 0; l < WAVE; l++)
-            th.emplace_back([&, l] {
-                threadIdx.x = l; t_lane = l; t_wave = 0;
-                aloam::ws_heap_sort(E.data(), 0, n, all ? nullptr : rel.data(), flags ? F.data() : nullptr);
-            });
-        for (auto& x : th) x.join();
+        run_group(WAVE, [&](int) { aloam::ws_heap_sort(E.data(), 0, n, all ? nullptr : rel.data(), flags ? F.data() : nullptr); });
         if (all && E != A) { bad++; std::printf("heap (all pops) mismatch trial %d n %d kinds %u\n", t, n, kinds); continue; }
         auto order = [&](const std::vector<unsigned long long>& X) {
             std::vector<std::pair<unsigned, unsigned>> v;
@@ -326,21 +364,17 @@ static int reduce_trials(int trials, std::mt19937_64& rng) {
             g_waves.clear();
             for (int w = 0; w < NT / WAVE; w++) {
                 auto c = std::make_unique<WaveCtx>();
-                c->bar = std::make_unique<std::barrier<>>(WAVE);
+                c->bar = std::make_unique<FBarrier>(WAVE);
                 g_waves.push_back(std::move(c));
             }
-            g_block = std::make_unique<std::barrier<>>(NT);
-            std::vector<std::thread> th;
+            g_block = std::make_unique<FBarrier>(NT);
             std::vector<int> r(NT);
-            for (int tt = 0; tt < NT; tt++)
-                th.emplace_back([&, tt] {
-                    threadIdx.x = tt; t_lane = tt % WAVE; t_wave = tt / WAVE;
+            run_group(NT, [&](int tt) {
                     auto pt = [&](int i) { return P[i]; };
                     auto of = [&](int q, float4 v) { out[form][q] = v; };
                     r[tt] = form == 0 ? aloam::rvg_reduce_loop<NT>(S.data(), n, rel.data(), fpos.data(), pt, of, sc.data())
                                       : aloam::rvg_reduce_batched<NT, 8>(S.data(), n, rel.data(), fpos.data(), pt, of, sc.data());
                 });
-            for (auto& x : th) x.join();
             tot[form] = r[0];
         }
         if (tot[0] != tot[1] || std::memcmp(out[0].data(), out[1].data(), sizeof(float4) * (size_t)tot[0]) != 0) {
