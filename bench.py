@@ -314,7 +314,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # timed region: plain throughput (no per-kernel events, so the round loops run as HIP graphs)
+    # timed region: plain throughput (no per-kernel events)
     if args.mode == "serial":
         for k in range(W, W + K):
             od, mp = ctx.process_scan(device_ptr=d_frames[k].data_ptr(), n=n_pts[k])

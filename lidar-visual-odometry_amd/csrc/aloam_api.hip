@@ -183,7 +183,9 @@ static void allocate(Ctx& C) {
     C.d_last_sorted = (int*)dalloc(C, sizeof(int) * 2);
     C.d_odom_nq = (int*)dalloc(C, sizeof(int) * 2);
     lm_init(C);
-    C.use_graphs = getenv("ALOAM_NO_GRAPHS") == nullptr;
+    // round loops issued eagerly by default: replaying them as HIP graphs measured ~1 % slower on the driver's
+    // config (graph entry / exit ~10 us per replay, profiles/r05_graph_ab.txt); ALOAM_GRAPHS=1 replays graphs
+    C.use_graphs = getenv("ALOAM_GRAPHS") != nullptr && getenv("ALOAM_NO_GRAPHS") == nullptr;
     C.d_cand = C.d_out->cand;
     // mapping
     const int M = std::max(P.max_map_points, 1024);
