@@ -1292,9 +1292,12 @@ static void rebuild_maps(Ctx& C, const float4* cstack, const float4* sstack, con
     k_rb_scatter<<<dim3(nblk(n_old + ub), 2), MB, 0, st>>>(P);
     prof_phase(C, Ctx::PM_MAP_ADD);
     // tuning knobs: segment size of the split cubes' parallel sorts; cubes up to `fit` points are sorted
-    // whole by their own workgroup, larger ones split
+    // whole by their own workgroup, larger ones split. fit 2048 (round 5, was RVG_FIT = 4096): the slowest
+    // cubes of a frame were in-LDS cubes of ~3900 points whose heap-sorted segments queued on the workgroup's
+    // 4 waves; split, their segments spread over workgroups (profiles/r05_cube_fit_ab.txt: 1024 / 1536 /
+    // 2048 / 3072 / 4096 -> 2048 best, C3 50 steps 1025 vs 992 scans/s)
     static const int seg_limit = getenv("ALOAM_CUBE_SEG") ? std::max(2048, std::min(RBV_CAP, atoi(getenv("ALOAM_CUBE_SEG")))) : 4096;
-    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(512, std::min(RVG_FIT, atoi(getenv("ALOAM_CUBE_FIT")))) : RVG_FIT;
+    static const int fit = getenv("ALOAM_CUBE_FIT") ? std::max(512, std::min(RVG_FIT, atoi(getenv("ALOAM_CUBE_FIT")))) : std::min(RVG_FIT, 2048);
     // ALOAM_RB_FORK=1: the cubes sorted in LDS on stream2 beside the split cubes' chain (split, segment sorts,
     // sums) on the frame's stream. Off by default: measured slower (C3 20 steps 867-870 vs 881-882 scans/s,
     // steady state 798-801 vs 819-821, profiles/r05_fork_ab.txt; the mapping rounds of the next frames ran
