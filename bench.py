@@ -75,13 +75,14 @@ def c4_traffic(timeout_s=240):
     """HBM-side bytes per launch of the C4 search kernel: one rocprofv3 PMC pass (FETCH_SIZE only, no
     traces) over a child `bench.py --c4-only`, corrected as MI355X_MICROARCH.md prescribes for
     gfx950 (FETCH_SIZE is in KiB and reports half the bytes of 16-B/lane streaming reads: x1024 x2).
-    Infinity-Cache hits are counted too, so this is an upper bound on HBM reads. None on any failure."""
+    Infinity-Cache hits are counted too, so this is an upper bound on HBM reads. Returns (bytes, None), or
+    (None, reason) on any failure: the reason goes into the line (roofline.traffic_error)."""
     import csv
     import shutil
     import subprocess
     import tempfile
     if not shutil.which("rocprofv3"):
-        return None
+        return None, "rocprofv3 not on PATH"
     out = tempfile.mkdtemp(prefix="c4pmc_", dir="/tmp")
     # the child is a single-process run on this rank's GPU: drop the torchrun rendezvous variables, or
     # under --gpus N it would try to join the job's process group as a second rank 0
@@ -98,18 +99,24 @@ def c4_traffic(timeout_s=240):
     cmd = ["rocprofv3", "--pmc", "FETCH_SIZE", "-d", out, "-o", "run", "--output-format", "csv", "--",
            sys.executable, os.path.abspath(__file__), "--c4-only", "--c4-launches", "3"]
     try:
-        subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout_s, check=True, capture_output=True)
-        vals = []
+        r = subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout_s, capture_output=True, text=True)
+        if r.returncode != 0:
+            tail = (r.stderr or r.stdout or "").strip().splitlines()[-3:]
+            return None, f"rocprofv3 exit {r.returncode}: " + " | ".join(tail)[-400:]
+        vals, names = [], set()
         for root, _, files in os.walk(out):
             for f in files:
                 if f.endswith("counter_collection.csv"):
-                    for r in csv.DictReader(open(os.path.join(root, f))):
+                    for row in csv.DictReader(open(os.path.join(root, f))):
+                        names.add(row.get("Kernel_Name", "?")[:60])
                         # the timed instance only (CNT = false); the counting instance runs untimed beside it
-                        if re.search(r"k_knn_\w+<\d+, \d+, false>", r["Kernel_Name"]) and r["Counter_Name"] == "FETCH_SIZE":
-                            vals.append(float(r["Counter_Value"]))
-        return float(np.median(vals)) * 1024.0 * 2.0 if vals else None
-    except Exception:
-        return None
+                        if re.search(r"k_knn_\w+<\d+, \d+, false", row["Kernel_Name"]) and row["Counter_Name"] == "FETCH_SIZE":
+                            vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None, f"no FETCH_SIZE row for the timed k_knn instance (kernels seen: {sorted(names)[:6]})"
+        return float(np.median(vals)) * 1024.0 * 2.0, None
+    except Exception as e:  # noqa: BLE001
+        return None, repr(e)[-400:]
     finally:
         shutil.rmtree(out, ignore_errors=True)
 
@@ -472,7 +479,7 @@ def main():
     if rank == 0 and args.c4_launches > 0:
         c4 = c4_search(lvo, torch, dev, args.c4_launches)
         ach = c4["bytes"] / (c4["ms"] * 1e-3) / 1e9
-        traffic = None if args.no_traffic else c4_traffic()
+        traffic, traffic_err = (None, "skipped (--no-traffic)") if args.no_traffic else c4_traffic()
         hbm_ach = traffic / (c4["ms"] * 1e-3) / 1e9 if traffic else None
         # the search roofline is judged on C4; the C3 kernel is latency-bound (roofline_c3).
         # Bound from the evidence: the 33 MB map stays on die (FETCH_SIZE << algorithmic bytes, TCC hit rate
@@ -490,6 +497,7 @@ def main():
             "unit": "GB/s",
             "frac": round(st_ach / L2_GATHER_GBS, 4),
             "traffic": traffic,
+            "traffic_error": traffic_err,
             "avg_launch_us": round(c4["ms"] * 1000.0, 2),
             "algorithmic_bytes_per_launch": round(c4["streamed"], 0),
             "note": "bound from the evidence: the 33 MB map is re-read on die (traffic = rocprofv3 FETCH_SIZE per launch, "

@@ -980,6 +980,14 @@ void scan_registration_launch(Ctx& C, const float4* in, int n, bool side) {
     } else {
         prof_phase(C, Ctx::PM_SCAN_PREP);
         prof_phase(C, Ctx::PM_SCAN_CURV);
+        if (side) {
+            // an empty sweep still orders stream2 after k_meta_init: the early mapping stacks
+            // (do_odometry_issue) read this scan's counts and last clouds on stream2, and the
+            // counts copy waits on ev_lf, which must mark this registration, not an older one
+            HIPCHK(hipEventRecord(C.ev_scan, st));
+            HIPCHK(hipStreamWaitEvent(C.stream2, C.ev_scan, 0));
+            HIPCHK(hipEventRecord(C.ev_lf, C.stream2));
+        }
     }
     HIPCHK(hipGetLastError());
 }

@@ -573,6 +573,52 @@ def test_pipeline_side_stream_stacks(lvo):
         np.testing.assert_allclose(m[3:], m_ref["q_w_curr"], rtol=1e-9, atol=1e-12)
 
 
+_EARLY_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from lvo_amd_loader import lvo
+synth = lvo.synth
+p = lvo.abi.default_params(64)
+frames = [synth.scan("hdl64", k) for k in range(3)]
+frames = frames + [frames[0][:0]] + [synth.scan("hdl64", k) for k in range(3, 6)]
+pipe = lvo.Pipeline(p)
+rows = []
+def keep(od, mp):
+    if mp is not None:
+        rows.append([int(mp[k]) for k in ("corner_stack_num", "surf_stack_num", "map_corner_num", "map_surf_num")]
+                    + [float(v).hex() for v in list(mp["t_w_curr"]) + list(mp["q_w_curr"])])
+for f in frames:
+    keep(*pipe.push(f))
+for od, mp in pipe.flush():
+    keep(od, mp)
+pipe.close()
+print(json.dumps(rows))
+"""
+
+
+def test_pipeline_early_stacks_with_empty_sweep():
+    """ALOAM_EARLY_STACKS (read once per process, so each schedule in a child): the mapping stacks read from the
+    last-cloud buffers with counts copied on stream2 (1, default) and from the publish copy (0) give the same
+    stack counts, map counts and bit-identical poses, over a sequence with an EMPTY sweep between full ones
+    (stream2 must be ordered after the empty registration's k_meta_init, not read the previous scan's counts)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    for early in ("0", "1"):
+        env = dict(os.environ, ALOAM_EARLY_STACKS=early)
+        out = subprocess.run([sys.executable, "-c", _EARLY_SCRIPT, here], env=env, capture_output=True, text=True,
+                             timeout=110, cwd=here)
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+        res[early] = json.loads(out.stdout.strip().splitlines()[-1])
+    assert len(res["1"]) == 7, len(res["1"])
+    assert res["0"] == res["1"]
+    assert res["1"][3][:2] == [0, 0]                  # the empty sweep's stacks are empty, not the previous scan's
+
+
 def test_pipeline_errors_and_timing(lvo):
     """The native pipeline reports stage errors through aloam_pipeline_last_error and stays usable;
     with profiling on, every stage's HIP-event timing of its last job is available."""

@@ -156,6 +156,58 @@ def test_s2m_c4_scale_device_resident(gpu_ctx_factory):
         assert np.array_equal(r["x"].view(np.uint64), g["x"].view(np.uint64))
 
 
+def test_s2m_c4_full_size_vs_oracle(gpu_ctx_factory):
+    """BASELINE configs[3] parity-tested at its own size: the whole 128-line sweep (232k surf + 29k corner
+    queries) against the ~2.1M-point map, 2 registration rounds (laserMapping.cpp:562 with 2 instead of
+    10, the bench's oracle sample) on the GPU and through the oracle (leaf-15 kd-trees, Eigen fits,
+    Ceres-style LM): pose within 1e-6 relative, per-round correspondence counts and LM iteration counts
+    equal."""
+    import torch
+
+    cm, sm, cq, sq, x0, _ = synth.c4_registration()
+    p = abi.default_params(128)
+    p.map_rounds = 2
+    dev = torch.device("cuda", 0)
+    dm, dcq, dsq = (torch.from_numpy(a).to(dev) for a in (cm, cq, sq))
+    ctx = gpu_ctx_factory(128, max_scan_points=1024, max_map_points=1024, map_rounds=2)
+    ctx.s2m_set_map(dm.data_ptr(), dm.data_ptr(), len(cm), len(sm))
+    ctx.s2m_set_queries(dcq.data_ptr(), dsq.data_ptr(), len(cq), len(sq))
+    g = ctx.s2m_register(x0)
+    p.max_scan_points, p.max_map_points = 1024, 1024
+    o = ob.s2m_register(p, cm, sm, cq, sq, x0)
+    assert g["rounds"] == o["rounds"] == 2
+    assert g["corner_num"] == o["corner_num"] and g["surf_num"] == o["surf_num"], (g["surf_num"], o["surf_num"])
+    assert [l[0] for l in g["lm"]] == [l[0] for l in o["lm"]]
+    assert rel(g["x"], o["x"]) <= POSE_RTOL, (g["x"], o["x"])
+    assert min(g["surf_num"]) >= 0.7 * len(sq)
+
+
+def test_knn_device_c4_full_map_vs_oracle(gpu_ctx_factory):
+    """The roofline configuration itself (bench.py c4_search): 128-line sweep vs the 2.09M-point map on the
+    0.107 m lattice through aloam_knn_device; a 3,000-query sample equals the oracle's kd-tree radius 5-NN
+    (indices and distance bits), and every query's slots are written."""
+    import torch
+
+    m = synth.dense_map(4, 0.0, 0.0, step=0.107)
+    R, o = synth.pose("l128", 0)
+    s = synth.scan("l128", 0)
+    q = s.copy()
+    q[:, :3] = (s[:, :3].astype(np.float64) @ R.T + o).astype(np.float32)
+    dm, dq = torch.from_numpy(m).cuda(), torch.from_numpy(q).cuda()
+    idx = torch.full((len(q), 5), -7, dtype=torch.int32, device="cuda")
+    d2 = torch.empty((len(q), 5), dtype=torch.float32, device="cuda")
+    ctx = gpu_ctx_factory(128)
+    ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), 5, 1.0, idx.data_ptr(), d2.data_ptr())
+    gi, gd = idx.cpu().numpy(), d2.cpu().numpy()
+    assert len(m) > 2_000_000 and (gi >= -1).all()
+    sel = np.random.default_rng(6).choice(len(q), 3000, replace=False)
+    oi, od = ob.knn(m, q[sel], 5, 1.0)
+    assert np.array_equal(gi[sel], oi)
+    ok = oi >= 0
+    assert np.array_equal(gd[sel][ok].view(np.uint32), od[ok].view(np.uint32))
+    assert (gi[:, 4] >= 0).mean() > 0.9
+
+
 @pytest.mark.parametrize("batch_min,fine_cell,split", [("1", "0.3", "0"), ("1", "0", "0"), ("100000000", "0.3", "0"),
                                                       ("100000000", "0.15", "0"), ("1", "0.3", "1"), ("1", "0", "1")])
 def test_s2m_assoc_paths_bit_identical(gpu_ctx_factory, monkeypatch, batch_min, fine_cell, split):
