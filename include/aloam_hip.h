@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ALOAM_ABI_VERSION 5
+#define ALOAM_ABI_VERSION 6
 
 /* error codes */
 #define ALOAM_OK             0
@@ -248,7 +248,17 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
  * Replaces the KdTreeFLANN::nearestKSearch calls of laserMapping.cpp:582,648 at C4 scale. */
 int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k,
                      float radius, int* d_idx, float* d_d2);
-/* Name of the search kernel the context's last aloam_knn_device call launched (e.g. "k_knn_2phase<5,8>";
+/* The same search split into build and query, so repeated queries against one map pay for the
+ * index once — laserMapping.cpp builds its map kd-trees once per frame (kdtreeCornerFromMap /
+ * kdtreeSurfFromMap->setInputCloud, :558-559) and queries them in every round (nearestKSearch, :582,
+ * :648). aloam_knn_build indexes the n device float4 points for radius-`radius` searches (both grids of
+ * the two-phase search; the points are copied into the index, so d_pts may change afterwards);
+ * aloam_knn_query answers nq device queries against the last built index (same results as
+ * aloam_knn_device with the same points and radius; ALOAM_E_STATE before any build). Synchronous.
+ * aloam_knn_device = aloam_knn_build + aloam_knn_query. */
+int aloam_knn_build(aloam_ctx* ctx, const float* d_pts, int n, float radius);
+int aloam_knn_query(aloam_ctx* ctx, const float* d_queries, int nq, int k, int* d_idx, float* d_d2);
+/* Name of the search kernel the context's last aloam_knn_device / aloam_knn_query call launched (e.g. "k_knn_2phase<5,8>";
  * "" before the first call), so a timing of that call can be attributed to a kernel. ALOAM_KNN_TILE=1
  * (read per call) selects the LDS-tiled phase 1 ("k_knn_tile<...>"). Valid until the next call. */
 const char* aloam_knn_kernel(const aloam_ctx* ctx);
@@ -288,6 +298,7 @@ typedef struct aloam_timing {
     int   knn_launches;
     double knn_bytes;         /* its algorithmic bytes: sum_q (16 + 16 |C27(q)|) + 8 k Q         */
     double knn_streamed_bytes;/* bytes it actually streamed (both phases of the two-phase search)   */
+    float knn_build_ms;       /* aloam_knn_build / aloam_knn_device: index build time (HIP events)  */
     /* the reference's TicToc stage surface (tic_toc.h; printed by the three nodes), GPU time of the
      * same phases from HIP events on the stage's stream, indexed by ALOAM_TT_* below */
     float tictoc_ms[ALOAM_TICTOC_N];

@@ -62,6 +62,8 @@ def _declare(L):
     L.aloam_get_timing.argtypes = [vp, C.POINTER(abi.Timing)]
     L.aloam_forward_mapping_input.argtypes = [vp, vp]
     L.aloam_knn_device.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int, C.c_float, vp, vp]
+    L.aloam_knn_build.argtypes = [vp, vp, C.c_int, C.c_float]
+    L.aloam_knn_query.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp]
     L.aloam_forward_features.argtypes = [vp, vp]
     L.aloam_s2m_set_map.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int]
     L.aloam_s2m_set_queries.argtypes = [vp, vp, C.c_int, vp, C.c_int, C.c_int]
@@ -94,7 +96,7 @@ def _declare(L):
     for name in ("aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
                  "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range"):
         getattr(L, name).restype = C.c_int
-    for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_forward_features", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
+    for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_knn_build", "aloam_knn_query", "aloam_forward_features", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
                  "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
                  "aloam_get_map_cloud", "aloam_get_registered_cloud", "aloam_process_scan", "aloam_eval_factors",
                  "aloam_lm_solve", "aloam_voxel_grid", "aloam_knn", "aloam_set_profiling", "aloam_get_timing"):
@@ -132,7 +134,7 @@ EXPORTED_SYMBOLS = [
     "aloam_scan_registration_pc2", "aloam_set_cu_mask", "aloam_serial_sort_fallbacks",
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
-    "aloam_map_high_freq_pose", "aloam_knn_kernel",
+    "aloam_map_high_freq_pose", "aloam_knn_kernel", "aloam_knn_build", "aloam_knn_query",
 ]
 
 
@@ -318,6 +320,15 @@ class Context:
         """aloam_knn_device on device pointers (ints, e.g. torch tensor .data_ptr())."""
         self._check(lib().aloam_knn_device(self.h, C.c_void_p(d_pts), int(n), C.c_void_p(d_queries), int(nq), int(k),
                                            float(radius), C.c_void_p(d_idx), C.c_void_p(d_d2)))
+
+    def knn_build(self, d_pts, n, radius):
+        """aloam_knn_build: index n device float4 points for radius searches (built once, queried many times)."""
+        self._check(lib().aloam_knn_build(self.h, C.c_void_p(d_pts), int(n), float(radius)))
+
+    def knn_query(self, d_queries, nq, k, d_idx, d_d2):
+        """aloam_knn_query against the last knn_build index (device pointers)."""
+        self._check(lib().aloam_knn_query(self.h, C.c_void_p(d_queries), int(nq), int(k), C.c_void_p(d_idx),
+                                          C.c_void_p(d_d2)))
 
     def knn_kernel(self):
         """Name of the search kernel the last knn_device call launched (aloam_knn_kernel)."""

@@ -133,6 +133,7 @@ class Timing(C.Structure):
         ("odom_search_launches", C.c_int), ("map_search_launches", C.c_int),
         ("map_search_bytes", C.c_double), ("odom_search_bytes", C.c_double),
         ("knn_ms", C.c_float), ("knn_launches", C.c_int), ("knn_bytes", C.c_double), ("knn_streamed_bytes", C.c_double),
+        ("knn_build_ms", C.c_float),
         ("tictoc_ms", C.c_float * 17),
     ]
 

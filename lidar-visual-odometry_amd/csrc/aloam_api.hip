@@ -1442,11 +1442,12 @@ int aloam_knn(aloam_ctx* ctx, const float* pts, int n, const float* queries, int
     API_END
 }
 
-int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k, float radius,
-                     int* d_idx, float* d_d2) {
-    API_BEGIN(ctx)
-    if (n < 0 || nq < 0 || k < 1 || k > 8 || !(radius > 0) || (n > 0 && !d_pts) || (nq > 0 && (!d_queries || !d_idx || !d_d2)))
-        throw ApiError{ALOAM_E_ARG, "bad knn args (device pointers, radius > 0, 1 <= k <= 8)"};
+// aloam_knn_build / aloam_knn_query: the map index is built once (both grids of the two-phase search, in
+// context memory grown on demand) and then queried any number of times — the split of laserMapping.cpp's
+// kdtree*FromMap->setInputCloud (:558-559, once per frame) and nearestKSearch (:582, :648, every round)
+static void knn_build(Ctx& C, const float* d_pts, int n, float radius) {
+    if (n < 0 || !(radius > 0) || (n > 0 && !d_pts)) throw ApiError{ALOAM_E_ARG, "bad knn build args (device pointer, radius > 0)"};
+    C.knn_built = false;
     if (!C.d_knn_n) C.d_knn_n = (int*)dalloc(C, sizeof(int) * 2);
     if (C.g_knn.cap < std::max(n, 1)) {          // grow (old buffers are released with the context)
         Grid g{};
@@ -1454,7 +1455,7 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
         C.g_knn = g;
     }
     C.g_knn.min_cell = radius * 1.025f;           // cells >= radius: the 27-cell block holds the ball
-    const char* fe = getenv("ALOAM_KNN_FINE");    // read per call (tests compare both paths in one process)
+    const char* fe = getenv("ALOAM_KNN_FINE");    // read per build (tests compare both paths in one process)
     const float fine_frac = fe ? (float)atof(fe) : 0.3f;
     const bool two_phase = fine_frac > 0.f && fine_frac < 1.f;
     if (two_phase && C.g_knn_fine.cap < std::max(n, 1)) {   // grown on demand (the old grid given back)
@@ -1465,6 +1466,7 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
         C.g_knn_fine = g;
     }
     set_counts2(C, C.d_knn_n, n, 0);
+    if (C.profiling) HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 2], C.stream));
     if (two_phase) {
         C.g_knn_fine.min_cell = radius * fine_frac;
         const GridBuild b[2] = {{&C.g_knn, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr},
@@ -1473,10 +1475,24 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
     } else {
         grid_build(C, C.g_knn, (const float4*)d_pts, C.d_knn_n, std::max(n, 1), nullptr, nullptr);
     }
+    if (C.profiling) HIPCHK(hipEventRecord(C.ev[Ctx::NEV - 1], C.stream));
+    sync(C);
+    if (C.profiling) C.timing.knn_build_ms = ev_ms(C, Ctx::NEV - 2, Ctx::NEV - 1);
+    C.knn_built = true;
+    C.knn_two_phase = two_phase;
+    C.knn_radius = radius;
+    C.knn_n = n;
+}
+
+static void knn_query(Ctx& C, const float* d_queries, int nq, int k, int* d_idx, float* d_d2) {
+    if (!C.knn_built) throw ApiError{ALOAM_E_STATE, "aloam_knn_query before aloam_knn_build"};
+    if (nq < 0 || k < 1 || k > 8 || (nq > 0 && (!d_queries || !d_idx || !d_d2)))
+        throw ApiError{ALOAM_E_ARG, "bad knn query args (device pointers, 1 <= k <= 8)"};
+    const float radius = C.knn_radius;
     // profiling: the timed launch runs without candidate counters (one same-address atomic per wave
     // would be on the measured path); an untimed second launch (identical results) counts them
     auto launch = [&](unsigned long long* cnt) {
-        if (two_phase)
+        if (C.knn_two_phase)
             knn_device_2phase_launch(C, C.g_knn_fine, C.g_knn, (const float4*)d_queries, nq, k, radius, d_idx, d_d2, cnt);
         else
             knn_device_launch(C, C.g_knn, (const float4*)d_queries, nq, k, radius, d_idx, d_d2, cnt);
@@ -1500,6 +1516,27 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
         C.timing.knn_bytes = 16.0 * nq + 16.0 * (double)cand[0] + 8.0 * k * (double)nq;
         C.timing.knn_streamed_bytes = 16.0 * nq + 16.0 * (double)cand[1] + 8.0 * k * (double)nq;
     }
+}
+
+int aloam_knn_build(aloam_ctx* ctx, const float* d_pts, int n, float radius) {
+    API_BEGIN(ctx)
+    knn_build(C, d_pts, n, radius);
+    API_END
+}
+
+int aloam_knn_query(aloam_ctx* ctx, const float* d_queries, int nq, int k, int* d_idx, float* d_d2) {
+    API_BEGIN(ctx)
+    knn_query(C, d_queries, nq, k, d_idx, d_d2);
+    API_END
+}
+
+int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_queries, int nq, int k, float radius,
+                     int* d_idx, float* d_d2) {
+    API_BEGIN(ctx)
+    if (n < 0 || nq < 0 || k < 1 || k > 8 || !(radius > 0) || (n > 0 && !d_pts) || (nq > 0 && (!d_queries || !d_idx || !d_d2)))
+        throw ApiError{ALOAM_E_ARG, "bad knn args (device pointers, radius > 0, 1 <= k <= 8)"};
+    knn_build(C, d_pts, n, radius);
+    knn_query(C, d_queries, nq, k, d_idx, d_d2);
     API_END
 }
 

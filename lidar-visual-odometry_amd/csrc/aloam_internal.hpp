@@ -180,6 +180,10 @@ struct Ctx {
     Grid g_knn_fine;                // its fine grid (first search phase, k_knn_2phase)
     char knn_kernel[48] = "";        // the search kernel the last aloam_knn_device call launched
     int* d_knn_n = nullptr;
+    // aloam_knn_build's index (the map's two grids), queried by aloam_knn_query until the next build
+    bool knn_built = false, knn_two_phase = false;
+    float knn_radius = 0.f;
+    int knn_n = 0;
     aloam_factor* d_factors = nullptr;
     int cap_factors = 0;
     LMState* d_lm = nullptr;

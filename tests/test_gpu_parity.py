@@ -335,6 +335,52 @@ def test_knn_device_c4_scale(gpu_ctx_factory):
 
 
 @pytest.mark.gpu
+def test_knn_build_once_query_many(gpu_ctx_factory):
+    """aloam_knn_build + aloam_knn_query (the kd-tree built once per map, laserMapping.cpp:558-559, queried
+    every round, :582/:648): several queries against one build equal aloam_knn_device call for call (bit
+    for bit), the index holds its own copy of the points (the map buffer may change after the build), a
+    rebuild over another map answers for that map, and a query before any build is ALOAM_E_STATE."""
+    import torch
+    m = synth.dense_map(4, 0.0, 0.0, step=0.25)
+    R, o = synth.pose("l128", 0)
+    s = synth.scan("l128", 0)
+    q = s.copy()
+    q[:, :3] = (s[:, :3].astype(np.float64) @ R.T + o).astype(np.float32)
+    dm, dq = torch.from_numpy(m).cuda(), torch.from_numpy(q).cuda()
+    ctx = gpu_ctx_factory(128)
+    with pytest.raises(lvo.ALOAMError):
+        ctx.knn_query(dq.data_ptr(), len(q), 5, dq.data_ptr(), dq.data_ptr())
+
+    def run(fn, k, n_q):
+        idx = torch.full((n_q, k), -7, dtype=torch.int32, device="cuda")
+        d2 = torch.full((n_q, k), -7.0, dtype=torch.float32, device="cuda")
+        fn(idx, d2)
+        return idx.cpu().numpy(), d2.cpu().numpy().view(np.uint32)
+
+    ref5 = run(lambda i, d: ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), 5, 1.0, i.data_ptr(), d.data_ptr()), 5, len(q))
+    ref3 = run(lambda i, d: ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr() + 16 * 1000, 5000, 3, 1.0, i.data_ptr(),
+                                           d.data_ptr()), 3, 5000)
+    ctx.knn_build(dm.data_ptr(), len(m), 1.0)
+    dm.fill_(1e6)                                         # the index keeps its own sorted copy
+    for _ in range(2):
+        g5 = run(lambda i, d: ctx.knn_query(dq.data_ptr(), len(q), 5, i.data_ptr(), d.data_ptr()), 5, len(q))
+        g3 = run(lambda i, d: ctx.knn_query(dq.data_ptr() + 16 * 1000, 5000, 3, i.data_ptr(), d.data_ptr()), 3, 5000)
+        assert np.array_equal(g5[0], ref5[0]) and np.array_equal(g5[1], ref5[1])
+        assert np.array_equal(g3[0], ref3[0]) and np.array_equal(g3[1], ref3[1])
+    assert (ref5[0][:, 4] >= 0).mean() > 0.3
+    # rebuild over another map (a shifted half): the oracle on a sample
+    m2 = m[::2].copy()
+    m2[:, 0] += 0.05
+    dm2 = torch.from_numpy(m2).cuda()
+    ctx.knn_build(dm2.data_ptr(), len(m2), 1.0)
+    gi, gd = run(lambda i, d: ctx.knn_query(dq.data_ptr(), len(q), 5, i.data_ptr(), d.data_ptr()), 5, len(q))
+    sel = np.random.default_rng(3).choice(len(q), 2000, replace=False)
+    oi, od = ob.knn(m2, q[sel], 5, 1.0)
+    assert np.array_equal(gi[sel], oi)
+    assert np.array_equal(gd[sel][oi >= 0], od[oi >= 0].view(np.uint32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("step,k,radius,frac", [(0.107, 5, 1.0, "0.3"), (0.15, 8, 1.0, "0.2"), (0.5, 5, 1.0, "0.3"),
                                                 (0.107, 3, 0.5, "0.45")])
 def test_knn_device_two_phase_bit_identical(gpu_ctx_factory, monkeypatch, step, k, radius, frac):
