@@ -424,7 +424,8 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
                                            const int* __restrict__ start, const float4* __restrict__ spts,
                                            const int* __restrict__ sidx, float qx, float qy, float qz, float r2, bool active,
                                            int* out_pos, float* out_d2, int* out_idx, int* ncand, int* tab, int npts,
-                                           const KnnCollect col = KnnCollect{0.f, nullptr, nullptr, 0}, int* ncol = nullptr) {
+                                           const KnnCollect col = KnnCollect{0.f, nullptr, nullptr, 0}, int* ncol = nullptr,
+                                           float prune = INFINITY) {
     const int gl = lane_id() & (GS - 1);
     int total;
     {
@@ -487,7 +488,9 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
                 if (take && slot < col.cap) { col.pts[slot] = v[u]; col.pos[slot] = ps[u]; }
                 nc += __popcll(gm);
             }
-            if (!(d2 < r2) || d2 > bd[K - 1]) continue;
+            // prune: an upper bound of the group's k-th distance known before the search (a candidate
+            // strictly beyond it cannot enter the top k; one AT it still can, by index)
+            if (!(d2 < r2) || d2 > fminf(bd[K - 1], prune)) continue;
             const int iu = IDXW ? __float_as_int(v[u].w) : id[u];
             if (d2 < bd[K - 1] || iu < bi[K - 1]) {
                 float nd = d2; int ni = iu, np = ps[u];

@@ -367,12 +367,12 @@ __device__ __forceinline__ int block27_total(const GridDesc& gd, const int* __re
 // dense map (C4: the 5 neighbours within ~0.15 m, ~1000 points in the coarse block) phase 1 streams
 // ~10x fewer candidates. cand (profiling): [0] += C27(q) of the coarse block (SURVEY §8(d)'s
 // algorithmic count), [1] += candidates actually streamed by both phases.
-template <int K, int GS, bool CNT, int U = 4>
+template <int K, int GS, bool CNT, int U = 4, bool WP2 = true>
 __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
                                                     const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
                                                     const int* __restrict__ cstart, const float4* __restrict__ cpts,
                                                     const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
-                                                    float* __restrict__ d2, unsigned long long* cand) {
+                                                    float* __restrict__ d2, unsigned long long* cand, int exp) {
     __shared__ int tabs[256 / GS][20];
     const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / GS;
     const bool live = qi < nq;
@@ -387,9 +387,36 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
 #pragma unroll
     for (int j = 0; j < K; j++) if (j == k - 1) dk = od[j];
     const float lim = 0.99f * gf.cell;
-    const bool need = live && !(f >= k && dk < lim * lim);
+    const bool need = live && !(f >= k && dk < lim * lim) && !(exp & 1);
     const GridDesc gc = *cgd;
-    if (__any(need)) {                         // wave-uniform: every lane takes part in the group search
+    const int gl = lane_id() & (GS - 1);
+    if constexpr (WP2) {
+        // Phase 2 by the whole wave, one unsettled query at a time: the coarse block holds ~10x the fine
+        // block's points, so with GS lanes per query a single unsettled query kept its wave ~10x longer than
+        // the settled ones; with 64 lanes its block streams in about as many load rounds as phase 1. The
+        // phase-1 k-th distance (when k were found) bounds phase 2's (its candidates are a superset), so
+        // candidates beyond it skip the insertion.
+        unsigned long long todo = __ballot(need && gl == 0);
+        int* wtab = tabs[(threadIdx.x & ~(WAVE - 1)) / GS];
+        while (todo) {
+            const int l = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const float x = readlane_f(qq.x, l), y = readlane_f(qq.y, l), z = readlane_f(qq.z, l);
+            const float pr = f >= k ? dk : INFINITY;
+            const float prl = readlane_f(pr, l);
+            int p2[K], i2[K], n2 = 0;
+            float e2[K];
+            const int f2 = group_knn27<K, WAVE, true, U>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts,
+                                                         nullptr, x, y, z, r2, true, p2, e2, i2, &n2, wtab, gc.n,
+                                                         KnnCollect{0.f, nullptr, nullptr, 0}, nullptr, prl);
+            if ((lane_id() & ~(GS - 1)) == (l & ~(GS - 1))) {
+#pragma unroll
+                for (int j = 0; j < K; j++) { od[j] = e2[j]; oi[j] = i2[j]; }
+                f = f2;
+                nc = n2;
+            }
+        }
+    } else if (__any(need)) {                  // wave-uniform: every lane takes part in the group search
         int p2[K], i2[K];
         float e2[K];
         const int f2 = group_knn27<K, GS, true, U>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, nullptr,
@@ -400,7 +427,6 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
             f = f2;
         }
     }
-    const int gl = lane_id() & (GS - 1);
     if (live) {
 #pragma unroll
         for (int j = 0; j < K; j++)
@@ -619,18 +645,27 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
         return;
     }
     // CNT: the candidate-counting instance (profiling), a separate symbol so kernel traces tell it apart.
-    // ALOAM_KNN_U (tuning knob, read per call): candidate loads in flight per lane, 4 (default) or 8
+    // ALOAM_KNN_U (tuning knob, read per call): candidate loads in flight per lane, 4 (default) or 8.
+    // ALOAM_KNN_P2 (A/B knob, read per call): 0 = phase 2 by each query's own GS-lane group (round 5),
+    // default 1 = by the whole wave. ALOAM_KNN_EXP (profiling experiments only, results invalid): 1 = no phase 2.
     const char* ue = getenv("ALOAM_KNN_U");
     const bool u8 = ue && atoi(ue) == 8;
-#define KNN2(KK, CN, UU) k_knn_2phase<KK, GS, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+    const char* pe = getenv("ALOAM_KNN_P2");
+    const bool wp2 = !(pe && atoi(pe) == 0);
+    const char* xe = getenv("ALOAM_KNN_EXP");
+    const int exp = xe ? atoi(xe) : 0;
+    std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<%d,%d%s%s>", k <= 5 ? 5 : 8, GS, u8 ? ",U8" : "",
+                  wp2 ? "" : ",P2G");
+#define KNN2(KK, CN, UU, WP) k_knn_2phase<KK, GS, CN, UU, WP><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp)
+#define KNN2W(KK, CN, UU) do { if (wp2) KNN2(KK, CN, UU, true); else KNN2(KK, CN, UU, false); } while (0)
     if (u8) {
-        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<%d,%d,U8>", k <= 5 ? 5 : 8, GS);
-        if (k <= 5) { if (cand) KNN2(5, true, 8); else KNN2(5, false, 8); }
-        else { if (cand) KNN2(8, true, 8); else KNN2(8, false, 8); }
+        if (k <= 5) { if (cand) KNN2W(5, true, 8); else KNN2W(5, false, 8); }
+        else { if (cand) KNN2W(8, true, 8); else KNN2W(8, false, 8); }
     } else {
-        if (k <= 5) { if (cand) KNN2(5, true, 4); else KNN2(5, false, 4); }
-        else { if (cand) KNN2(8, true, 4); else KNN2(8, false, 4); }
+        if (k <= 5) { if (cand) KNN2W(5, true, 4); else KNN2W(5, false, 4); }
+        else { if (cand) KNN2W(8, true, 4); else KNN2W(8, false, 4); }
     }
+#undef KNN2W
 #undef KNN2
 }
 
