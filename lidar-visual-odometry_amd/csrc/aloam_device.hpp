@@ -418,7 +418,7 @@ struct KnnCollect { float r2; float4* pts; int* pos; int cap; };
 // group min over 64-bit keys merge the lanes' lists. IDXW: the grid stores each point's original
 // index in w (no second load per candidate). Same total order as the wave / thread versions;
 // every lane returns the same result. COL: also collect the block points within col.r2 (above).
-template <int K, int GS, bool IDXW, int U = 4, bool COL = false>
+template <int K, int GS, bool IDXW, int U = 4, bool COL = false, int XP = 0>
 __device__ __forceinline__ int group_knn27(const float ox, const float oy, const float oz, const float inv_cell,
                                            const int gdx, const int gdy, const int gdz,
                                            const int* __restrict__ start, const float4* __restrict__ spts,
@@ -442,6 +442,7 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
             pre[r + 1] = pre[r] + (load_or(start, c + x1 + 1, ok, 0) - rb[r]);
         }
         total = pre[9];
+        if constexpr ((XP & 2) != 0) total = pre[9] > 1000000000 ? 1 : 0;   // (experiment: no candidate loop)
         __builtin_amdgcn_wave_barrier();
         if (gl == 0) {
 #pragma unroll
@@ -503,6 +504,12 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
         }
     }
     if constexpr (COL) { if (ncol) *ncol = nc; }
+    if constexpr ((XP & 4) != 0) {            // (experiment: no merge — each lane returns its own list)
+        int found = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) { out_pos[k] = bp[k]; out_d2[k] = bd[k]; out_idx[k] = bi[k]; found += bp[k] >= 0; }
+        return found;
+    }
     return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
 }
 // The same k-NN over an explicit candidate list (a query's collected block points, w = original

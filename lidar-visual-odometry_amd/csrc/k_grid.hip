@@ -367,7 +367,7 @@ __device__ __forceinline__ int block27_total(const GridDesc& gd, const int* __re
 // dense map (C4: the 5 neighbours within ~0.15 m, ~1000 points in the coarse block) phase 1 streams
 // ~10x fewer candidates. cand (profiling): [0] += C27(q) of the coarse block (SURVEY §8(d)'s
 // algorithmic count), [1] += candidates actually streamed by both phases.
-template <int K, int GS, bool CNT, int U = 4, bool WP2 = true>
+template <int K, int GS, bool CNT, int U = 4, bool WP2 = true, int XP = 0>
 __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
                                                     const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
                                                     const int* __restrict__ cstart, const float4* __restrict__ cpts,
@@ -381,13 +381,13 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
     int pos[K], oi[K], nf = 0, nc = 0;
     float od[K];
     const GridDesc gf = *fgd;
-    int f = group_knn27<K, GS, true, U>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, nullptr,
-                                     qq.x, qq.y, qq.z, r2, live, pos, od, oi, &nf, tabs[threadIdx.x / GS], gf.n);
+    int f = group_knn27<K, GS, true, U, false, XP>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, nullptr,
+                                                qq.x, qq.y, qq.z, r2, live, pos, od, oi, &nf, tabs[threadIdx.x / GS], gf.n);
     float dk = INFINITY;
 #pragma unroll
     for (int j = 0; j < K; j++) if (j == k - 1) dk = od[j];
     const float lim = 0.99f * gf.cell;
-    const bool need = live && !(f >= k && dk < lim * lim) && !(exp & 1);
+    const bool need = live && !(f >= k && dk < lim * lim) && !(exp & 1) && XP == 0;
     const GridDesc gc = *cgd;
     const int gl = lane_id() & (GS - 1);
     if constexpr (WP2) {
@@ -658,7 +658,13 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
                   wp2 ? "" : ",P2G");
 #define KNN2(KK, CN, UU, WP) k_knn_2phase<KK, GS, CN, UU, WP><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp)
 #define KNN2W(KK, CN, UU) do { if (wp2) KNN2(KK, CN, UU, true); else KNN2(KK, CN, UU, false); } while (0)
-    if (u8) {
+    const int xp = exp & 6;
+    if (xp && k <= 5 && !cand && !u8) {          // (profiling experiments: parts of phase 1 left out)
+        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<5,%d,XP%d>", GS, xp);
+        if (xp == 2) k_knn_2phase<5, GS, false, 4, false, 2><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp);
+        else if (xp == 4) k_knn_2phase<5, GS, false, 4, false, 4><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp);
+        else k_knn_2phase<5, GS, false, 4, false, 6><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp);
+    } else if (u8) {
         if (k <= 5) { if (cand) KNN2W(5, true, 8); else KNN2W(5, false, 8); }
         else { if (cand) KNN2W(8, true, 8); else KNN2W(8, false, 8); }
     } else {
@@ -673,7 +679,7 @@ void knn_device_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
                               unsigned long long* cand) {
     if (nq <= 0) return;
     const float r2 = radius * radius;
-    static const int gs = getenv("ALOAM_KNN_GS2") ? atoi(getenv("ALOAM_KNN_GS2")) : 8;   // tuning knob
+    const int gs = getenv("ALOAM_KNN_GS2") ? atoi(getenv("ALOAM_KNN_GS2")) : 8;   // tuning knob (read per call)
     if (gs == 16) knn_2phase_launch<16>(C, gf, gc, q, nq, k, r2, idx, d2, cand);
     else if (gs == 2) knn_2phase_launch<2>(C, gf, gc, q, nq, k, r2, idx, d2, cand);
     else if (gs == 4) knn_2phase_launch<4>(C, gf, gc, q, nq, k, r2, idx, d2, cand);

@@ -34,6 +34,8 @@ for v in variants:
     env = dict(kv.split("=", 1) for kv in v.split(",") if kv)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
+    if "ALOAM_KNN_FINE" in env or "ALOAM_KNN_FINE" in old and old["ALOAM_KNN_FINE"] is not None or v == "REBUILD":
+        ctx.knn_build(dm.data_ptr(), len(m), 1.0)    # the fine cell is a build parameter
     idx = torch.full((len(q), 5), -7, dtype=torch.int32, device="cuda")
     d2 = torch.full((len(q), 5), -7.0, dtype=torch.float32, device="cuda")
     us, by = [], []
@@ -55,4 +57,6 @@ for v in variants:
             os.environ.pop(k_, None)
         else:
             os.environ[k_] = v_
+    if "ALOAM_KNN_FINE" in env:
+        ctx.knn_build(dm.data_ptr(), len(m), 1.0)
 ctx.close()
