@@ -60,6 +60,13 @@ EOF
                 || fail "pmc $C" gpurun_out/${TAG}_pmc$i.log
         done
         echo "pmc done" ;;
+    pmc:*)
+        # pmc:<label>:<counters...> — one PMC pass over the C4 search (bench.py --c4-only)
+        L="${S#pmc:}"; N="${L%%:*}"; C="${L#*:}"
+        ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C -d $R/gpurun_out/${TAG}_pmc_$N \
+            -o run --output-format csv -- python3 $R/bench.py --c4-only --c4-launches 5 ) > gpurun_out/${TAG}_pmc_$N.log 2>&1 \
+            || fail "pmc $C" gpurun_out/${TAG}_pmc_$N.log
+        python micro/pmc_sum.py gpurun_out/${TAG}_pmc_$N ;;
     prof*)
         A="${S#prof}"; A="${A#:}"; [ -z "$A" ] && A="--steps 20 --warmup 5 --no-traffic --c4-reg-steps 0"
         ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof \
