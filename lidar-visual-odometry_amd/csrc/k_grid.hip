@@ -445,6 +445,174 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
     }
 }
 
+// Phase 1 shared by the queries of a wave (the default since round 6). A wave holds 8 consecutive queries
+// (8 lanes each); in ring order most of them lie in the same fine cell (C4: 2.8 distinct cells per wave, 8.5
+// queries per occupied cell), so their 3x3x3 blocks are the same few blocks. The wave finds its distinct
+// cells (ballot loop over the group leaders), loads the 9 row bounds of every distinct block in one
+// instruction per 64 values, lays the blocks' rows out as one flattened list (row table in LDS: cumulative
+// ends + position bases), and streams the list once, 64 consecutive candidates per load instruction, into
+// a per-wave LDS buffer; each query's 8 lanes then scan exactly its own block's stretch of the list from
+// LDS. Same candidates per query, same (d2, index) order and settle test as k_knn_2phase, so the result
+// is identical; a block's points cross L1 once per wave instead of once per query.
+template <int K, bool CNT, int U>
+__global__ void __launch_bounds__(256) k_knn_shared(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
+                                                    const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
+                                                    const int* __restrict__ cstart, const float4* __restrict__ cpts,
+                                                    const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
+                                                    float* __restrict__ d2, unsigned long long* cand) {
+    constexpr int GS = 8, NW = 256 / WAVE, CH = WAVE * U, MAXC = WAVE / GS, MAXR = 9 * MAXC;
+    __shared__ float4 cbuf[NW][CH];
+    __shared__ int rE[NW][MAXR], rB[NW][MAXR], rtmp[NW][18 * MAXC];
+    __shared__ int4 slotc[NW][MAXC];
+    __shared__ int tabs[256 / GS][20];
+    const int w = threadIdx.x / WAVE, lane = lane_id(), gl = lane & (GS - 1);
+    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+    const bool live = qi < nq;
+    if (!__ballot(live)) return;
+    const float4 qq = q[live ? qi : 0];
+    const GridDesc gf = *fgd;
+    const int cx = (int)floorf((qq.x - gf.ox) * gf.inv_cell), cy = (int)floorf((qq.y - gf.oy) * gf.inv_cell),
+              cz = (int)floorf((qq.z - gf.oz) * gf.inv_cell);
+    // the block [c-1, c+1]^3 meets the grid (its other rows / cells are clipped below, as in group_knn27)
+    const bool blk = live && cx >= -1 && cx <= gf.dx && cy >= -1 && cy <= gf.dy && cz >= -1 && cz <= gf.dz;
+    const int key = blk ? ((cz + 1) * (gf.dy + 2) + (cy + 1)) * (gf.dx + 2) + (cx + 1) : -1;
+    // distinct cells of the wave, in leader order
+    unsigned long long rem = __ballot(gl == 0 && key >= 0);
+    int myslot = -1, ncell = 0;
+    while (rem) {
+        const int l = __ffsll((long long)rem) - 1;
+        const int kk = readlane_i(key, l);
+        rem &= ~__ballot(gl == 0 && key == kk);
+        if (key == kk) myslot = ncell;
+        if (lane == l) slotc[w][ncell] = make_int4(cx, cy, cz, 0);
+        ncell++;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // row bounds of every distinct block: value i = (cell i / 18, row (i % 18) % 9, end if (i % 18) >= 9)
+    for (int b0 = 0; b0 < 18 * ncell; b0 += WAVE) {
+        const int i = b0 + lane;
+        int v = 0;
+        if (i < 18 * ncell) {
+            const int4 c = slotc[w][i / 18];
+            const int rr = i % 18, r = rr % 9;
+            const int x0 = max(c.x - 1, 0), x1 = min(c.x + 1, gf.dx - 1);
+            const int y = c.y + (r % 3) - 1, z = c.z + (r / 3) - 1;
+            const bool ok = x0 <= x1 && y >= 0 && y < gf.dy && z >= 0 && z < gf.dz;
+            v = load_or(fstart, (z * gf.dy + y) * gf.dx + (rr >= 9 ? x1 + 1 : x0), ok, 0);
+            rtmp[w][i] = v;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // flattened row table: row R = 9 j + r, E[R] = cumulative end, B[R] = position of flattened item 0 of its run
+    const int nr = 9 * ncell;
+    int T;
+    {
+        int rb0 = 0, len0 = 0, rb1 = 0, len1 = 0;
+        if (lane < nr) { const int j = lane / 9, r = lane % 9; rb0 = rtmp[w][18 * j + r]; len0 = rtmp[w][18 * j + 9 + r] - rb0; }
+        if (WAVE + lane < nr) {
+            const int R = WAVE + lane, j = R / 9, r = R % 9;
+            rb1 = rtmp[w][18 * j + r];
+            len1 = rtmp[w][18 * j + 9 + r] - rb1;
+        }
+        const int e0 = wave_incl_scan(len0);
+        const int t0 = readlane_i(e0, WAVE - 1);
+        const int e1 = wave_incl_scan(len1) + t0;
+        if (lane < nr) { rE[w][lane] = e0; rB[w][lane] = rb0 - (e0 - len0); }
+        if (WAVE + lane < nr) { rE[w][WAVE + lane] = e1; rB[w][WAVE + lane] = rb1 - (e1 - len1); }
+        T = nr <= WAVE ? readlane_i(e0, nr > 0 ? nr - 1 : 0) : readlane_i(e1, nr - WAVE - 1);
+        if (nr == 0) T = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int off = myslot > 0 ? rE[w][9 * myslot - 1] : 0, end = myslot >= 0 ? rE[w][9 * myslot + 8] : 0;
+    float bd[K];
+    int bi[K], bp[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) { bd[j] = INFINITY; bi[j] = 0x7fffffff; bp[j] = -1; }
+    for (int c0 = 0; c0 < T; c0 += CH) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = c0 + u * WAVE + lane;
+            // row of item t: the number of rows whose cumulative end is <= t (branch-free search, 7 steps)
+            int R = 0;
+#pragma unroll
+            for (int st = 64; st >= 1; st >>= 1)
+                if (R + st <= nr && rE[w][R + st - 1] <= t) R += st;
+            const int p = t < T && R < nr ? rB[w][R] + t : -1;
+            v[u] = load_or(fpts, p, p >= 0 && p < gf.n, make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) cbuf[w][u * WAVE + lane] = v[u];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int lo = max(off, c0), hi = min(end, c0 + CH);
+        for (int t = lo + gl; t < hi; t += GS) {
+            const float4 c = cbuf[w][t - c0];
+            const float dd = sqdist(c.x, c.y, c.z, qq.x, qq.y, qq.z);
+            if (!(dd < r2) || dd > bd[K - 1]) continue;
+            const int iu = __float_as_int(c.w);
+            if (dd < bd[K - 1] || iu < bi[K - 1]) {
+                float nd = dd; int ni = iu, np = t;
+#pragma unroll
+                for (int j = 0; j < K; j++) {
+                    const bool lt = nd < bd[j] || (nd == bd[j] && ni < bi[j]);
+                    if (lt) { float td = bd[j]; int ti = bi[j], tp = bp[j]; bd[j] = nd; bi[j] = ni; bp[j] = np; nd = td; ni = ti; np = tp; }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    int pos[K], oi[K];
+    float od[K];
+    int f = group_merge_topk<K, GS>(bd, bi, bp, pos, od, oi);
+    const int nf = end - off;
+    float dk = INFINITY;
+#pragma unroll
+    for (int j = 0; j < K; j++) if (j == k - 1) dk = od[j];
+    const float lim = 0.99f * gf.cell;
+    const bool need = live && !(f >= k && dk < lim * lim);
+    const GridDesc gc = *cgd;
+    int nc = 0;
+    if (__any(need)) {                         // phase 2 by each unsettled query's own group, bounded by phase 1
+        int p2[K], i2[K];
+        float e2[K];
+        const float pr = f >= k ? dk : INFINITY;
+        const int f2 = group_knn27<K, GS, true, 4>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, nullptr,
+                                                   qq.x, qq.y, qq.z, r2, need, p2, e2, i2, &nc, tabs[threadIdx.x / GS], gc.n,
+                                                   KnnCollect{0.f, nullptr, nullptr, 0}, nullptr, pr);
+        if (need) {
+#pragma unroll
+            for (int j = 0; j < K; j++) { od[j] = e2[j]; oi[j] = i2[j]; }
+            f = f2;
+        }
+    }
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if (j < k && j % GS == gl) {
+                idx[(size_t)qi * k + j] = j < f ? oi[j] : -1;
+                d2[(size_t)qi * k + j] = j < f ? od[j] : INFINITY;
+            }
+    }
+    if (CNT) {
+        const int c27 = live && gl == 0 ? (need ? nc : block27_total(gc, cstart, qq.x, qq.y, qq.z)) : 0;
+        const int a = wave_sum_i(c27), s = wave_sum_i(live && gl == 0 ? nf + (need ? nc : 0) : 0);
+        if (lane_id() == 0) {
+            if (a) atomicAdd(&cand[0], (unsigned long long)a);
+            if (s) atomicAdd(&cand[1], (unsigned long long)s);
+        }
+    }
+}
+
 // The same two-phase search with phase 1 read from LDS: a workgroup takes a tile of 256 / GS consecutive
 // queries (ring order: neighbours along a scan line, a metre or two of arc), loads the fine-grid cells of
 // the union of their 3x3x3 blocks into LDS once — row by row, each (y, z) row of the box one contiguous
@@ -646,18 +814,38 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
     }
     // CNT: the candidate-counting instance (profiling), a separate symbol so kernel traces tell it apart.
     // ALOAM_KNN_U (tuning knob, read per call): candidate loads in flight per lane, 4 (default) or 8.
-    // ALOAM_KNN_P2 (A/B knob, read per call): 0 = phase 2 by each query's own GS-lane group (round 5),
-    // default 1 = by the whole wave. ALOAM_KNN_EXP (profiling experiments only, results invalid): 1 = no phase 2.
+    // ALOAM_KNN_SHARED (read per call): default 1 = k_knn_shared (phase 1 shared by the wave's queries), 0 = the
+    // per-query k_knn_2phase; ALOAM_KNN_SU: its loads per lane per staging round (4, or 2).
+    // ALOAM_KNN_P2 (A/B knob, read per call, k_knn_2phase): 1 = phase 2 by the whole wave, one unsettled query at a
+    // time (measured slower); default = by each query's own group. ALOAM_KNN_EXP (profiling experiments only,
+    // results invalid): 1 = no phase 2, 2 / 4 = no phase-1 candidate loop / merge.
     const char* ue = getenv("ALOAM_KNN_U");
     const bool u8 = ue && atoi(ue) == 8;
     const char* pe = getenv("ALOAM_KNN_P2");
-    const bool wp2 = !(pe && atoi(pe) == 0);
+    const bool wp2 = pe && atoi(pe) == 1;     // measured slower (114 vs 95 us, r6 c4_exp): opt-in
     const char* xe = getenv("ALOAM_KNN_EXP");
     const int exp = xe ? atoi(xe) : 0;
     std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<%d,%d%s%s>", k <= 5 ? 5 : 8, GS, u8 ? ",U8" : "",
-                  wp2 ? "" : ",P2G");
+                  wp2 ? ",P2W" : "");
 #define KNN2(KK, CN, UU, WP) k_knn_2phase<KK, GS, CN, UU, WP><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp)
 #define KNN2W(KK, CN, UU) do { if (wp2) KNN2(KK, CN, UU, true); else KNN2(KK, CN, UU, false); } while (0)
+    const char* she = getenv("ALOAM_KNN_SHARED");
+    const bool shared = GS == 8 && !(she && atoi(she) == 0) && !u8 && !(exp & 6);
+    if (shared) {
+        const char* sue = getenv("ALOAM_KNN_SU");
+        const int su = sue ? atoi(sue) : 4;
+        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_shared<%d,%d>", k <= 5 ? 5 : 8, su == 2 ? 2 : 4);
+#define KNNS(KK, CN, UU) k_knn_shared<KK, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+        if (su == 2) {
+            if (k <= 5) { if (cand) KNNS(5, true, 2); else KNNS(5, false, 2); }
+            else { if (cand) KNNS(8, true, 2); else KNNS(8, false, 2); }
+        } else {
+            if (k <= 5) { if (cand) KNNS(5, true, 4); else KNNS(5, false, 4); }
+            else { if (cand) KNNS(8, true, 4); else KNNS(8, false, 4); }
+        }
+#undef KNNS
+        return;
+    }
     const int xp = exp & 6;
     if (xp && k <= 5 && !cand && !u8) {          // (profiling experiments: parts of phase 1 left out)
         std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<5,%d,XP%d>", GS, xp);
