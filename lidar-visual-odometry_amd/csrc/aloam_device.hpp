@@ -443,6 +443,47 @@ __device__ __forceinline__ int group_knn27(const float ox, const float oy, const
         }
         total = pre[9];
         if constexpr ((XP & 2) != 0) total = pre[9] > 1000000000 ? 1 : 0;   // (experiment: no candidate loop)
+        if constexpr ((XP & 8) != 0) {
+            // row bounds kept in registers: every candidate slot's position by 8 compare / select pairs on
+            // them, so the U loads of a batch issue back to back (no LDS round trip between them)
+#pragma unroll
+            for (int r = 0; r < 9; r++) rb[r] -= pre[r];
+            if (ncand) *ncand = total;
+            float bd[K];
+            int bi[K], bp[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) { bd[k] = INFINITY; bi[k] = 0x7fffffff; bp[k] = -1; }
+            for (int t0 = gl; t0 < total; t0 += U * GS) {
+                float4 v[U];
+                int ps[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int t = t0 + u * GS;
+                    int o = rb[0];
+#pragma unroll
+                    for (int r = 1; r < 9; r++) o = t >= pre[r] ? rb[r] : o;
+                    int p = t < total ? o + t : -1;
+                    if ((unsigned)p >= (unsigned)npts) p = -1;                 // defensive: inconsistent index
+                    ps[u] = p;
+                    v[u] = load_or(spts, p, p >= 0, make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+                    if (!(d2 < r2) || d2 > fminf(bd[K - 1], prune)) continue;
+                    const int iu = __float_as_int(v[u].w);
+                    if (d2 < bd[K - 1] || iu < bi[K - 1]) {
+                        float nd = d2; int ni = iu, np = ps[u];
+#pragma unroll
+                        for (int k = 0; k < K; k++) {
+                            const bool lt = nd < bd[k] || (nd == bd[k] && ni < bi[k]);
+                            if (lt) { float td = bd[k]; int ti = bi[k], tp = bp[k]; bd[k] = nd; bi[k] = ni; bp[k] = np; nd = td; ni = ti; np = tp; }
+                        }
+                    }
+                }
+            }
+            return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
+        }
         __builtin_amdgcn_wave_barrier();
         if (gl == 0) {
 #pragma unroll

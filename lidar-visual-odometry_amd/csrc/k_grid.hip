@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
 #pragma unroll
     for (int j = 0; j < K; j++) if (j == k - 1) dk = od[j];
     const float lim = 0.99f * gf.cell;
-    const bool need = live && !(f >= k && dk < lim * lim) && !(exp & 1) && XP == 0;
+    const bool need = live && !(f >= k && dk < lim * lim) && !(exp & 1) && (XP & 6) == 0;
     const GridDesc gc = *cgd;
     const int gl = lane_id() & (GS - 1);
     if constexpr (WP2) {
@@ -553,17 +553,27 @@ __global__ void __launch_bounds__(256) k_knn_shared(const GridDesc* __restrict__
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int lo = max(off, c0), hi = min(end, c0 + CH);
-        for (int t = lo + gl; t < hi; t += GS) {
-            const float4 c = cbuf[w][t - c0];
-            const float dd = sqdist(c.x, c.y, c.z, qq.x, qq.y, qq.z);
-            if (!(dd < r2) || dd > bd[K - 1]) continue;
-            const int iu = __float_as_int(c.w);
-            if (dd < bd[K - 1] || iu < bi[K - 1]) {
-                float nd = dd; int ni = iu, np = t;
+        for (int tb = lo + gl; tb < hi; tb += 4 * GS) {
+            float4 cv[4];
 #pragma unroll
-                for (int j = 0; j < K; j++) {
-                    const bool lt = nd < bd[j] || (nd == bd[j] && ni < bi[j]);
-                    if (lt) { float td = bd[j]; int ti = bi[j], tp = bp[j]; bd[j] = nd; bi[j] = ni; bp[j] = np; nd = td; ni = ti; np = tp; }
+            for (int u = 0; u < 4; u++) {              // 4 LDS reads in flight, then the 4 candidates
+                const int t = tb + u * GS;
+                cv[u] = cbuf[w][min(t, hi - 1) - c0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = tb + u * GS;
+                const float4 c = cv[u];
+                const float dd = sqdist(c.x, c.y, c.z, qq.x, qq.y, qq.z);
+                if (t >= hi || !(dd < r2) || dd > bd[K - 1]) continue;
+                const int iu = __float_as_int(c.w);
+                if (dd < bd[K - 1] || iu < bi[K - 1]) {
+                    float nd = dd; int ni = iu, np = t;
+#pragma unroll
+                    for (int j = 0; j < K; j++) {
+                        const bool lt = nd < bd[j] || (nd == bd[j] && ni < bi[j]);
+                        if (lt) { float td = bd[j]; int ti = bi[j], tp = bp[j]; bd[j] = nd; bi[j] = ni; bp[j] = np; nd = td; ni = ti; np = tp; }
+                    }
                 }
             }
         }
@@ -844,6 +854,17 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
             else { if (cand) KNNS(8, true, 4); else KNNS(8, false, 4); }
         }
 #undef KNNS
+        return;
+    }
+    const char* rre = getenv("ALOAM_KNN_RR");
+    const bool rr = rre && atoi(rre) == 1;
+    if (rr && !u8 && !(exp & 6)) {
+        // row bounds in registers (no LDS row table in the candidate loop)
+        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_2phase<%d,%d,RR>", k <= 5 ? 5 : 8, GS);
+        if (k <= 5) { if (cand) k_knn_2phase<5, GS, true, 4, false, 8><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp);
+                      else k_knn_2phase<5, GS, false, 4, false, 8><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp); }
+        else { if (cand) k_knn_2phase<8, GS, true, 4, false, 8><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp);
+               else k_knn_2phase<8, GS, false, 4, false, 8><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp); }
         return;
     }
     const int xp = exp & 6;
