@@ -1451,7 +1451,7 @@ static void knn_build(Ctx& C, const float* d_pts, int n, float radius) {
     if (!C.d_knn_n) C.d_knn_n = (int*)dalloc(C, sizeof(int) * 2);
     if (C.g_knn.cap < std::max(n, 1)) {          // grow (old buffers are released with the context)
         Grid g{};
-        grid_alloc(C, g, std::max(std::max(n, 1), C.g_knn.cap * 2), radius * 1.025f, 1, true);
+        grid_alloc(C, g, std::max(std::max(n, 1), C.g_knn.cap * 2), radius * 1.025f, 1, true, false, GRID_MAX_CELLS_BIG);
         C.g_knn = g;
     }
     C.g_knn.min_cell = radius * 1.025f;           // cells >= radius: the 27-cell block holds the ball
@@ -1462,7 +1462,7 @@ static void knn_build(Ctx& C, const float* d_pts, int n, float radius) {
         const int cap = std::max(std::max(n, 1), C.g_knn_fine.cap * 2);
         if (C.g_knn_fine.cap) grid_free(C, C.g_knn_fine);
         Grid g{};
-        grid_alloc(C, g, cap, radius * fine_frac, 1, true);
+        grid_alloc(C, g, cap, radius * fine_frac, 1, true, false, GRID_MAX_CELLS_BIG);
         C.g_knn_fine = g;
     }
     set_counts2(C, C.d_knn_n, n, 0);

@@ -21,7 +21,8 @@ constexpr int LINE_FLAT_CAP = 24;    // 4 per segment x 6   (:359)
 constexpr int ODOM_CNT_SLOTS = 64, ODOM_CNT_STRIDE = 16;   // odometry search counters: 64 lines of 64 B per round
 constexpr int LINE_LDS_CAP = 4096;   // points per line kept in LDS (larger lines use global scratch)
 constexpr int CUBE_W = 21, CUBE_H = 21, CUBE_D = 11, CUBE_N = 21 * 21 * 11;  // laserMapping.cpp:74-82
-constexpr int GRID_MAX_CELLS = 1 << 23;
+constexpr int GRID_MAX_CELLS = 1 << 23;        // default cell cap of a grid (the cell grows x1.25 until it fits)
+constexpr int GRID_MAX_CELLS_BIG = 1 << 24;    // cap of the large-map search grids (C4 index, s2m): a 0.3 m cell over ~120 x 100 x 25 m
 
 // ---- device-resident bookkeeping of scanRegistration ----
 struct ScanMeta {
@@ -52,6 +53,7 @@ struct Grid {
     bool flat = false;             // one z cell (2-D cells per layer: a scan line is a thin cone)
     int cap = 0;
     float min_cell = 1.f;
+    int max_cells = GRID_MAX_CELLS;
 };
 
 // ---- Ceres-equivalent LM state (device) ----
@@ -350,7 +352,8 @@ void knn_device_launch(Ctx& C, Grid& g, const float4* q, int nq, int k, float ra
                        unsigned long long* cand);
 void knn_device_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int nq, int k, float radius, int* idx, float* d2,
                               unsigned long long* cand);
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false);
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers = 1, bool w_index = false, bool flat = false,
+                int max_cells = GRID_MAX_CELLS);
 void odom_round_search(Ctx& C, int round);
 unsigned long long serial_sort_calls_map();
 unsigned long long serial_sort_calls_scan();

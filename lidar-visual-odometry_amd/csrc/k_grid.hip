@@ -16,7 +16,7 @@ namespace aloam {
 
 constexpr int GB = 256;
 
-__device__ inline void grid_params(const unsigned bb[6], float min_cell, int nlayers, int flat, GridDesc* d) {
+__device__ inline void grid_params(const unsigned bb[6], float min_cell, int nlayers, int flat, int max_cells, GridDesc* d) {
     float mn[3], mx[3];
     for (int a = 0; a < 3; a++) { mn[a] = ord2f(bb[a]); mx[a] = ord2f(bb[3 + a]); }
     float cell = min_cell;
@@ -29,7 +29,7 @@ __device__ inline void grid_params(const unsigned bb[6], float min_cell, int nla
             dims[a] = (a == 2 && flat) ? 1 : (int)(ext / cell) + 2;
             prod *= dims[a];
         }
-        if (prod <= GRID_MAX_CELLS) break;
+        if (prod <= max_cells) break;
         cell *= 1.25f;
     }
     d->ox = mn[0]; d->oy = mn[1]; d->oz = mn[2];
@@ -73,7 +73,7 @@ __device__ inline bool grid_include(int i, const int* cube_of, const unsigned ch
 // sum of the preceding chunk sums + a local scan. 1024 threads x 16 consecutive cells per chunk (int4
 // loads), so an 8M-cell grid is 512 chunks and the chunk-sum prefix is one value per thread.
 constexpr int SCAN_T = 1024, SCAN_PER = 16, SCAN_CHUNK = SCAN_T * SCAN_PER;
-static_assert(GRID_MAX_CELLS / SCAN_CHUNK <= SCAN_T, "chunk sums: one per thread");
+static_assert(GRID_MAX_CELLS_BIG / SCAN_CHUNK <= SCAN_T, "chunk sums: one per thread");
 __device__ __forceinline__ void load16(const int* __restrict__ cnt, int i0, int nc, int v[SCAN_PER]) {
     if (i0 + SCAN_PER <= nc) {
         const int4* q = (const int4*)(cnt + i0);
@@ -128,15 +128,17 @@ __device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, c
     if (base + SCAN_CHUNK >= nc && threadIdx.x == 0) start[nc] = ptot + tot;
 }
 
-void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_index, bool flat) {
+void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_index, bool flat, int max_cells) {
+    if (max_cells > GRID_MAX_CELLS_BIG) throw ApiError{ALOAM_E_ARG, "grid_alloc: cell cap above GRID_MAX_CELLS_BIG"};
     g.cap = cap;
+    g.max_cells = max_cells;
     g.flat = flat;
     g.min_cell = min_cell;
     g.nlayers = nlayers;
     g.w_index = w_index;
     g.desc = (GridDesc*)dalloc(C, sizeof(GridDesc));
-    g.cell_count = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
-    g.cell_start = (int*)dalloc(C, sizeof(int) * (GRID_MAX_CELLS + 1));
+    g.cell_count = (int*)dalloc(C, sizeof(int) * ((size_t)max_cells + 1));
+    g.cell_start = (int*)dalloc(C, sizeof(int) * ((size_t)max_cells + 1));
     g.blk = (int*)dalloc(C, sizeof(int) * 2048);
     g.pts = (float4*)dalloc(C, sizeof(float4) * cap);
     g.idx = (int*)dalloc(C, sizeof(int) * cap);
@@ -163,7 +165,7 @@ void grid_build(Ctx& C, Grid& g, const float4* pts, const int* d_n, int cap_n, c
 struct GridJob {
     GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx; int* pcell;
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
-    float min_cell; int nlayers; int w_index; int flat;
+    float min_cell; int nlayers; int w_index; int flat; int max_cells;
 };
 struct GridJobs { GridJob j[GRID_MULTI_MAX]; };
 
@@ -201,7 +203,7 @@ __global__ void k_gm_count(GridJobs J) {
     if (threadIdx.x == 0) {
         unsigned bb[6];
         for (int a = 0; a < 6; a++) bb[a] = g.desc->bb[a];
-        grid_params(bb, g.min_cell, g.nlayers, g.flat, &gd);
+        grid_params(bb, g.min_cell, g.nlayers, g.flat, g.max_cells, &gd);
         if (blockIdx.x == 0) {
             GridDesc* d = g.desc;
             d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
@@ -270,16 +272,17 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     if (nj > GRID_MULTI_MAX) throw ApiError{ALOAM_E_ARG, "grid_build_multi: too many grids"};
     hipStream_t st = C.stream;
     GridJobs J{};
-    int cap = 1;
+    int cap = 1, maxc = 0;
     for (int k = 0; k < nj; k++) {
         const Grid& g = *b[k].g;
         J.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell,
                          b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0,
-                         g.flat ? 1 : 0};
+                         g.flat ? 1 : 0, g.max_cells};
         cap = std::max(cap, b[k].cap_n);
+        maxc = std::max(maxc, g.max_cells);
     }
     const int nb = std::max(1, std::min(1024, (cap + GB - 1) / GB));
-    const int nsb = GRID_MAX_CELLS / SCAN_CHUNK;
+    const int nsb = maxc / SCAN_CHUNK;
     k_gm_bbox<<<dim3(nb, nj), GB, 0, st>>>(J);
     k_gm_count<<<dim3(nb, nj), GB, 0, st>>>(J);
     k_gm_scan1<<<dim3(nsb, nj), SCAN_T, 0, st>>>(J);

@@ -159,7 +159,7 @@ void s2m_set_map(Ctx& C, const float* corner, int nc, const float* surf, int ns,
     const float fine_cell = fe ? (float)atof(fe) : 0.3f;
     S.fine = fine_cell > 0.f;
     auto need = [&](Grid& g, int n, float cell) {
-        if (g.cap < std::max(n, 1)) { Grid ng{}; grid_alloc(C, ng, std::max(std::max(n, 1), 2 * g.cap), cell, 1, true); g = ng; }
+        if (g.cap < std::max(n, 1)) { Grid ng{}; grid_alloc(C, ng, std::max(std::max(n, 1), 2 * g.cap), cell, 1, true, false, GRID_MAX_CELLS_BIG); g = ng; }
         g.min_cell = cell;
     };
     need(S.gc, nc, 1.0f * 1.025f);
