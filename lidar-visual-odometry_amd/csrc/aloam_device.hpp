@@ -591,6 +591,79 @@ __device__ __forceinline__ int group_knn_list(const float4* __restrict__ lpts, c
     }
     return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
 }
+// Large-search variant of group_knn27 (aloam_knn_device, round 6): a candidate is one 64-bit key, (d2 bits
+// << 32) | original index (w of the sorted copy); d2 >= 0, so unsigned key order is exactly the (d2, index)
+// order of group_knn27. A lane's top K is a sorted key array updated without branches (one 64-bit compare
+// and two selects per slot), entered only when some lane of the wave holds a key below its K-th; the nine
+// row bounds stay in registers (a slot's position by compare / select on them, no LDS table); invalid slots
+// and points outside the radius are ~0 keys. `bound`: a key known to be >= the group's final K-th (keys
+// above it are dropped). Returns the group's K smallest keys (~0 = none), the same on every group lane.
+template <int K, int GS, int U>
+__device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, const float oz, const float inv_cell,
+                                                const int gdx, const int gdy, const int gdz, const int* __restrict__ start,
+                                                const float4* __restrict__ spts, float qx, float qy, float qz, float r2,
+                                                bool active, unsigned long long* out_key, int* ncand, int npts,
+                                                unsigned long long bound = ~0ull) {
+    const int gl = lane_id() & (GS - 1);
+    const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gdx - 1);
+    int off[9], pre[10];
+    pre[0] = 0;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
+        const bool ok = active && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
+        const int c = (z * gdy + y) * gdx;
+        const int b = load_or(start, c + x0, ok, 0);
+        pre[r + 1] = pre[r] + (load_or(start, c + x1 + 1, ok, 0) - b);
+        off[r] = b - pre[r];
+    }
+    const int total = pre[9];
+    if (ncand) *ncand = total;
+    unsigned long long bk[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) bk[k] = ~0ull;
+    for (int t0 = gl; t0 < total; t0 += U * GS) {
+        float4 v[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + u * GS;
+            int o = off[0];
+#pragma unroll
+            for (int r = 1; r < 9; r++) o = t >= pre[r] ? off[r] : o;
+            const int p = o + t;
+            ok[u] = t < total && (unsigned)p < (unsigned)npts;
+            v[u] = spts[ok[u] ? p : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+            unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)__float_as_int(v[u].w);
+            if (!(ok[u] && d2 < r2) || key > bound) key = ~0ull;
+            if (__any(key < bk[K - 1])) {           // wave-uniform: the branch-free insertion below
+#pragma unroll
+                for (int k = K - 1; k > 0; k--) bk[k] = key < bk[k - 1] ? bk[k - 1] : (key < bk[k] ? key : bk[k]);
+                bk[0] = key < bk[0] ? key : bk[0];
+            }
+        }
+    }
+    // merge: K rounds of a group min over the lanes' list heads; the owner of the minimum (unique: one
+    // lane per candidate) advances its head
+    int head = 0, found = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        unsigned long long hk = ~0ull;
+#pragma unroll
+        for (int j = 0; j < K; j++) if (j == head) hk = bk[j];
+        constexpr int NS = GS >= 64 ? 6 : GS >= 32 ? 5 : GS >= 16 ? 4 : GS >= 8 ? 3 : GS >= 4 ? 2 : GS >= 2 ? 1 : 0;
+        const unsigned long long mn = allreduce_u64<NS>(hk, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
+        if (hk == mn && mn != ~0ull) head++;
+        out_key[k] = mn;
+        found += mn != ~0ull;
+    }
+    return found;
+}
 // v / k for a point count k in [1, 2^24), correctly rounded like the IEEE division PCL's centroid
 // (Eigen "/= num_pts") does. For |x| in [2^-89, 2^90) or x == 0, v_div_scale / v_div_fmas /
 // v_div_fixup in the compiler's fp32 division sequence are identities, leaving rcp, one Newton step on

@@ -448,6 +448,61 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
     }
 }
 
+// k_knn_2phase on 64-bit keys (group_knn27_keys): the same two phases, settle test and results; the
+// candidate loop has no data-dependent branches (register row bounds, branch-free top-K insertion), and
+// phase 2 starts from the phase-1 K-th key as its bound. Default since round 6 (ALOAM_KNN_KEYS=0: the
+// round-5 kernel).
+template <int K, int GS, bool CNT, int U>
+__global__ void __launch_bounds__(256) k_knn_keys(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
+                                                  const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
+                                                  const int* __restrict__ cstart, const float4* __restrict__ cpts,
+                                                  const float4* __restrict__ q, int nq, int k, float r2, int* __restrict__ idx,
+                                                  float* __restrict__ d2, unsigned long long* cand) {
+    const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / GS;
+    const bool live = qi < nq;
+    if (!__ballot(live)) return;
+    const float4 qq = q[live ? qi : 0];
+    unsigned long long key[K];
+    int nf = 0, nc = 0;
+    const GridDesc gf = *fgd;
+    int f = group_knn27_keys<K, GS, U>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, qq.x, qq.y, qq.z,
+                                       r2, live, key, &nf, gf.n);
+    unsigned long long kk = ~0ull;
+#pragma unroll
+    for (int j = 0; j < K; j++) if (j == k - 1) kk = key[j];
+    const float dk = kk == ~0ull ? INFINITY : __uint_as_float((unsigned)(kk >> 32));
+    const float lim = 0.99f * gf.cell;
+    const bool need = live && !(f >= k && dk < lim * lim);
+    const GridDesc gc = *cgd;
+    if (__any(need)) {                         // wave-uniform: every lane takes part in the group search
+        unsigned long long k2[K];
+        const int f2 = group_knn27_keys<K, GS, U>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, qq.x, qq.y,
+                                                  qq.z, r2, need, k2, &nc, gc.n, kk);
+        if (need) {
+#pragma unroll
+            for (int j = 0; j < K; j++) key[j] = k2[j];
+            f = f2;
+        }
+    }
+    const int gl = lane_id() & (GS - 1);
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if (j < k && j % GS == gl) {
+                idx[(size_t)qi * k + j] = j < f ? (int)(unsigned)key[j] : -1;
+                d2[(size_t)qi * k + j] = j < f ? __uint_as_float((unsigned)(key[j] >> 32)) : INFINITY;
+            }
+    }
+    if (CNT) {
+        const int c27 = live && gl == 0 ? (need ? nc : block27_total(gc, cstart, qq.x, qq.y, qq.z)) : 0;
+        const int a = wave_sum_i(c27), s = wave_sum_i(live && gl == 0 ? nf + (need ? nc : 0) : 0);
+        if (lane_id() == 0) {
+            if (a) atomicAdd(&cand[0], (unsigned long long)a);
+            if (s) atomicAdd(&cand[1], (unsigned long long)s);
+        }
+    }
+}
+
 // Phase 1 shared by the queries of a wave (the default since round 6). A wave holds 8 consecutive queries
 // (8 lanes each); in ring order most of them lie in the same fine cell (C4: 2.8 distinct cells per wave, 8.5
 // queries per occupied cell), so their 3x3x3 blocks are the same few blocks. The wave finds its distinct
@@ -842,8 +897,24 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
                   wp2 ? ",P2W" : "");
 #define KNN2(KK, CN, UU, WP) k_knn_2phase<KK, GS, CN, UU, WP><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp)
 #define KNN2W(KK, CN, UU) do { if (wp2) KNN2(KK, CN, UU, true); else KNN2(KK, CN, UU, false); } while (0)
+    const char* ke = getenv("ALOAM_KNN_KEYS");
+    const bool keys = !(ke && atoi(ke) == 0) && !(exp & 6);
+    if (keys) {
+        const int uk = u8 ? 8 : 4;
+        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d%s>", k <= 5 ? 5 : 8, GS, u8 ? ",U8" : "");
+#define KNNK(KK, CN, UU) k_knn_keys<KK, GS, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
+        if (uk == 8) {
+            if (k <= 5) { if (cand) KNNK(5, true, 8); else KNNK(5, false, 8); }
+            else { if (cand) KNNK(8, true, 8); else KNNK(8, false, 8); }
+        } else {
+            if (k <= 5) { if (cand) KNNK(5, true, 4); else KNNK(5, false, 4); }
+            else { if (cand) KNNK(8, true, 4); else KNNK(8, false, 4); }
+        }
+#undef KNNK
+        return;
+    }
     const char* she = getenv("ALOAM_KNN_SHARED");
-    const bool shared = GS == 8 && !(she && atoi(she) == 0) && !u8 && !(exp & 6);
+    const bool shared = GS == 8 && she && atoi(she) == 1 && !u8 && !(exp & 6);
     if (shared) {
         const char* sue = getenv("ALOAM_KNN_SU");
         const int su = sue ? atoi(sue) : 4;

@@ -414,8 +414,8 @@ def test_knn_device_two_phase_bit_identical(gpu_ctx_factory, monkeypatch, step, 
 @pytest.mark.parametrize("step,frac", [(0.107, "0.3"), (0.107, "0.1"), (0.107, "0.45")])
 def test_knn_device_kernels_bit_identical(gpu_ctx_factory, monkeypatch, step, frac):
     """Every phase-1 variant of aloam_knn_device returns the single-phase result bit for bit, and the library
-    names the kernel it launched (aloam_knn_kernel): k_knn_shared (default; 4 or 2 loads per lane per staging
-    round), k_knn_2phase (ALOAM_KNN_SHARED=0), k_knn_tile (ALOAM_KNN_TILE=1,
+    names the kernel it launched (aloam_knn_kernel): k_knn_keys (default, 64-bit keys; 4 or 8 loads in flight),
+    k_knn_2phase (ALOAM_KNN_KEYS=0), k_knn_shared (+ ALOAM_KNN_SHARED=1), k_knn_tile (+ ALOAM_KNN_TILE=1,
     per call) and k_knn_tile with every tile over its LDS budget (ALOAM_KNN_TILE=2: phase 1 from global
     memory inside the tile kernel). frac 0.1 puts the far tiles' boxes over 768 fine cells and frac 0.45 over
     2048 points (~5 m of arc at 50 m for 32 ring-ordered queries), so the natural overflow path runs too."""
@@ -428,23 +428,31 @@ def test_knn_device_kernels_bit_identical(gpu_ctx_factory, monkeypatch, step, fr
     dm, dq = torch.from_numpy(m).cuda(), torch.from_numpy(q).cuda()
     ctx = gpu_ctx_factory(128)
     out, names = {}, {}
-    for fine, tile, shared in (("0", "0", "1"), (frac, "0", "1"), (frac, "0", "0"), (frac, "1", "0"), (frac, "2", "0"),
-                               (frac, "0", "2")):
+    variants = {                                   # env -> the kernel aloam_knn_kernel must name
+        ("0", ""): "k_knn_group<5,8>",
+        (frac, ""): "k_knn_keys<5,8>",
+        (frac, "ALOAM_KNN_U=8"): "k_knn_keys<5,8,U8>",
+        (frac, "ALOAM_KNN_KEYS=0"): "k_knn_2phase<5,8>",
+        (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_SHARED=1"): "k_knn_shared<5,4>",
+        (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_SHARED=1,ALOAM_KNN_SU=2"): "k_knn_shared<5,2>",
+        (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_TILE=1"): "k_knn_tile<5,8>",
+        (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_TILE=2"): "k_knn_tile<5,8>",
+    }
+    knobs = ("ALOAM_KNN_U", "ALOAM_KNN_KEYS", "ALOAM_KNN_SHARED", "ALOAM_KNN_SU", "ALOAM_KNN_TILE")
+    for (fine, env), name in variants.items():
+        for kn in knobs:
+            monkeypatch.delenv(kn, raising=False)
+        for kv in filter(None, env.split(",")):
+            a, b = kv.split("=")
+            monkeypatch.setenv(a, b)
         monkeypatch.setenv("ALOAM_KNN_FINE", fine)
-        monkeypatch.setenv("ALOAM_KNN_TILE", tile)
-        monkeypatch.setenv("ALOAM_KNN_SHARED", "0" if shared == "0" else "1")
-        monkeypatch.setenv("ALOAM_KNN_SU", "2" if shared == "2" else "4")
         idx = torch.full((len(q), 5), -7, dtype=torch.int32, device="cuda")
         d2 = torch.full((len(q), 5), -7.0, dtype=torch.float32, device="cuda")
         ctx.knn_device(dm.data_ptr(), len(m), dq.data_ptr(), len(q), 5, 1.0, idx.data_ptr(), d2.data_ptr())
-        out[(fine, tile, shared)] = (idx.cpu().numpy(), d2.cpu().numpy())
-        names[(fine, tile, shared)] = ctx.knn_kernel()
-    assert names[("0", "0", "1")] == "k_knn_group<5,8>"
-    assert names[(frac, "0", "1")] == "k_knn_shared<5,4>"
-    assert names[(frac, "0", "2")] == "k_knn_shared<5,2>"
-    assert names[(frac, "0", "0")] == "k_knn_2phase<5,8>"
-    assert names[(frac, "1", "0")] == names[(frac, "2", "0")] == "k_knn_tile<5,8>"
-    i0, e0 = out[("0", "0", "1")]
+        out[(fine, env)] = (idx.cpu().numpy(), d2.cpu().numpy())
+        names[(fine, env)] = ctx.knn_kernel()
+        assert names[(fine, env)] == name, (env, names[(fine, env)])
+    i0, e0 = out[("0", "")]
     assert (i0 >= -1).all() and (i0[:, 4] >= 0).mean() > 0.3
     for key, (i1, e1) in out.items():
         assert np.array_equal(i0, i1), key
