@@ -591,6 +591,7 @@ __device__ __forceinline__ int group_knn_list(const float4* __restrict__ lpts, c
     }
     return group_merge_topk<K, GS>(bd, bi, bp, out_pos, out_d2, out_idx);
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed fp32 pair (v_pk_*_f32)
 // Large-search variant of group_knn27 (aloam_knn_device, round 6): a candidate is one 64-bit key, (d2 bits
 // << 32) | original index (w of the sorted copy); d2 >= 0, so unsigned key order is exactly the (d2, index)
 // order of group_knn27. A lane's top K is a sorted key array updated without branches (one 64-bit compare
@@ -636,9 +637,22 @@ __device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, 
             ok[u] = t < total && (unsigned)p < (unsigned)npts;
             v[u] = spts[ok[u] ? p : 0];
         }
+        // distances two slots at a time in packed fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE
+        // operations in the same order as sqdist, ((dx^2 + dy^2) + dz^2), no contraction)
+        float dd[U];
+#pragma unroll
+        for (int u = 0; u + 1 < U; u += 2) {
+            const f32x2 ex = f32x2{v[u].x, v[u + 1].x} - f32x2{qx, qx};
+            const f32x2 ey = f32x2{v[u].y, v[u + 1].y} - f32x2{qy, qy};
+            const f32x2 ez = f32x2{v[u].z, v[u + 1].z} - f32x2{qz, qz};
+            const f32x2 s = (ex * ex + ey * ey) + ez * ez;
+            dd[u] = s.x;
+            dd[u + 1] = s.y;
+        }
+        if constexpr (U % 2) dd[U - 1] = sqdist(v[U - 1].x, v[U - 1].y, v[U - 1].z, qx, qy, qz);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const float d2 = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+            const float d2 = dd[u];
             unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)__float_as_int(v[u].w);
             if (!(ok[u] && d2 < r2) || key > bound) key = ~0ull;
             if (__any(key < bk[K - 1])) {           // wave-uniform: the branch-free insertion below

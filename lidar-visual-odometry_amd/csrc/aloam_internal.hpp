@@ -22,7 +22,7 @@ constexpr int ODOM_CNT_SLOTS = 64, ODOM_CNT_STRIDE = 16;   // odometry search co
 constexpr int LINE_LDS_CAP = 4096;   // points per line kept in LDS (larger lines use global scratch)
 constexpr int CUBE_W = 21, CUBE_H = 21, CUBE_D = 11, CUBE_N = 21 * 21 * 11;  // laserMapping.cpp:74-82
 constexpr int GRID_MAX_CELLS = 1 << 23;        // default cell cap of a grid (the cell grows x1.25 until it fits)
-constexpr int GRID_MAX_CELLS_BIG = 1 << 24;    // cap of the large-map search grids (C4 index, s2m): a 0.3 m cell over ~120 x 100 x 25 m
+constexpr int GRID_MAX_CELLS_BIG = 1 << 26;    // cap of the large-map search grids (C4 index, s2m): down to a 0.2 m cell over ~120 x 100 x 25 m
 
 // ---- device-resident bookkeeping of scanRegistration ----
 struct ScanMeta {

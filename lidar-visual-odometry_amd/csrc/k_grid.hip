@@ -73,7 +73,8 @@ __device__ inline bool grid_include(int i, const int* cube_of, const unsigned ch
 // sum of the preceding chunk sums + a local scan. 1024 threads x 16 consecutive cells per chunk (int4
 // loads), so an 8M-cell grid is 512 chunks and the chunk-sum prefix is one value per thread.
 constexpr int SCAN_T = 1024, SCAN_PER = 16, SCAN_CHUNK = SCAN_T * SCAN_PER;
-static_assert(GRID_MAX_CELLS_BIG / SCAN_CHUNK <= SCAN_T, "chunk sums: one per thread");
+constexpr int SCAN_CPT = 4;      // chunk sums per thread in the second scan launch
+static_assert(GRID_MAX_CELLS_BIG / SCAN_CHUNK <= SCAN_T * SCAN_CPT, "chunk sums: SCAN_CPT per thread");
 __device__ __forceinline__ void load16(const int* __restrict__ cnt, int i0, int nc, int v[SCAN_PER]) {
     if (i0 + SCAN_PER <= nc) {
         const int4* q = (const int4*)(cnt + i0);
@@ -102,7 +103,12 @@ __device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, c
     const int i0 = base + threadIdx.x * SCAN_PER;
     int v[SCAN_PER];
     load16(cnt, i0, nc, v);
-    const int pre = threadIdx.x < (int)blockIdx.x ? blk[threadIdx.x] : 0;   // chunks before this one
+    int pre = 0;                                                             // chunks before this one
+#pragma unroll
+    for (int c = 0; c < SCAN_CPT; c++) {
+        const int ci = threadIdx.x * SCAN_CPT + c;
+        if (ci < (int)blockIdx.x) pre += blk[ci];
+    }
     int s = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_PER; k++) s += v[k];
@@ -139,7 +145,7 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_in
     g.desc = (GridDesc*)dalloc(C, sizeof(GridDesc));
     g.cell_count = (int*)dalloc(C, sizeof(int) * ((size_t)max_cells + 1));
     g.cell_start = (int*)dalloc(C, sizeof(int) * ((size_t)max_cells + 1));
-    g.blk = (int*)dalloc(C, sizeof(int) * 2048);
+    g.blk = (int*)dalloc(C, sizeof(int) * (SCAN_T * SCAN_CPT));
     g.pts = (float4*)dalloc(C, sizeof(float4) * cap);
     g.idx = (int*)dalloc(C, sizeof(int) * cap);
     g.pcell = (int*)dalloc(C, sizeof(int) * cap);
