@@ -742,7 +742,8 @@ __device__ __forceinline__ bool keys_increasing(const unsigned long long* E, int
     return up;
 }
 
-// global layout of a split cube's scratch region G = gscr + 4 p0 (4 n u64, n > RVG_FIT >= 512)
+// global layout of a split cube's scratch region G = gscr + 4 p0 (4 n u64; split cubes have n > fit >= 512, fit =
+// ALOAM_CUBE_FIT, default 2048). rvg_T spans n + 64 u64 = 8 n + 512 bytes: rvg_mark_bytes' n + 31 relevance bytes fit.
 __device__ __forceinline__ unsigned long long* rvg_S(unsigned long long* G, int n) { return G + n; }
 __device__ __forceinline__ unsigned long long* rvg_T(unsigned long long* G, int n) { return G + 2 * (size_t)n + 64; }
 __device__ __forceinline__ int* rvg_fpos(unsigned long long* G, int n) { return (int*)(G + 3 * (size_t)n + 128); }

@@ -47,9 +47,12 @@ __device__ __forceinline__ void rvg_mark(const unsigned long long* S, const int 
 
 // The same marks as bytes, relB[point] = 0 / 1 (every point's byte written, S holds each point once), for S and
 // relB in global memory: plain byte stores instead of contended atomics on the bit words; rvg_pack_bits then
-// builds the bit words (after a workgroup barrier). relB: 16-byte aligned, n + 31 bytes readable.
+// builds the bit words (after a workgroup barrier). relB: 16-byte aligned, n + 31 bytes writable (the bytes
+// from n up to the next multiple of 32 are zeroed here, so every byte rvg_pack_bits reads is exactly 0 or 1:
+// its 4-bytes-to-4-bits fold relies on that; split cubes pass the 8 n + 512-byte rvg_T region).
 template <int NT>
 __device__ __forceinline__ void rvg_mark_bytes(const unsigned long long* S, const int n, unsigned char* relB, int* nrel) {
+    if (threadIdx.x < (unsigned)(((n + 31) & ~31) - n)) relB[n + threadIdx.x] = 0;
     int mine = 0;
     for (int q0 = threadIdx.x; q0 < n; q0 += 4 * NT) {     // 4 positions per lane in flight
         unsigned kk[4][5], pi[4];
