@@ -904,8 +904,8 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
 #define KNN2(KK, CN, UU, WP) k_knn_2phase<KK, GS, CN, UU, WP><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand, exp)
 #define KNN2W(KK, CN, UU) do { if (wp2) KNN2(KK, CN, UU, true); else KNN2(KK, CN, UU, false); } while (0)
     const char* ke = getenv("ALOAM_KNN_KEYS");
-    const bool keys = !(ke && atoi(ke) == 0) && !(exp & 6);
-    if (keys) {
+    const bool keys = GS >= 8 && !(ke && atoi(ke) == 0) && !(exp & 6);
+    if constexpr (GS >= 8) if (keys) {
         const int uk = u8 ? 8 : 4;
         std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d%s>", k <= 5 ? 5 : 8, GS, u8 ? ",U8" : "");
 #define KNNK(KK, CN, UU) k_knn_keys<KK, GS, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
