@@ -599,90 +599,31 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed fp32 pair (
 // row bounds stay in registers (a slot's position by compare / select on them, no LDS table); invalid slots
 // and points outside the radius are ~0 keys. `bound`: a key known to be >= the group's final K-th (keys
 // above it are dropped). Returns the group's K smallest keys (~0 = none), the same on every group lane.
-// UU candidate slots t, t + GS, ... of one lane into its sorted top-K key list (see group_knn27_keys)
-template <int K, int GS, int UU>
-__device__ __forceinline__ void keys_slots(const int t, const int total, const int* off, const int* pre,
-                                           const float4* __restrict__ spts, int npts, float qx, float qy, float qz, float r2,
-                                           unsigned long long bound, unsigned long long* bk) {
-    float4 v[UU];
-    bool ok[UU];
-#pragma unroll
-    for (int u = 0; u < UU; u++) {
-        const int tu = t + u * GS;
-        int o = off[0];
-#pragma unroll
-        for (int r = 1; r < 9; r++) o = tu >= pre[r] ? off[r] : o;
-        const int p = o + tu;
-        ok[u] = tu < total && (unsigned)p < (unsigned)npts;
-        v[u] = spts[ok[u] ? p : 0];
-    }
-    // distances two slots at a time in packed fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations in
-    // the same order as sqdist, ((dx^2 + dy^2) + dz^2), no contraction)
-    float dd[UU];
-#pragma unroll
-    for (int u = 0; u + 1 < UU; u += 2) {
-        const f32x2 ex = f32x2{v[u].x, v[u + 1].x} - f32x2{qx, qx};
-        const f32x2 ey = f32x2{v[u].y, v[u + 1].y} - f32x2{qy, qy};
-        const f32x2 ez = f32x2{v[u].z, v[u + 1].z} - f32x2{qz, qz};
-        const f32x2 s = (ex * ex + ey * ey) + ez * ez;
-        dd[u] = s.x;
-        dd[u + 1] = s.y;
-    }
-    if constexpr (UU % 2) dd[UU - 1] = sqdist(v[UU - 1].x, v[UU - 1].y, v[UU - 1].z, qx, qy, qz);
-#pragma unroll
-    for (int u = 0; u < UU; u++) {
-        const float d2 = dd[u];
-        unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)__float_as_int(v[u].w);
-        if (!(ok[u] && d2 < r2) || key > bound) key = ~0ull;
-        if (__any(key < bk[K - 1])) {           // wave-uniform: the branch-free insertion below
-#pragma unroll
-            for (int k = K - 1; k > 0; k--) bk[k] = key < bk[k - 1] ? bk[k - 1] : (key < bk[k] ? key : bk[k]);
-            bk[0] = key < bk[0] ? key : bk[0];
-        }
-    }
-}
 // Large-search variant of group_knn27 (aloam_knn_device, round 6): a candidate is one 64-bit key, (d2 bits
 // << 32) | original index (w of the sorted copy); d2 >= 0, so unsigned key order is exactly the (d2, index)
 // order of group_knn27. A lane's top K is a sorted key array updated without branches (one 64-bit compare
 // and two selects per slot), entered only when some lane of the wave holds a key below its K-th; the nine
-// row bounds are loaded two per lane and shared in the group by lane permutes, then stay in registers (a
-// slot's position by compare / select on them, no LDS table); full batches of U slots per lane, then single
-// slots for the rest (a wave runs its longest group's trip count); invalid slots and points outside the
-// radius are ~0 keys. `bound`: a key known to be >= the group's final K-th (keys above it are dropped).
-// Returns the group's K smallest keys (~0 = none), the same on every group lane.
+// row bounds stay in registers (a slot's position by compare / select on them, no LDS table); invalid slots
+// and points outside the radius are ~0 keys. `bound`: a key known to be >= the group's final K-th (keys
+// above it are dropped). Returns the group's K smallest keys (~0 = none), the same on every group lane.
 template <int K, int GS, int U>
 __device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, const float oz, const float inv_cell,
                                                 const int gdx, const int gdy, const int gdz, const int* __restrict__ start,
                                                 const float4* __restrict__ spts, float qx, float qy, float qz, float r2,
                                                 bool active, unsigned long long* out_key, int* ncand, int npts,
                                                 unsigned long long bound = ~0ull) {
-    static_assert(GS >= 8 || GS == 0, "row bounds: 9 rows over the group's lanes (GS >= 8)");
     const int gl = lane_id() & (GS - 1);
     const int cx = (int)floorf((qx - ox) * inv_cell), cy = (int)floorf((qy - oy) * inv_cell), cz = (int)floorf((qz - oz) * inv_cell);
     const int x0 = max(cx - 1, 0), x1 = min(cx + 1, gdx - 1);
-    // lane gl loads row gl's bounds (lane 0 also row 8)
-    int rb_a, re_a, rb_b = 0, re_b = 0;
-    {
-        const int r = gl < 9 ? gl : 0;
-        const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
-        const bool ok = active && gl < 9 && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
-        const int c = (z * gdy + y) * gdx;
-        rb_a = load_or(start, c + x0, ok, 0);
-        re_a = load_or(start, c + x1 + 1, ok, 0);
-        const int y8 = cy + 1, z8 = cz + 1;   // row 8 = (y + 1, z + 1)
-        const bool ok8 = active && gl == 0 && x0 <= x1 && y8 >= 0 && y8 < gdy && z8 >= 0 && z8 < gdz;
-        const int c8 = (z8 * gdy + y8) * gdx;
-        rb_b = load_or(start, c8 + x0, ok8, 0);
-        re_b = load_or(start, c8 + x1 + 1, ok8, 0);
-    }
     int off[9], pre[10];
     pre[0] = 0;
-    const int gbase = lane_id() & ~(GS - 1);
 #pragma unroll
     for (int r = 0; r < 9; r++) {
-        const int src = gbase + (r < 8 ? r : 0);
-        const int b = __shfl(r < 8 ? rb_a : rb_b, src, WAVE), e = __shfl(r < 8 ? re_a : re_b, src, WAVE);
-        pre[r + 1] = pre[r] + (e - b);
+        const int y = cy + (r % 3) - 1, z = cz + (r / 3) - 1;
+        const bool ok = active && x0 <= x1 && y >= 0 && y < gdy && z >= 0 && z < gdz;
+        const int c = (z * gdy + y) * gdx;
+        const int b = load_or(start, c + x0, ok, 0);
+        pre[r + 1] = pre[r] + (load_or(start, c + x1 + 1, ok, 0) - b);
         off[r] = b - pre[r];
     }
     const int total = pre[9];
@@ -690,9 +631,44 @@ __device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, 
     unsigned long long bk[K];
 #pragma unroll
     for (int k = 0; k < K; k++) bk[k] = ~0ull;
-    int t = gl;
-    for (; t + (U - 1) * GS < total; t += U * GS) keys_slots<K, GS, U>(t, total, off, pre, spts, npts, qx, qy, qz, r2, bound, bk);
-    for (; t < total; t += GS) keys_slots<K, GS, 1>(t, total, off, pre, spts, npts, qx, qy, qz, r2, bound, bk);
+    for (int t0 = gl; t0 < total; t0 += U * GS) {
+        float4 v[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + u * GS;
+            int o = off[0];
+#pragma unroll
+            for (int r = 1; r < 9; r++) o = t >= pre[r] ? off[r] : o;
+            const int p = o + t;
+            ok[u] = t < total && (unsigned)p < (unsigned)npts;
+            v[u] = spts[ok[u] ? p : 0];
+        }
+        // distances two slots at a time in packed fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE
+        // operations in the same order as sqdist, ((dx^2 + dy^2) + dz^2), no contraction)
+        float dd[U];
+#pragma unroll
+        for (int u = 0; u + 1 < U; u += 2) {
+            const f32x2 ex = f32x2{v[u].x, v[u + 1].x} - f32x2{qx, qx};
+            const f32x2 ey = f32x2{v[u].y, v[u + 1].y} - f32x2{qy, qy};
+            const f32x2 ez = f32x2{v[u].z, v[u + 1].z} - f32x2{qz, qz};
+            const f32x2 s = (ex * ex + ey * ey) + ez * ez;
+            dd[u] = s.x;
+            dd[u + 1] = s.y;
+        }
+        if constexpr (U % 2) dd[U - 1] = sqdist(v[U - 1].x, v[U - 1].y, v[U - 1].z, qx, qy, qz);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const float d2 = dd[u];
+            unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)__float_as_int(v[u].w);
+            if (!(ok[u] && d2 < r2) || key > bound) key = ~0ull;
+            if (__any(key < bk[K - 1])) {           // wave-uniform: the branch-free insertion below
+#pragma unroll
+                for (int k = K - 1; k > 0; k--) bk[k] = key < bk[k - 1] ? bk[k - 1] : (key < bk[k] ? key : bk[k]);
+                bk[0] = key < bk[0] ? key : bk[0];
+            }
+        }
+    }
     // merge: K rounds of a group min over the lanes' list heads; the owner of the minimum (unique: one
     // lane per candidate) advances its head
     int head = 0, found = 0;
