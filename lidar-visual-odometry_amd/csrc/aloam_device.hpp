@@ -606,7 +606,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));   // packed fp32 pair (
 // row bounds stay in registers (a slot's position by compare / select on them, no LDS table); invalid slots
 // and points outside the radius are ~0 keys. `bound`: a key known to be >= the group's final K-th (keys
 // above it are dropped). Returns the group's K smallest keys (~0 = none), the same on every group lane.
-template <int K, int GS, int U>
+template <int K, int GS, int U, bool PK = true>
 __device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, const float oz, const float inv_cell,
                                                 const int gdx, const int gdy, const int gdz, const int* __restrict__ start,
                                                 const float4* __restrict__ spts, float qx, float qy, float qz, float r2,
@@ -647,6 +647,10 @@ __device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, 
         // distances two slots at a time in packed fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE
         // operations in the same order as sqdist, ((dx^2 + dy^2) + dz^2), no contraction)
         float dd[U];
+        if constexpr (!PK) {
+#pragma unroll
+            for (int u = 0; u < U; u++) dd[u] = sqdist(v[u].x, v[u].y, v[u].z, qx, qy, qz);
+        } else
 #pragma unroll
         for (int u = 0; u + 1 < U; u += 2) {
             const f32x2 ex = f32x2{v[u].x, v[u + 1].x} - f32x2{qx, qx};
@@ -656,7 +660,7 @@ __device__ __forceinline__ int group_knn27_keys(const float ox, const float oy, 
             dd[u] = s.x;
             dd[u + 1] = s.y;
         }
-        if constexpr (U % 2) dd[U - 1] = sqdist(v[U - 1].x, v[U - 1].y, v[U - 1].z, qx, qy, qz);
+        if constexpr (PK && U % 2) dd[U - 1] = sqdist(v[U - 1].x, v[U - 1].y, v[U - 1].z, qx, qy, qz);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const float d2 = dd[u];

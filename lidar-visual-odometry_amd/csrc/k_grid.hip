@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(256) k_knn_2phase(const GridDesc* __restrict__
 // candidate loop has no data-dependent branches (register row bounds, branch-free top-K insertion), and
 // phase 2 starts from the phase-1 K-th key as its bound. Default since round 6 (ALOAM_KNN_KEYS=0: the
 // round-5 kernel).
-template <int K, int GS, bool CNT, int U>
+template <int K, int GS, bool CNT, int U, bool PK = true>
 __global__ void __launch_bounds__(256) k_knn_keys(const GridDesc* __restrict__ fgd, const int* __restrict__ fstart,
                                                   const float4* __restrict__ fpts, const GridDesc* __restrict__ cgd,
                                                   const int* __restrict__ cstart, const float4* __restrict__ cpts,
@@ -471,7 +471,7 @@ __global__ void __launch_bounds__(256) k_knn_keys(const GridDesc* __restrict__ f
     unsigned long long key[K];
     int nf = 0, nc = 0;
     const GridDesc gf = *fgd;
-    int f = group_knn27_keys<K, GS, U>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, qq.x, qq.y, qq.z,
+    int f = group_knn27_keys<K, GS, U, PK>(gf.ox, gf.oy, gf.oz, gf.inv_cell, gf.dx, gf.dy, gf.dz, fstart, fpts, qq.x, qq.y, qq.z,
                                        r2, live, key, &nf, gf.n);
     unsigned long long kk = ~0ull;
 #pragma unroll
@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(256) k_knn_keys(const GridDesc* __restrict__ f
     const GridDesc gc = *cgd;
     if (__any(need)) {                         // wave-uniform: every lane takes part in the group search
         unsigned long long k2[K];
-        const int f2 = group_knn27_keys<K, GS, U>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, qq.x, qq.y,
+        const int f2 = group_knn27_keys<K, GS, U, PK>(gc.ox, gc.oy, gc.oz, gc.inv_cell, gc.dx, gc.dy, gc.dz, cstart, cpts, qq.x, qq.y,
                                                   qq.z, r2, need, k2, &nc, gc.n, kk);
         if (need) {
 #pragma unroll
@@ -907,6 +907,15 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
     const bool keys = GS >= 8 && !(ke && atoi(ke) == 0) && !(exp & 6);
     if constexpr (GS >= 8) if (keys) {
         const int uk = u8 ? 8 : 4;
+        const char* pke = getenv("ALOAM_KNN_PK");   // A/B knob: 0 = scalar fp32 distances
+        if (pke && atoi(pke) == 0 && !u8) {
+            std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d,S>", k <= 5 ? 5 : 8, GS);
+            if (k <= 5) { if (cand) k_knn_keys<5, GS, true, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand);
+                          else k_knn_keys<5, GS, false, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); }
+            else { if (cand) k_knn_keys<8, GS, true, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand);
+                   else k_knn_keys<8, GS, false, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); }
+            return;
+        }
         std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d%s>", k <= 5 ? 5 : 8, GS, u8 ? ",U8" : "");
 #define KNNK(KK, CN, UU) k_knn_keys<KK, GS, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
         if (uk == 8) {
