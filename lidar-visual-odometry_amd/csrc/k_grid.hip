@@ -907,16 +907,18 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
     const bool keys = GS >= 8 && !(ke && atoi(ke) == 0) && !(exp & 6);
     if constexpr (GS >= 8) if (keys) {
         const int uk = u8 ? 8 : 4;
-        const char* pke = getenv("ALOAM_KNN_PK");   // A/B knob: 0 = scalar fp32 distances
-        if (pke && atoi(pke) == 0 && !u8) {
-            std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d,S>", k <= 5 ? 5 : 8, GS);
+        // A/B knob: ALOAM_KNN_PK=1 = distances in packed fp32 (measured 59.0 vs 57.0 us: the pair packing moves
+        // cost more than the packed ops save), default scalar
+        const char* pke = getenv("ALOAM_KNN_PK");
+        if (!(pke && atoi(pke) == 1) && !u8) {
+            std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d>", k <= 5 ? 5 : 8, GS);
             if (k <= 5) { if (cand) k_knn_keys<5, GS, true, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand);
                           else k_knn_keys<5, GS, false, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); }
             else { if (cand) k_knn_keys<8, GS, true, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand);
                    else k_knn_keys<8, GS, false, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); }
             return;
         }
-        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d%s>", k <= 5 ? 5 : 8, GS, u8 ? ",U8" : "");
+        std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d,%s>", k <= 5 ? 5 : 8, GS, u8 ? "U8" : "PK");
 #define KNNK(KK, CN, UU) k_knn_keys<KK, GS, CN, UU><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand)
         if (uk == 8) {
             if (k <= 5) { if (cand) KNNK(5, true, 8); else KNNK(5, false, 8); }

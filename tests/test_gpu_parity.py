@@ -432,13 +432,14 @@ def test_knn_device_kernels_bit_identical(gpu_ctx_factory, monkeypatch, step, fr
         ("0", ""): "k_knn_group<5,8>",
         (frac, ""): "k_knn_keys<5,8>",
         (frac, "ALOAM_KNN_U=8"): "k_knn_keys<5,8,U8>",
+        (frac, "ALOAM_KNN_PK=1"): "k_knn_keys<5,8,PK>",
         (frac, "ALOAM_KNN_KEYS=0"): "k_knn_2phase<5,8>",
         (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_SHARED=1"): "k_knn_shared<5,4>",
         (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_SHARED=1,ALOAM_KNN_SU=2"): "k_knn_shared<5,2>",
         (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_TILE=1"): "k_knn_tile<5,8>",
         (frac, "ALOAM_KNN_KEYS=0,ALOAM_KNN_TILE=2"): "k_knn_tile<5,8>",
     }
-    knobs = ("ALOAM_KNN_U", "ALOAM_KNN_KEYS", "ALOAM_KNN_SHARED", "ALOAM_KNN_SU", "ALOAM_KNN_TILE")
+    knobs = ("ALOAM_KNN_U", "ALOAM_KNN_PK", "ALOAM_KNN_KEYS", "ALOAM_KNN_SHARED", "ALOAM_KNN_SU", "ALOAM_KNN_TILE")
     for (fine, env), name in variants.items():
         for kn in knobs:
             monkeypatch.delenv(kn, raising=False)
