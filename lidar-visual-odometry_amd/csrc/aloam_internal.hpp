@@ -39,6 +39,7 @@ struct GridDesc {
     int dx, dy, dz, ncells, n;
     int nlayers;                   // > 1: cells also split by scan line (layer = int(intensity))
     int n_acc;                     // build-time counter (published to n by the scatter)
+    int npass;                     // radix build: 9-bit digit passes the cell keys need
 };
 struct Grid {
     GridDesc* desc = nullptr;      // device
@@ -54,6 +55,13 @@ struct Grid {
     int cap = 0;
     float min_cell = 1.f;
     int max_cells = GRID_MAX_CELLS;
+    // radix build scratch (large grids, grid_build_radix): key / index ping-pong, (digit, tile) counts
+    unsigned* rk[2] = {nullptr, nullptr};
+    int* rv[2] = {nullptr, nullptr};
+    int* rH = nullptr;
+    int* rHo = nullptr;
+    int* rblk = nullptr;
+    int rcap = 0;
 };
 
 // ---- Ceres-equivalent LM state (device) ----

@@ -85,8 +85,7 @@ __device__ __forceinline__ void load16(const int* __restrict__ cnt, int i0, int 
         for (int k = 0; k < SCAN_PER; k++) v[k] = i0 + k < nc ? cnt[i0 + k] : 0;
     }
 }
-__device__ __forceinline__ void k_grid_scan1_body(const int* __restrict__ cnt, const GridDesc* d, int* blk) {
-    const int nc = d->ncells;
+__device__ __forceinline__ void k_grid_scan1_body(const int* __restrict__ cnt, const int nc, int* blk) {
     const int base = blockIdx.x * SCAN_CHUNK;
     int v[SCAN_PER];
     load16(cnt, base + threadIdx.x * SCAN_PER, nc, v);
@@ -97,8 +96,7 @@ __device__ __forceinline__ void k_grid_scan1_body(const int* __restrict__ cnt, c
     (void)block_exscan<SCAN_T, true>(s, &tot);
     if (threadIdx.x == 0) blk[blockIdx.x] = tot;
 }
-__device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, const GridDesc* d, const int* blk, int* start) {
-    const int nc = d->ncells;
+__device__ __forceinline__ void k_grid_scan3_body(const int* __restrict__ cnt, const int nc, const int* blk, int* start) {
     const int base = blockIdx.x * SCAN_CHUNK;
     const int i0 = base + threadIdx.x * SCAN_PER;
     int v[SCAN_PER];
@@ -154,8 +152,9 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_in
 }
 
 void grid_free(Ctx& C, Grid& g) {
-    for (void* p : {(void*)g.desc, (void*)g.cell_count, (void*)g.cell_start, (void*)g.blk, (void*)g.pts, (void*)g.idx, (void*)g.pcell})
-        dfree(C, p);
+    for (void* p : {(void*)g.desc, (void*)g.cell_count, (void*)g.cell_start, (void*)g.blk, (void*)g.pts, (void*)g.idx, (void*)g.pcell,
+                    (void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk})
+        if (p) dfree(C, p);
     g = Grid{};
 }
 
@@ -239,12 +238,12 @@ __global__ void k_gm_count(GridJobs J) {
 __global__ void __launch_bounds__(SCAN_T) k_gm_scan1(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
     if (blockIdx.x * SCAN_CHUNK >= g.desc->ncells) return;
-    k_grid_scan1_body(g.cell_count, g.desc, g.blk);
+    k_grid_scan1_body(g.cell_count, g.desc->ncells, g.blk);
 }
 __global__ void __launch_bounds__(SCAN_T) k_gm_scan3(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
     if (blockIdx.x * SCAN_CHUNK >= g.desc->ncells) return;
-    k_grid_scan3_body(g.cell_count, g.desc, g.blk, g.cell_start);
+    k_grid_scan3_body(g.cell_count, g.desc->ncells, g.blk, g.cell_start);
 }
 __global__ void k_gm_scatter(GridJobs J) {
     const GridJob& g = J.j[blockIdx.y];
@@ -273,9 +272,19 @@ __global__ void k_gm_scatter(GridJobs J) {
     }
 }
 
+static void grid_build_radix(Ctx& C, const GridBuild* b, int nj);
+constexpr int GR_MIN = 1 << 18;   // large-map grids from this many points take the radix build
 void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     if (nj <= 0) return;
     if (nj > GRID_MULTI_MAX) throw ApiError{ALOAM_E_ARG, "grid_build_multi: too many grids"};
+    {
+        // large-map search grids (aloam_knn_build, aloam_s2m_set_map) of >= GR_MIN points: radix build
+        // (ALOAM_GRID_RADIX=0, read per build: the atomic counting sort below for them too)
+        const char* re = getenv("ALOAM_GRID_RADIX");
+        bool big = !(re && atoi(re) == 0);
+        for (int k = 0; k < nj; k++) big = big && b[k].g->max_cells == GRID_MAX_CELLS_BIG && b[k].cap_n >= GR_MIN;
+        if (big) { grid_build_radix(C, b, nj); return; }
+    }
     hipStream_t st = C.stream;
     GridJobs J{};
     int cap = 1, maxc = 0;
@@ -294,6 +303,245 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
     k_gm_scan1<<<dim3(nsb, nj), SCAN_T, 0, st>>>(J);
     k_gm_scan3<<<dim3(nsb, nj), SCAN_T, 0, st>>>(J);
     k_gm_scatter<<<dim3(nb, nj), GB, 0, st>>>(J);
+    HIPCHK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// Large grids (>= GR_MIN points: the map index of aloam_knn_build and aloam_s2m_set_map). The counting sort
+// above pays two scattered global atomics per point (count, then claim a slot), which on the 2.1M-point C4
+// map cost ~280 of the ~340 us build (k_gm_count + k_gm_scatter, profiles/r05_c4_kernel_stats.csv). Here the
+// (cell, index) pairs are radix-sorted instead (k_gm_bbox as above counts the included points): 9-bit digits, least significant first, one pass per digit
+// the cell ids need (<= 3 below 2^26 cells); per pass a digit histogram of each 4096-point tile, an
+// exclusive scan of the (digit, tile) counts, and a stable scatter in which each wave ranks its 64 keys of
+// a chunk by 9 ballots (peers with the same digit) and advances its own per-digit run in LDS. No per-point
+// global atomic; inside a cell the points end in original index order, so the built grid is deterministic.
+// Then the sorted copy (gather), each occupied cell's count from its run, the cell scan above, and the
+// counts cleared again. Excluded points (cube gating) take key ncells and sort past the last cell.
+constexpr int GR_T = 256, GR_PER = 16, GR_TILE = GR_T * GR_PER, GR_BITS = 9, GR_NB = 1 << GR_BITS;
+constexpr int GR_WAVES = GR_T / WAVE, GR_WCH = GR_TILE / GR_WAVES / WAVE;   // chunks of 64 per wave and tile
+struct GrJob {
+    GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx;
+    const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
+    float min_cell; int nlayers; int w_index; int flat; int max_cells;
+    unsigned* k0; unsigned* k1; int* v0; int* v1; int* H; int* Ho; int* Hblk;
+};
+struct GrJobs { GrJob j[GRID_MULTI_MAX]; };
+__device__ __forceinline__ int gr_tiles(int n) { return (n + GR_TILE - 1) / GR_TILE; }
+
+// grid parameters, cell keys, first digit histogram per tile
+__global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
+    const GrJob& g = J.j[blockIdx.y];
+    __shared__ GridDesc gd;
+    __shared__ int hist[GR_NB];
+    if (threadIdx.x == 0) {
+        unsigned bb[6];
+        for (int a = 0; a < 6; a++) bb[a] = g.desc->bb[a];
+        grid_params(bb, g.min_cell, g.nlayers, g.flat, g.max_cells, &gd);
+        const int bits = 32 - __clz((unsigned)gd.ncells);          // keys 0 .. ncells (ncells = excluded)
+        gd.npass = max(1, (bits + GR_BITS - 1) / GR_BITS);
+        if (blockIdx.x == 0) {
+            GridDesc* d = g.desc;
+            d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
+            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers; d->npass = gd.npass;
+        }
+    }
+    for (int i = threadIdx.x; i < GR_NB; i += GR_T) hist[i] = 0;
+    __syncthreads();
+    const int n = *g.d_n, nt = gr_tiles(n);
+    if ((int)blockIdx.x >= nt) return;
+#pragma unroll 4
+    for (int k = 0; k < GR_PER; k++) {
+        const int i = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
+        if (i >= n) break;
+        unsigned key = (unsigned)gd.ncells;                       // excluded: past the last cell
+        if (grid_include(i, g.cube_of, g.cube_valid)) {
+            const float4 p = g.pts[i];
+            const int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
+            const int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
+            const int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
+            const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
+            key = (unsigned)(((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx);
+        }
+        g.k0[i] = key;
+        g.v0[i] = i;
+        atomicAdd(&hist[key & (GR_NB - 1)], 1);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
+}
+// digit histogram of pass `pass` (data in k[pass & 1])
+__global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass) {
+    const GrJob& g = J.j[blockIdx.y];
+    if (pass >= g.desc->npass) return;
+    __shared__ int hist[GR_NB];
+    const int n = *g.d_n, nt = gr_tiles(n);
+    if ((int)blockIdx.x >= nt) return;
+    for (int i = threadIdx.x; i < GR_NB; i += GR_T) hist[i] = 0;
+    __syncthreads();
+    const unsigned* sk = (pass & 1) ? g.k1 : g.k0;
+    const int sh = pass * GR_BITS;
+#pragma unroll 4
+    for (int k = 0; k < GR_PER; k++) {
+        const int i = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
+        if (i < n) atomicAdd(&hist[(sk[i] >> sh) & (GR_NB - 1)], 1);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
+}
+// exclusive scan of the (digit, tile) counts, digit-major: H -> Ho
+__global__ void __launch_bounds__(SCAN_T) k_gr_hscan1(GrJobs J, int pass) {
+    const GrJob& g = J.j[blockIdx.y];
+    if (pass >= g.desc->npass) return;
+    const int nc = GR_NB * gr_tiles(*g.d_n);
+    if ((int)blockIdx.x * SCAN_CHUNK >= nc) return;
+    k_grid_scan1_body(g.H, nc, g.Hblk);
+}
+__global__ void __launch_bounds__(SCAN_T) k_gr_hscan3(GrJobs J, int pass) {
+    const GrJob& g = J.j[blockIdx.y];
+    if (pass >= g.desc->npass) return;
+    const int nc = GR_NB * gr_tiles(*g.d_n);
+    if ((int)blockIdx.x * SCAN_CHUNK >= nc) return;
+    k_grid_scan3_body(g.H, nc, g.Hblk, g.Ho);
+}
+// stable scatter of pass `pass`: k[pass & 1] -> k[(pass + 1) & 1]. Wave w of a tile owns its elements
+// [w * 1024, (w + 1) * 1024) and its own per-digit run in LDS (started at the tile's digit offset plus the
+// earlier waves' counts), so positions follow element order within every digit.
+__global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
+    const GrJob& g = J.j[blockIdx.y];
+    if (pass >= g.desc->npass) return;
+    __shared__ int run[GR_WAVES][GR_NB];
+    const int n = *g.d_n, nt = gr_tiles(n);
+    if ((int)blockIdx.x >= nt) return;
+    const unsigned* sk = (pass & 1) ? g.k1 : g.k0;
+    const int* sv = (pass & 1) ? g.v1 : g.v0;
+    unsigned* dk = (pass & 1) ? g.k0 : g.k1;
+    int* dv = (pass & 1) ? g.v0 : g.v1;
+    const int sh = pass * GR_BITS;
+    const int w = threadIdx.x / WAVE, lane = lane_id();
+    for (int i = threadIdx.x; i < GR_WAVES * GR_NB; i += GR_T) (&run[0][0])[i] = 0;
+    __syncthreads();
+    const int e0 = blockIdx.x * GR_TILE + w * (GR_TILE / GR_WAVES);
+    for (int j = 0; j < GR_WCH; j++) {
+        const int e = e0 + j * WAVE + lane;
+        if (e < n) atomicAdd(&run[w][(sk[e] >> sh) & (GR_NB - 1)], 1);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < GR_NB; d += GR_T) {
+        int r = g.Ho[d * nt + blockIdx.x];
+#pragma unroll
+        for (int ww = 0; ww < GR_WAVES; ww++) { const int c = run[ww][d]; run[ww][d] = r; r += c; }
+    }
+    __syncthreads();
+    const unsigned long long lt = lanemask_lt64();
+    for (int j = 0; j < GR_WCH; j++) {
+        const int e = e0 + j * WAVE + lane;
+        const bool valid = e < n;
+        const unsigned key = valid ? sk[e] : 0u;
+        const int val = valid ? sv[e] : 0;
+        const int d = (int)((key >> sh) & (GR_NB - 1));
+        unsigned long long m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < GR_BITS; b++) {
+            const bool bit = (d >> b) & 1;
+            const unsigned long long bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const int rank = __popcll(m & lt);
+        const int base = run[w][d];
+        // every lane has read its digit's run before the leader (rank 0) advances it: one wave, LDS in order
+        if (valid && rank == 0) run[w][d] = base + __popcll(m);
+        if (valid) { dk[base + rank] = key; dv[base + rank] = val; }
+    }
+}
+// sorted copy + each occupied cell's count (at the first point of its run)
+__global__ void __launch_bounds__(GR_T) k_gr_finish(GrJobs J) {
+    const GrJob& g = J.j[blockIdx.y];
+    GridDesc* d = g.desc;
+    const int npass = d->npass, ninc = d->n_acc;
+    const unsigned* sk = (npass & 1) ? g.k1 : g.k0;
+    const int* sv = (npass & 1) ? g.v1 : g.v0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) d->n = ninc;      // published for the clear and the searches
+#pragma unroll 4
+    for (int k = 0; k < GR_PER; k++) {
+        const int p = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
+        if (p >= ninc) break;
+        const unsigned key = sk[p];
+        const int val = sv[p];
+        const float4 pt = g.pts[val];
+        g.spts[p] = g.w_index ? make_float4(pt.x, pt.y, pt.z, __int_as_float(val)) : pt;
+        g.sidx[p] = val;
+        if (p == 0 || sk[p - 1] != key) {
+            int l = 1;
+            while (p + l < ninc && sk[p + l] == key) l++;
+            g.cell_count[key] = l;
+        }
+    }
+}
+// counts back to zero (the invariant between builds), bbox re-armed
+__global__ void __launch_bounds__(GR_T) k_gr_clear(GrJobs J) {
+    const GrJob& g = J.j[blockIdx.y];
+    GridDesc* d = g.desc;
+    const int npass = d->npass, ninc = d->n;
+    const unsigned* sk = (npass & 1) ? g.k1 : g.k0;
+#pragma unroll 4
+    for (int k = 0; k < GR_PER; k++) {
+        const int p = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
+        if (p >= ninc) break;
+        const unsigned key = sk[p];
+        if (p == 0 || sk[p - 1] != key) g.cell_count[key] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d->n_acc = 0;
+        for (int a = 0; a < 3; a++) { d->bb[a] = 0xffffffffu; d->bb[3 + a] = 0u; }
+    }
+}
+
+static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
+    hipStream_t st = C.stream;
+    GrJobs J{};
+    GridJobs GJ{};
+    int cap = 1, maxc = 0;
+    for (int k = 0; k < nj; k++) {
+        Grid& g = *b[k].g;
+        const int tc = (std::max(b[k].cap_n, 1) + GR_TILE - 1) / GR_TILE;
+        const int need = std::max(b[k].cap_n, g.cap);
+        if (g.rcap < need) {
+            for (void* p : {(void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk})
+                if (p) dfree(C, p);
+            const int tcap = (need + GR_TILE - 1) / GR_TILE;
+            g.rk[0] = (unsigned*)dalloc(C, sizeof(unsigned) * need);
+            g.rk[1] = (unsigned*)dalloc(C, sizeof(unsigned) * need);
+            g.rv[0] = (int*)dalloc(C, sizeof(int) * need);
+            g.rv[1] = (int*)dalloc(C, sizeof(int) * need);
+            g.rH = (int*)dalloc(C, sizeof(int) * ((size_t)GR_NB * tcap + 1));
+            g.rHo = (int*)dalloc(C, sizeof(int) * ((size_t)GR_NB * tcap + 1));   // + the scan's total
+            g.rblk = (int*)dalloc(C, sizeof(int) * SCAN_T * SCAN_CPT);
+            g.rcap = need;
+        }
+        (void)tc;
+        J.j[k] = GrJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid,
+                       g.min_cell, g.nlayers, g.w_index ? 1 : 0, g.flat ? 1 : 0, g.max_cells,
+                       g.rk[0], g.rk[1], g.rv[0], g.rv[1], g.rH, g.rHo, g.rblk};
+        GJ.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell, b[k].pts, b[k].d_n, b[k].cube_of,
+                          b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0, g.flat ? 1 : 0, g.max_cells};
+        cap = std::max(cap, b[k].cap_n);
+        maxc = std::max(maxc, g.max_cells);
+    }
+    const int nb = std::max(1, std::min(1024, (cap + GB - 1) / GB));
+    const int tiles = (cap + GR_TILE - 1) / GR_TILE;
+    const int nsbH = (GR_NB * tiles + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    k_gm_bbox<<<dim3(nb, nj), GB, 0, st>>>(GJ);
+    k_gr_keys<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
+    for (int pass = 0; pass < 3; pass++) {
+        if (pass > 0) k_gr_hist<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
+        k_gr_hscan1<<<dim3(nsbH, nj), SCAN_T, 0, st>>>(J, pass);
+        k_gr_hscan3<<<dim3(nsbH, nj), SCAN_T, 0, st>>>(J, pass);
+        k_gr_scatter<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
+    }
+    k_gr_finish<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
+    k_gm_scan1<<<dim3(maxc / SCAN_CHUNK, nj), SCAN_T, 0, st>>>(GJ);
+    k_gm_scan3<<<dim3(maxc / SCAN_CHUNK, nj), SCAN_T, 0, st>>>(GJ);
+    k_gr_clear<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     HIPCHK(hipGetLastError());
 }
 

@@ -34,8 +34,13 @@ for v in variants:
     env = dict(kv.split("=", 1) for kv in v.split(",") if kv)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
-    if "ALOAM_KNN_FINE" in env or "ALOAM_KNN_FINE" in old and old["ALOAM_KNN_FINE"] is not None or v == "REBUILD":
-        ctx.knn_build(dm.data_ptr(), len(m), 1.0)    # the fine cell is a build parameter
+    rebuild = any(k_ in env for k_ in ("ALOAM_KNN_FINE", "ALOAM_GRID_RADIX"))
+    if rebuild:                                      # build parameters: rebuild, report the build time
+        bts = []
+        for _ in range(3):
+            ctx.knn_build(dm.data_ptr(), len(m), 1.0)
+            bts.append(ctx.timing()["knn_build_ms"] * 1e3)
+        print(f"  build with {v}: {[round(b_, 1) for b_ in bts]} us", flush=True)
     idx = torch.full((len(q), 5), -7, dtype=torch.int32, device="cuda")
     d2 = torch.full((len(q), 5), -7.0, dtype=torch.float32, device="cuda")
     us, by = [], []
