@@ -255,7 +255,9 @@ int aloam_knn_device(aloam_ctx* ctx, const float* d_pts, int n, const float* d_q
  * the two-phase search; the points are copied into the index, so d_pts may change afterwards);
  * aloam_knn_query answers nq device queries against the last built index (same results as
  * aloam_knn_device with the same points and radius; ALOAM_E_STATE before any build). Synchronous.
- * aloam_knn_device = aloam_knn_build + aloam_knn_query. */
+ * aloam_knn_device = aloam_knn_build + aloam_knn_query. Device buffers passed by pointer must be complete
+ * when the call is made: the context's stream does not wait for another stream that is still filling
+ * them (or filling the output arrays). */
 int aloam_knn_build(aloam_ctx* ctx, const float* d_pts, int n, float radius);
 int aloam_knn_query(aloam_ctx* ctx, const float* d_queries, int nq, int k, int* d_idx, float* d_d2);
 /* Name of the search kernel the context's last aloam_knn_device / aloam_knn_query call launched (e.g. "k_knn_2phase<5,8>";

@@ -13,6 +13,7 @@ raises. The CPU restatement in ``oracle/`` is test infrastructure and is never i
 """
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -316,17 +317,29 @@ class Context:
         self._check(lib().aloam_knn(self.h, abi.fptr(pts), len(pts), abi.fptr(q), len(q), k, radius, abi.iptr(idx), abi.fptr(d2)))
         return idx, d2
 
+    @staticmethod
+    def _producer_sync():
+        """Device buffers handed over by pointer must be complete: torch fills / copies them on ITS current
+        stream, which the library's stream does not wait for (a torch.full still running when the search
+        writes its output would overwrite it). Not used on the per-scan path (the caller syncs once there)."""
+        tm = sys.modules.get("torch")
+        if tm is not None and tm.cuda.is_initialized():
+            tm.cuda.current_stream().synchronize()
+
     def knn_device(self, d_pts, n, d_queries, nq, k, radius, d_idx, d_d2):
         """aloam_knn_device on device pointers (ints, e.g. torch tensor .data_ptr())."""
+        self._producer_sync()
         self._check(lib().aloam_knn_device(self.h, C.c_void_p(d_pts), int(n), C.c_void_p(d_queries), int(nq), int(k),
                                            float(radius), C.c_void_p(d_idx), C.c_void_p(d_d2)))
 
     def knn_build(self, d_pts, n, radius):
         """aloam_knn_build: index n device float4 points for radius searches (built once, queried many times)."""
+        self._producer_sync()
         self._check(lib().aloam_knn_build(self.h, C.c_void_p(d_pts), int(n), float(radius)))
 
     def knn_query(self, d_queries, nq, k, d_idx, d_d2):
         """aloam_knn_query against the last knn_build index (device pointers)."""
+        self._producer_sync()
         self._check(lib().aloam_knn_query(self.h, C.c_void_p(d_queries), int(nq), int(k), C.c_void_p(d_idx),
                                           C.c_void_p(d_d2)))
 
@@ -345,6 +358,7 @@ class Context:
 
     def s2m_set_map(self, corner, surf, n_corner=None, n_surf=None):
         """The local map (laserCloudCornerFromMap / SurfFromMap) as host arrays or device pointers."""
+        self._producer_sync()
         c, nc, fc = self._pts_arg(corner, n_corner)
         s, ns, fs = self._pts_arg(surf, n_surf)
         if fc != fs:
@@ -355,6 +369,7 @@ class Context:
 
     def s2m_set_queries(self, corner, surf, n_corner=None, n_surf=None):
         """The query stacks (laserCloudCornerStack / SurfStack, body frame)."""
+        self._producer_sync()
         c, nc, fc = self._pts_arg(corner, n_corner)
         s, ns, fs = self._pts_arg(surf, n_surf)
         if fc != fs:
