@@ -73,6 +73,11 @@ EOF
             -o run --output-format csv -- python3 $R/bench.py --no-cpu $A ) > gpurun_out/${TAG}_prof.log 2>&1 \
             || fail prof gpurun_out/${TAG}_prof.log
         tail -1 gpurun_out/${TAG}_prof.log ;;
+    tpy:*)
+        # kernel trace of a python script: tpy:<script args>
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_tpy \
+            -o run --output-format csv -- python3 $R/${S#tpy:} ) > gpurun_out/${TAG}_tpy.log 2>&1 || fail "$S" gpurun_out/${TAG}_tpy.log
+        python profiles/stats.py $(find gpurun_out/${TAG}_tpy -name "*kernel_stats.csv" | head -1) 1 30 ;;
     py:*)
         timeout -k 10 600 python -u ${S#py:} > gpurun_out/${TAG}_py.txt 2>&1 || fail "$S" gpurun_out/${TAG}_py.txt
         tail -15 gpurun_out/${TAG}_py.txt ;;
