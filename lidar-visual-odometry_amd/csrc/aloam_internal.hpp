@@ -40,6 +40,7 @@ struct GridDesc {
     int nlayers;                   // > 1: cells also split by scan line (layer = int(intensity))
     int n_acc;                     // build-time counter (published to n by the scatter)
     int npass;                     // radix build: 9-bit digit passes the cell keys need
+    int ticket;                    // radix build: bbox tiles done (the last one reduces the partials)
 };
 struct Grid {
     GridDesc* desc = nullptr;      // device
@@ -61,6 +62,7 @@ struct Grid {
     int* rH = nullptr;
     int* rHo = nullptr;
     int* rblk = nullptr;
+    unsigned* rbb = nullptr;      // per-tile bbox partials (7 words per tile)
     int rcap = 0;
 };
 

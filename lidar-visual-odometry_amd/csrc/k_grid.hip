@@ -43,7 +43,7 @@ __device__ inline int cell_coord(float v, float o, float inv) { return (int)floo
 
 __global__ void k_grid_init(GridDesc* d) {
     if (threadIdx.x < 6) d->bb[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    if (threadIdx.x == 0) { d->n = 0; d->n_acc = 0; d->ncells = 0; }
+    if (threadIdx.x == 0) { d->n = 0; d->n_acc = 0; d->ncells = 0; d->npass = 1; d->ticket = 0; }
 }
 
 // Runs of equal cell ids among consecutive lanes (input clouds come line by line, so neighbours
@@ -323,53 +323,134 @@ struct GrJob {
     GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx;
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
     float min_cell; int nlayers; int w_index; int flat; int max_cells;
-    unsigned* k0; unsigned* k1; int* v0; int* v1; int* H; int* Ho; int* Hblk;
+    unsigned* k0; unsigned* k1; int* v0; int* v1; int* H; int* Ho; int* Hblk; unsigned* bbp;
 };
 struct GrJobs { GrJob j[GRID_MULTI_MAX]; };
 __device__ __forceinline__ int gr_tiles(int n) { return (n + GR_TILE - 1) / GR_TILE; }
 
-// grid parameters, cell keys, first digit histogram per tile
-__global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
+// bbox: per-tile partials (16 points per thread, loads batched), the last tile to finish reduces them and
+// writes the grid parameters, the included count and the number of digit passes into the descriptor
+__global__ void __launch_bounds__(GR_T) k_gr_bbox(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
-    __shared__ GridDesc gd;
-    __shared__ int hist[GR_NB];
-    if (threadIdx.x == 0) {
-        unsigned bb[6];
-        for (int a = 0; a < 6; a++) bb[a] = g.desc->bb[a];
-        grid_params(bb, g.min_cell, g.nlayers, g.flat, g.max_cells, &gd);
-        const int bits = 32 - __clz((unsigned)gd.ncells);          // keys 0 .. ncells (ncells = excluded)
-        gd.npass = max(1, (bits + GR_BITS - 1) / GR_BITS);
-        if (blockIdx.x == 0) {
-            GridDesc* d = g.desc;
-            d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
-            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers; d->npass = gd.npass;
+    __shared__ unsigned sh[7];
+    __shared__ int last;
+    if (threadIdx.x < 7) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    const int n = *g.d_n;
+    unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    int cnt = 0;
+    const int i0 = blockIdx.x * GR_TILE + threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < GR_PER; h += 8) {
+        float4 p[8];
+        bool in[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = i0 + (h + u) * GR_T;
+            in[u] = i < n && grid_include(i, g.cube_of, g.cube_valid);
+            p[u] = g.pts[in[u] ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (!in[u]) continue;
+            const unsigned v[3] = {f2ord(p[u].x), f2ord(p[u].y), f2ord(p[u].z)};
+#pragma unroll
+            for (int a = 0; a < 3; a++) { mn[a] = min(mn[a], v[a]); mx[a] = max(mx[a], v[a]); }
+            cnt++;
         }
     }
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const unsigned long long lo = wave_min_u64(mn[a]), hi = wave_max_u64(mx[a]);
+        if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
+    }
+    cnt = wave_sum_i(cnt);
+    if (lane_id() == 0 && cnt) atomicAdd(&sh[6], (unsigned)cnt);
+    __syncthreads();
+    if (threadIdx.x < 7) g.bbp[blockIdx.x * 8 + threadIdx.x] = sh[threadIdx.x];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&g.desc->ticket, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    // the last tile: reduce every tile's partials
+    unsigned r[7] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0, 0};
+    for (int t = threadIdx.x; t < (int)gridDim.x; t += GR_T) {
+        unsigned v[7];
+#pragma unroll
+        for (int a = 0; a < 7; a++) v[a] = __hip_atomic_load(&g.bbp[t * 8 + a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int a = 0; a < 3; a++) { r[a] = min(r[a], v[a]); r[3 + a] = max(r[3 + a], v[3 + a]); }
+        r[6] += v[6];
+    }
+    __syncthreads();
+    if (threadIdx.x < 7) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const unsigned long long lo = wave_min_u64(r[a]), hi = wave_max_u64(r[3 + a]);
+        if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
+    }
+    const int c = wave_sum_i((int)r[6]);
+    if (lane_id() == 0 && c) atomicAdd(&sh[6], (unsigned)c);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        GridDesc* d = g.desc;
+        unsigned bb[6];
+        for (int a = 0; a < 6; a++) { bb[a] = sh[a]; d->bb[a] = sh[a]; }
+        GridDesc gd;
+        grid_params(bb, g.min_cell, g.nlayers, g.flat, g.max_cells, &gd);
+        const int bits = 32 - __clz((unsigned)gd.ncells);          // keys 0 .. ncells (ncells = excluded)
+        d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
+        d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers;
+        d->npass = max(1, (bits + GR_BITS - 1) / GR_BITS);
+        d->n_acc = (int)sh[6];
+        d->ticket = 0;
+    }
+}
+// cell keys (index order) and the first digit's histogram per tile
+__global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
+    const GrJob& g = J.j[blockIdx.y];
+    __shared__ int hist[GR_NB];
+    const GridDesc gd = *g.desc;
     for (int i = threadIdx.x; i < GR_NB; i += GR_T) hist[i] = 0;
     __syncthreads();
     const int n = *g.d_n, nt = gr_tiles(n);
     if ((int)blockIdx.x >= nt) return;
-#pragma unroll 4
-    for (int k = 0; k < GR_PER; k++) {
-        const int i = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
-        if (i >= n) break;
-        unsigned key = (unsigned)gd.ncells;                       // excluded: past the last cell
-        if (grid_include(i, g.cube_of, g.cube_valid)) {
-            const float4 p = g.pts[i];
-            const int cx = min(max(cell_coord(p.x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
-            const int cy = min(max(cell_coord(p.y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
-            const int cz = min(max(cell_coord(p.z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
-            const int layer = gd.nlayers > 1 ? min(max((int)p.w, 0), gd.nlayers - 1) : 0;
-            key = (unsigned)(((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx);
+    const int i0 = blockIdx.x * GR_TILE + threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < GR_PER; h += 8) {
+        float4 p[8];
+        bool in[8], ok[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = i0 + (h + u) * GR_T;
+            ok[u] = i < n;
+            in[u] = ok[u] && grid_include(i, g.cube_of, g.cube_valid);
+            p[u] = g.pts[in[u] ? i : 0];
         }
-        g.k0[i] = key;
-        g.v0[i] = i;
-        atomicAdd(&hist[key & (GR_NB - 1)], 1);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (!ok[u]) continue;
+            const int i = i0 + (h + u) * GR_T;
+            unsigned key = (unsigned)gd.ncells;                   // excluded: past the last cell
+            if (in[u]) {
+                const int cx = min(max(cell_coord(p[u].x, gd.ox, gd.inv_cell), 0), gd.dx - 1);
+                const int cy = min(max(cell_coord(p[u].y, gd.oy, gd.inv_cell), 0), gd.dy - 1);
+                const int cz = min(max(cell_coord(p[u].z, gd.oz, gd.inv_cell), 0), gd.dz - 1);
+                const int layer = gd.nlayers > 1 ? min(max((int)p[u].w, 0), gd.nlayers - 1) : 0;
+                key = (unsigned)(((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx);
+            }
+            g.k0[i] = key;
+            g.v0[i] = i;
+            atomicAdd(&hist[key & (GR_NB - 1)], 1);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
 }
-// digit histogram of pass `pass` (data in k[pass & 1])
+// digit histogram of pass `pass` (data in k[pass & 1]), 16 keys per thread loaded at once
 __global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass) {
     const GrJob& g = J.j[blockIdx.y];
     if (pass >= g.desc->npass) return;
@@ -380,11 +461,15 @@ __global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass) {
     __syncthreads();
     const unsigned* sk = (pass & 1) ? g.k1 : g.k0;
     const int sh = pass * GR_BITS;
-#pragma unroll 4
+    unsigned kk[GR_PER];
+#pragma unroll
     for (int k = 0; k < GR_PER; k++) {
         const int i = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
-        if (i < n) atomicAdd(&hist[(sk[i] >> sh) & (GR_NB - 1)], 1);
+        kk[k] = i < n ? sk[i] : 0xffffffffu;
     }
+#pragma unroll
+    for (int k = 0; k < GR_PER; k++)
+        if (blockIdx.x * GR_TILE + k * GR_T + (int)threadIdx.x < n) atomicAdd(&hist[(kk[k] >> sh) & (GR_NB - 1)], 1);
     __syncthreads();
     for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
 }
@@ -404,8 +489,8 @@ __global__ void __launch_bounds__(SCAN_T) k_gr_hscan3(GrJobs J, int pass) {
     k_grid_scan3_body(g.H, nc, g.Hblk, g.Ho);
 }
 // stable scatter of pass `pass`: k[pass & 1] -> k[(pass + 1) & 1]. Wave w of a tile owns its elements
-// [w * 1024, (w + 1) * 1024) and its own per-digit run in LDS (started at the tile's digit offset plus the
-// earlier waves' counts), so positions follow element order within every digit.
+// [w * 1024, (w + 1) * 1024) (16 per lane, loaded at once) and its own per-digit run in LDS (started at the
+// tile's digit offset plus the earlier waves' counts), so positions follow element order within every digit.
 __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
     const GrJob& g = J.j[blockIdx.y];
     if (pass >= g.desc->npass) return;
@@ -419,12 +504,19 @@ __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
     const int sh = pass * GR_BITS;
     const int w = threadIdx.x / WAVE, lane = lane_id();
     for (int i = threadIdx.x; i < GR_WAVES * GR_NB; i += GR_T) (&run[0][0])[i] = 0;
-    __syncthreads();
-    const int e0 = blockIdx.x * GR_TILE + w * (GR_TILE / GR_WAVES);
+    const int e0 = blockIdx.x * GR_TILE + w * (GR_TILE / GR_WAVES) + lane;
+    unsigned kk[GR_WCH];
+    int vv[GR_WCH];
+#pragma unroll
     for (int j = 0; j < GR_WCH; j++) {
-        const int e = e0 + j * WAVE + lane;
-        if (e < n) atomicAdd(&run[w][(sk[e] >> sh) & (GR_NB - 1)], 1);
+        const int e = e0 + j * WAVE;
+        kk[j] = e < n ? sk[e] : 0u;
+        vv[j] = e < n ? sv[e] : 0;
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < GR_WCH; j++)
+        if (e0 + j * WAVE < n) atomicAdd(&run[w][(kk[j] >> sh) & (GR_NB - 1)], 1);
     __syncthreads();
     for (int d = threadIdx.x; d < GR_NB; d += GR_T) {
         int r = g.Ho[d * nt + blockIdx.x];
@@ -433,12 +525,10 @@ __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
     }
     __syncthreads();
     const unsigned long long lt = lanemask_lt64();
+#pragma unroll
     for (int j = 0; j < GR_WCH; j++) {
-        const int e = e0 + j * WAVE + lane;
-        const bool valid = e < n;
-        const unsigned key = valid ? sk[e] : 0u;
-        const int val = valid ? sv[e] : 0;
-        const int d = (int)((key >> sh) & (GR_NB - 1));
+        const bool valid = e0 + j * WAVE < n;
+        const int d = (int)((kk[j] >> sh) & (GR_NB - 1));
         unsigned long long m = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < GR_BITS; b++) {
@@ -450,47 +540,67 @@ __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
         const int base = run[w][d];
         // every lane has read its digit's run before the leader (rank 0) advances it: one wave, LDS in order
         if (valid && rank == 0) run[w][d] = base + __popcll(m);
-        if (valid) { dk[base + rank] = key; dv[base + rank] = val; }
+        if (valid) { dk[base + rank] = kk[j]; dv[base + rank] = vv[j]; }
     }
 }
-// sorted copy + each occupied cell's count (at the first point of its run)
+// sorted copy; each occupied cell's run END + 1 into its count slot (k_gr_counts subtracts the run start)
 __global__ void __launch_bounds__(GR_T) k_gr_finish(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
     GridDesc* d = g.desc;
     const int npass = d->npass, ninc = d->n_acc;
     const unsigned* sk = (npass & 1) ? g.k1 : g.k0;
     const int* sv = (npass & 1) ? g.v1 : g.v0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) d->n = ninc;      // published for the clear and the searches
-#pragma unroll 4
-    for (int k = 0; k < GR_PER; k++) {
-        const int p = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
-        if (p >= ninc) break;
-        const unsigned key = sk[p];
-        const int val = sv[p];
-        const float4 pt = g.pts[val];
-        g.spts[p] = g.w_index ? make_float4(pt.x, pt.y, pt.z, __int_as_float(val)) : pt;
-        g.sidx[p] = val;
-        if (p == 0 || sk[p - 1] != key) {
-            int l = 1;
-            while (p + l < ninc && sk[p + l] == key) l++;
-            g.cell_count[key] = l;
+    if (blockIdx.x == 0 && threadIdx.x == 0) d->n = ninc;      // published for the searches and the clear
+    const int p0 = blockIdx.x * GR_TILE + threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < GR_PER; h += 8) {
+        int val[8];
+        unsigned key[8], nxt[8];
+        float4 pt[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + (h + u) * GR_T;
+            const bool ok = p < ninc;
+            key[u] = ok ? sk[p] : 0u;
+            nxt[u] = p + 1 < ninc ? sk[p + 1] : 0xffffffffu;
+            val[u] = ok ? sv[p] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) pt[u] = g.pts[val[u]];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int p = p0 + (h + u) * GR_T;
+            if (p >= ninc) continue;
+            g.spts[p] = g.w_index ? make_float4(pt[u].x, pt[u].y, pt[u].z, __int_as_float(val[u])) : pt[u];
+            g.sidx[p] = val[u];
+            if (nxt[u] != key[u]) g.cell_count[key[u]] = p + 1;
         }
     }
 }
-// counts back to zero (the invariant between builds), bbox re-armed
-__global__ void __launch_bounds__(GR_T) k_gr_clear(GrJobs J) {
+// run starts: count = (end + 1) - start; clear = 0 (counts back to zero after the cell scan, bbox re-armed)
+template <bool CLEAR>
+__global__ void __launch_bounds__(GR_T) k_gr_runs(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
     GridDesc* d = g.desc;
     const int npass = d->npass, ninc = d->n;
     const unsigned* sk = (npass & 1) ? g.k1 : g.k0;
-#pragma unroll 4
+    const int p0 = blockIdx.x * GR_TILE + threadIdx.x;
+    unsigned key[GR_PER], prv[GR_PER];
+#pragma unroll
     for (int k = 0; k < GR_PER; k++) {
-        const int p = blockIdx.x * GR_TILE + k * GR_T + threadIdx.x;
-        if (p >= ninc) break;
-        const unsigned key = sk[p];
-        if (p == 0 || sk[p - 1] != key) g.cell_count[key] = 0;
+        const int p = p0 + k * GR_T;
+        key[k] = p < ninc ? sk[p] : 0u;
+        prv[k] = p > 0 && p < ninc ? sk[p - 1] : 0xffffffffu;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < GR_PER; k++) {
+        const int p = p0 + k * GR_T;
+        if (p < ninc && prv[k] != key[k]) {
+            if (CLEAR) g.cell_count[key[k]] = 0;
+            else g.cell_count[key[k]] -= p;
+        }
+    }
+    if (CLEAR && blockIdx.x == 0 && threadIdx.x == 0) {
         d->n_acc = 0;
         for (int a = 0; a < 3; a++) { d->bb[a] = 0xffffffffu; d->bb[3 + a] = 0u; }
     }
@@ -503,10 +613,10 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
     int cap = 1, maxc = 0;
     for (int k = 0; k < nj; k++) {
         Grid& g = *b[k].g;
-        const int tc = (std::max(b[k].cap_n, 1) + GR_TILE - 1) / GR_TILE;
-        const int need = std::max(b[k].cap_n, g.cap);
+        const int need = std::max(std::max(b[k].cap_n, g.cap), 1);
         if (g.rcap < need) {
-            for (void* p : {(void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk})
+            for (void* p : {(void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk,
+                            (void*)g.rbb})
                 if (p) dfree(C, p);
             const int tcap = (need + GR_TILE - 1) / GR_TILE;
             g.rk[0] = (unsigned*)dalloc(C, sizeof(unsigned) * need);
@@ -516,21 +626,24 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
             g.rH = (int*)dalloc(C, sizeof(int) * ((size_t)GR_NB * tcap + 1));
             g.rHo = (int*)dalloc(C, sizeof(int) * ((size_t)GR_NB * tcap + 1));   // + the scan's total
             g.rblk = (int*)dalloc(C, sizeof(int) * SCAN_T * SCAN_CPT);
+            g.rbb = (unsigned*)dalloc(C, sizeof(unsigned) * 8 * (size_t)tcap);
             g.rcap = need;
         }
-        (void)tc;
         J.j[k] = GrJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid,
                        g.min_cell, g.nlayers, g.w_index ? 1 : 0, g.flat ? 1 : 0, g.max_cells,
-                       g.rk[0], g.rk[1], g.rv[0], g.rv[1], g.rH, g.rHo, g.rblk};
+                       g.rk[0], g.rk[1], g.rv[0], g.rv[1], g.rH, g.rHo, g.rblk, g.rbb};
         GJ.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell, b[k].pts, b[k].d_n, b[k].cube_of,
                           b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0, g.flat ? 1 : 0, g.max_cells};
         cap = std::max(cap, b[k].cap_n);
         maxc = std::max(maxc, g.max_cells);
     }
-    const int nb = std::max(1, std::min(1024, (cap + GB - 1) / GB));
+    // every job's grid is sized by the largest cap (tiles beyond a job's live count exit; the bbox ticket
+    // counts all launched tiles of a job)
     const int tiles = (cap + GR_TILE - 1) / GR_TILE;
+    for (int k = 0; k < nj; k++)
+        if ((tiles + 0) > (b[k].g->rcap + GR_TILE - 1) / GR_TILE) throw ApiError{ALOAM_E_ARG, "grid_build_radix: tile scratch"};
     const int nsbH = (GR_NB * tiles + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    k_gm_bbox<<<dim3(nb, nj), GB, 0, st>>>(GJ);
+    k_gr_bbox<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     k_gr_keys<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     for (int pass = 0; pass < 3; pass++) {
         if (pass > 0) k_gr_hist<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
@@ -539,9 +652,10 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
         k_gr_scatter<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
     }
     k_gr_finish<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
+    k_gr_runs<false><<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     k_gm_scan1<<<dim3(maxc / SCAN_CHUNK, nj), SCAN_T, 0, st>>>(GJ);
     k_gm_scan3<<<dim3(maxc / SCAN_CHUNK, nj), SCAN_T, 0, st>>>(GJ);
-    k_gr_clear<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
+    k_gr_runs<true><<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     HIPCHK(hipGetLastError());
 }
 
