@@ -319,6 +319,7 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
 // counts cleared again. Excluded points (cube gating) take key ncells and sort past the last cell.
 constexpr int GR_T = 256, GR_PER = 16, GR_TILE = GR_T * GR_PER, GR_BITS = 9, GR_NB = 1 << GR_BITS;
 constexpr int GR_WAVES = GR_T / WAVE, GR_WCH = GR_TILE / GR_WAVES / WAVE;   // chunks of 64 per wave and tile
+static_assert(GR_NB == 2 * GR_T, "k_gr_scatter: two digits per thread in the tile prefix");
 struct GrJob {
     GridDesc* desc; int* cell_count; int* cell_start; int* blk; float4* spts; int* sidx;
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
@@ -328,12 +329,27 @@ struct GrJob {
 struct GrJobs { GrJob j[GRID_MULTI_MAX]; };
 __device__ __forceinline__ int gr_tiles(int n) { return (n + GR_TILE - 1) / GR_TILE; }
 
-// bbox: per-tile partials (16 points per thread, loads batched), the last tile to finish reduces them and
-// writes the grid parameters, the included count and the number of digit passes into the descriptor
+// the lanes of a wave holding the same 9-bit digit (peers), by 9 ballots; invalid lanes are in no set
+__device__ __forceinline__ unsigned long long gr_peers(int d, bool valid) {
+    unsigned long long m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < GR_BITS; b++) {
+        const bool bit = (d >> b) & 1;
+        const unsigned long long bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+// one LDS atomic per distinct digit of the wave (a tile's keys crowd into few digits in the high passes)
+__device__ __forceinline__ void gr_count(int* hist, int d, bool valid) {
+    const unsigned long long m = gr_peers(d, valid);
+    if (valid && __popcll(m & lanemask_lt64()) == 0) atomicAdd(&hist[d], __popcll(m));
+}
+
+// bbox: per-tile partials (16 points per thread, loads batched); k_gr_keys reduces them
 __global__ void __launch_bounds__(GR_T) k_gr_bbox(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
     __shared__ unsigned sh[7];
-    __shared__ int last;
     if (threadIdx.x < 7) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     __syncthreads();
     const int n = *g.d_n;
@@ -368,54 +384,53 @@ __global__ void __launch_bounds__(GR_T) k_gr_bbox(GrJobs J) {
     if (lane_id() == 0 && cnt) atomicAdd(&sh[6], (unsigned)cnt);
     __syncthreads();
     if (threadIdx.x < 7) g.bbp[blockIdx.x * 8 + threadIdx.x] = sh[threadIdx.x];
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&g.desc->ticket, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    // the last tile: reduce every tile's partials
-    unsigned r[7] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0, 0};
-    for (int t = threadIdx.x; t < (int)gridDim.x; t += GR_T) {
-        unsigned v[7];
-#pragma unroll
-        for (int a = 0; a < 7; a++) v[a] = __hip_atomic_load(&g.bbp[t * 8 + a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int a = 0; a < 3; a++) { r[a] = min(r[a], v[a]); r[3 + a] = max(r[3 + a], v[3 + a]); }
-        r[6] += v[6];
-    }
-    __syncthreads();
-    if (threadIdx.x < 7) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const unsigned long long lo = wave_min_u64(r[a]), hi = wave_max_u64(r[3 + a]);
-        if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
-    }
-    const int c = wave_sum_i((int)r[6]);
-    if (lane_id() == 0 && c) atomicAdd(&sh[6], (unsigned)c);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        GridDesc* d = g.desc;
-        unsigned bb[6];
-        for (int a = 0; a < 6; a++) { bb[a] = sh[a]; d->bb[a] = sh[a]; }
-        GridDesc gd;
-        grid_params(bb, g.min_cell, g.nlayers, g.flat, g.max_cells, &gd);
-        const int bits = 32 - __clz((unsigned)gd.ncells);          // keys 0 .. ncells (ncells = excluded)
-        d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
-        d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers;
-        d->npass = max(1, (bits + GR_BITS - 1) / GR_BITS);
-        d->n_acc = (int)sh[6];
-        d->ticket = 0;
-    }
 }
-// cell keys (index order) and the first digit's histogram per tile
+// every block: the bbox from all tiles' partials (the same order, the same result), the grid parameters
+// (block 0 publishes them, the included count and the digit passes); then the cell keys in index order
+// and the first digit's histogram per tile
 __global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
     __shared__ int hist[GR_NB];
-    const GridDesc gd = *g.desc;
+    __shared__ unsigned sh[7];
+    __shared__ GridDesc gds;
+    if (threadIdx.x < 7) sh[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
     for (int i = threadIdx.x; i < GR_NB; i += GR_T) hist[i] = 0;
     __syncthreads();
+    {
+        unsigned r[7] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0, 0};
+        for (int t = threadIdx.x; t < (int)gridDim.x; t += GR_T) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) { r[a] = min(r[a], g.bbp[t * 8 + a]); r[3 + a] = max(r[3 + a], g.bbp[t * 8 + 3 + a]); }
+            r[6] += g.bbp[t * 8 + 6];
+        }
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const unsigned long long lo = wave_min_u64(r[a]), hi = wave_max_u64(r[3 + a]);
+            if (lane_id() == 0) { atomicMin(&sh[a], (unsigned)lo); atomicMax(&sh[3 + a], (unsigned)hi); }
+        }
+        const int c = wave_sum_i((int)r[6]);
+        if (lane_id() == 0 && c) atomicAdd(&sh[6], (unsigned)c);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned bb[6];
+        for (int a = 0; a < 6; a++) bb[a] = sh[a];
+        GridDesc gd;
+        grid_params(bb, g.min_cell, g.nlayers, g.flat, g.max_cells, &gd);
+        const int bits = 32 - __clz((unsigned)gd.ncells);          // keys 0 .. ncells (ncells = excluded)
+        gd.npass = max(1, (bits + GR_BITS - 1) / GR_BITS);
+        gds = gd;
+        if (blockIdx.x == 0) {
+            GridDesc* d = g.desc;
+            for (int a = 0; a < 6; a++) d->bb[a] = bb[a];
+            d->ox = gd.ox; d->oy = gd.oy; d->oz = gd.oz; d->cell = gd.cell; d->inv_cell = gd.inv_cell;
+            d->dx = gd.dx; d->dy = gd.dy; d->dz = gd.dz; d->ncells = gd.ncells; d->nlayers = gd.nlayers;
+            d->npass = gd.npass;
+            d->n_acc = (int)sh[6];
+        }
+    }
+    __syncthreads();
+    const GridDesc gd = gds;
     const int n = *g.d_n, nt = gr_tiles(n);
     if ((int)blockIdx.x >= nt) return;
     const int i0 = blockIdx.x * GR_TILE + threadIdx.x;
@@ -432,7 +447,6 @@ __global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            if (!ok[u]) continue;
             const int i = i0 + (h + u) * GR_T;
             unsigned key = (unsigned)gd.ncells;                   // excluded: past the last cell
             if (in[u]) {
@@ -442,9 +456,8 @@ __global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
                 const int layer = gd.nlayers > 1 ? min(max((int)p[u].w, 0), gd.nlayers - 1) : 0;
                 key = (unsigned)(((layer * gd.dz + cz) * gd.dy + cy) * gd.dx + cx);
             }
-            g.k0[i] = key;
-            g.v0[i] = i;
-            atomicAdd(&hist[key & (GR_NB - 1)], 1);
+            if (ok[u]) { g.k0[i] = key; g.v0[i] = i; }
+            gr_count(hist, (int)(key & (GR_NB - 1)), ok[u]);
         }
     }
     __syncthreads();
@@ -469,7 +482,7 @@ __global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass) {
     }
 #pragma unroll
     for (int k = 0; k < GR_PER; k++)
-        if (blockIdx.x * GR_TILE + k * GR_T + (int)threadIdx.x < n) atomicAdd(&hist[(kk[k] >> sh) & (GR_NB - 1)], 1);
+        gr_count(hist, (int)((kk[k] >> sh) & (GR_NB - 1)), blockIdx.x * GR_TILE + k * GR_T + (int)threadIdx.x < n);
     __syncthreads();
     for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
 }
@@ -489,12 +502,17 @@ __global__ void __launch_bounds__(SCAN_T) k_gr_hscan3(GrJobs J, int pass) {
     k_grid_scan3_body(g.H, nc, g.Hblk, g.Ho);
 }
 // stable scatter of pass `pass`: k[pass & 1] -> k[(pass + 1) & 1]. Wave w of a tile owns its elements
-// [w * 1024, (w + 1) * 1024) (16 per lane, loaded at once) and its own per-digit run in LDS (started at the
-// tile's digit offset plus the earlier waves' counts), so positions follow element order within every digit.
+// [w * 1024, (w + 1) * 1024) (16 per lane, loaded at once) and its own per-digit run (started at the tile's
+// digit prefix plus the earlier waves' counts), so positions follow element order within every digit. The
+// tile is first laid out by digit in LDS, then written out by consecutive threads: each digit's stretch of
+// the tile is one contiguous run of the output (coalesced stores).
 __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
     const GrJob& g = J.j[blockIdx.y];
     if (pass >= g.desc->npass) return;
     __shared__ int run[GR_WAVES][GR_NB];
+    __shared__ int lpre[GR_NB], gofs[GR_NB];
+    __shared__ unsigned stk[GR_TILE];
+    __shared__ int stv[GR_TILE];
     const int n = *g.d_n, nt = gr_tiles(n);
     if ((int)blockIdx.x >= nt) return;
     const unsigned* sk = (pass & 1) ? g.k1 : g.k0;
@@ -514,33 +532,59 @@ __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
         vv[j] = e < n ? sv[e] : 0;
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < GR_WCH; j++)
-        if (e0 + j * WAVE < n) atomicAdd(&run[w][(kk[j] >> sh) & (GR_NB - 1)], 1);
-    __syncthreads();
-    for (int d = threadIdx.x; d < GR_NB; d += GR_T) {
-        int r = g.Ho[d * nt + blockIdx.x];
-#pragma unroll
-        for (int ww = 0; ww < GR_WAVES; ww++) { const int c = run[ww][d]; run[ww][d] = r; r += c; }
-    }
-    __syncthreads();
+    unsigned long long pm[GR_WCH];
     const unsigned long long lt = lanemask_lt64();
 #pragma unroll
     for (int j = 0; j < GR_WCH; j++) {
         const bool valid = e0 + j * WAVE < n;
         const int d = (int)((kk[j] >> sh) & (GR_NB - 1));
-        unsigned long long m = __ballot(valid);
+        pm[j] = gr_peers(d, valid);
+        if (valid && __popcll(pm[j] & lt) == 0) atomicAdd(&run[w][d], __popcll(pm[j]));
+    }
+    __syncthreads();
+    // tile-local digit prefix (LDS layout) and the digit's global offset for this tile
+    {
+        int tc[2];
 #pragma unroll
-        for (int b = 0; b < GR_BITS; b++) {
-            const bool bit = (d >> b) & 1;
-            const unsigned long long bb = __ballot(bit);
-            m &= bit ? bb : ~bb;
+        for (int q = 0; q < 2; q++) {
+            const int d = threadIdx.x * 2 + q;
+            int c = 0;
+#pragma unroll
+            for (int ww = 0; ww < GR_WAVES; ww++) c += run[ww][d];
+            tc[q] = c;
         }
-        const int rank = __popcll(m & lt);
+        int tot;
+        const int ex = block_exscan<GR_T>(tc[0] + tc[1], &tot);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int d = threadIdx.x * 2 + q;
+            int r = ex + (q ? tc[0] : 0);
+            lpre[d] = r;
+            gofs[d] = g.Ho[d * nt + blockIdx.x];
+#pragma unroll
+            for (int ww = 0; ww < GR_WAVES; ww++) { const int c = run[ww][d]; run[ww][d] = r; r += c; }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < GR_WCH; j++) {
+        const bool valid = e0 + j * WAVE < n;
+        const int d = (int)((kk[j] >> sh) & (GR_NB - 1));
+        const int rank = __popcll(pm[j] & lt);
         const int base = run[w][d];
         // every lane has read its digit's run before the leader (rank 0) advances it: one wave, LDS in order
-        if (valid && rank == 0) run[w][d] = base + __popcll(m);
-        if (valid) { dk[base + rank] = kk[j]; dv[base + rank] = vv[j]; }
+        if (valid && rank == 0) run[w][d] = base + __popcll(pm[j]);
+        if (valid) { stk[base + rank] = kk[j]; stv[base + rank] = vv[j]; }
+    }
+    __syncthreads();
+    const int cnt = min(GR_TILE, n - (int)blockIdx.x * GR_TILE);
+#pragma unroll 4
+    for (int t = threadIdx.x; t < cnt; t += GR_T) {
+        const unsigned key = stk[t];
+        const int d = (int)((key >> sh) & (GR_NB - 1));
+        const int pos = gofs[d] + (t - lpre[d]);
+        dk[pos] = key;
+        dv[pos] = stv[t];
     }
 }
 // sorted copy; each occupied cell's run END + 1 into its count slot (k_gr_counts subtracts the run start)
