@@ -71,6 +71,64 @@ def parse():
     return ap.parse_args()
 
 
+def c4_pmc(counters, timeout_s=240):
+    """One rocprofv3 --pmc pass (no traces) over a child `bench.py --c4-only`: mean per launch of each counter
+    for the timed search instance. Returns ({counter: value}, None) or (None, reason)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None, "rocprofv3 not on PATH"
+    out = tempfile.mkdtemp(prefix="c4pmc_", dir="/tmp")
+    dist_vars = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+                 "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+                 "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE", "ROLE_NAME")
+    env = {k: v for k, v in os.environ.items() if k not in dist_vars}
+    env["TMPDIR"] = "/tmp"
+    local = os.environ.get("LOCAL_RANK")
+    if local is not None:
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+        ids = vis.split(",") if vis else None
+        env["HIP_VISIBLE_DEVICES"] = ids[int(local)] if ids and int(local) < len(ids) else local
+    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["-d", out, "-o", "run", "--output-format", "csv", "--",
+                                                     sys.executable, os.path.abspath(__file__), "--c4-only", "--c4-launches", "3"]
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout_s, capture_output=True, text=True)
+        if r.returncode != 0:
+            tail = (r.stderr or r.stdout or "").strip().splitlines()[-3:]
+            return None, f"rocprofv3 exit {r.returncode}: " + " | ".join(tail)[-400:]
+        vals = {}
+        for root, _, files in os.walk(out):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    for row in csv.DictReader(open(os.path.join(root, f))):
+                        if re.search(r"k_knn_\w+<\d+, \d+, false", row["Kernel_Name"]):
+                            vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        if not vals:
+            return None, "no counter rows for the timed k_knn instance"
+        return {k: float(np.median(v)) for k, v in vals.items()}, None
+    except Exception as e:  # noqa: BLE001
+        return None, repr(e)[-400:]
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def c4_valu_issue():
+    """VALU issue occupancy of the timed C4 search: SQ_INSTS_VALU wave instructions per launch x 4 cycles (a
+    wave64 VALU instruction on a 16-lane SIMD) over the 1024 SIMDs (256 CUs x 4) x the launch's GPU cycles
+    (GRBM_GUI_ACTIVE, summed over the 8 XCDs: / 8). Returns (dict, None) or (None, reason)."""
+    v, err = c4_pmc(["SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"])
+    if v is None:
+        return None, err
+    cyc = v.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    ins = v.get("SQ_INSTS_VALU", 0.0)
+    if cyc <= 0:
+        return None, "no GRBM_GUI_ACTIVE"
+    return {"valu_wave_insts_per_launch": ins, "waves": v.get("SQ_WAVES"), "gpu_cycles_per_launch": round(cyc, 0),
+            "simd_issue_frac": round(ins * 4.0 / (1024.0 * cyc), 4)}, None
+
+
 def c4_traffic(timeout_s=240):
     """HBM-side bytes per launch of the C4 search kernel: one rocprofv3 PMC pass (FETCH_SIZE only, no
     traces) over a child `bench.py --c4-only`, corrected as MI355X_MICROARCH.md prescribes for
@@ -487,6 +545,7 @@ def main():
         c4 = c4_search(lvo, torch, dev, args.c4_launches)
         ach = c4["bytes"] / (c4["ms"] * 1e-3) / 1e9
         traffic, traffic_err = (None, "skipped (--no-traffic)") if args.no_traffic else c4_traffic()
+        valu, valu_err = (None, "skipped (--no-traffic)") if args.no_traffic else c4_valu_issue()
         hbm_ach = traffic / (c4["ms"] * 1e-3) / 1e9 if traffic else None
         # the search roofline is judged on C4; the C3 kernel is latency-bound (roofline_c3).
         # Bound from the evidence: the 33 MB map stays on die (FETCH_SIZE << algorithmic bytes, TCC hit rate
@@ -505,6 +564,10 @@ def main():
             "frac": round(st_ach / L2_GATHER_GBS, 4),
             "traffic": traffic,
             "traffic_error": traffic_err,
+            # the resource that binds this kernel (PMC, separate pass): VALU instruction issue, ~0.9 of the SIMDs'
+            # issue slots — per candidate the distance, the (d2, index) key and the sorted top-k insertion
+            "valu_issue": valu,
+            "valu_issue_error": valu_err,
             "avg_launch_us": round(c4["ms"] * 1000.0, 2),
             "algorithmic_bytes_per_launch": round(c4["streamed"], 0),
             "note": "bound from the evidence: the 33 MB map is re-read on die (traffic = rocprofv3 FETCH_SIZE per launch, "
