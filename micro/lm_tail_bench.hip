@@ -77,3 +77,46 @@ extern "C" int parts_run(const double* tot, unsigned long long* cyc, double* out
     hipFree(dt); hipFree(dout); hipFree(dc);
     return (int)hipGetLastError();
 }
+
+// the same passes with the solver state in registers (thread 0's private copy), tot / x still in LDS
+__global__ void k_tail_reg(const double* tot_in, const double* x_in, unsigned long long* cyc, double* out, int reps) {
+    __shared__ double tot[NACC];
+    __shared__ double xl[7];
+    __shared__ LMState sink;
+    if (threadIdx.x < NACC) tot[threadIdx.x] = tot_in[threadIdx.x];
+    if (threadIdx.x < 7) xl[threadIdx.x] = x_in[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        LMState L;
+        unsigned long long acc0 = 0, acc1 = 0;
+        for (int r = 0; r < reps; r++) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            lm_tail_fast(&L, tot, 0, xl, nullptr, 4);
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            lm_post(&L);
+            tot[27] = tot[27] * 0.9;           // a decrease: accepted
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            lm_tail_fast(&L, tot, 1, xl, nullptr, 4);
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+            acc0 += t1 - t0; acc1 += t3 - t2;
+            tot[27] = tot_in[27];
+            for (int i = 0; i < 7; i++) xl[i] = x_in[i];
+        }
+        cyc[0] = acc0 / reps; cyc[1] = acc1 / reps;
+        for (int i = 0; i < 7; i++) out[i] = L.cand[i];
+        sink = L;
+    }
+}
+extern "C" int tail_run_reg(const double* tot, const double* x, unsigned long long* cyc, double* out) {
+    double *dt, *dx, *dout; unsigned long long* dc;
+    (void)hipMalloc(&dt, 8 * 32); (void)hipMalloc(&dx, 64); (void)hipMalloc(&dout, 64); (void)hipMalloc(&dc, 16);
+    (void)hipMemcpy(dt, tot, 8 * 29, hipMemcpyHostToDevice); (void)hipMemcpy(dx, x, 56, hipMemcpyHostToDevice);
+    k_tail_reg<<<1, 64>>>(dt, dx, dc, dout, 20);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(cyc, dc, 16, hipMemcpyDeviceToHost); (void)hipMemcpy(out, dout, 56, hipMemcpyDeviceToHost);
+    (void)hipFree(dt); (void)hipFree(dx); (void)hipFree(dout); (void)hipFree(dc);
+    return (int)hipGetLastError();
+}

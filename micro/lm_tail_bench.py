@@ -19,3 +19,7 @@ print(f"rc {rc}: tail pass 0 {cyc[0]} cycles ({cyc[0] / 2.4e3:.2f} us), accepted
 cy = (C.c_ulonglong * 4)(); o = np.zeros(8)
 L.parts_run(tot.ctypes.data_as(C.c_void_p), cy, o.ctypes.data_as(C.c_void_p))
 print(f"pieces: chol_solve6 {cy[0]}, plus7 {cy[1]}, 3 dependent fp64 divisions {cy[2]}, rsqrt_nr {cy[3]} cycles")
+cyr = (C.c_ulonglong * 2)(); outr = np.zeros(8)
+rc = L.tail_run_reg(tot.ctypes.data_as(C.c_void_p), x.ctypes.data_as(C.c_void_p), cyr, outr.ctypes.data_as(C.c_void_p))
+print(f"state in registers: rc {rc}: tail pass 0 {cyr[0]} cycles ({cyr[0] / 2.4e3:.2f} us), accepted pass {cyr[1]} cycles "
+      f"({cyr[1] / 2.4e3:.2f} us); same candidate {bool(np.array_equal(outr[:7], out[:7]))}")
