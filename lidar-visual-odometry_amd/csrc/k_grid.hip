@@ -1317,11 +1317,16 @@ static void knn_2phase_launch(Ctx& C, Grid& gf, Grid& gc, const float4* q, int n
         // cost more than the packed ops save), default scalar
         const char* pke = getenv("ALOAM_KNN_PK");
         if (!(pke && atoi(pke) == 1) && !u8) {
-            std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d>", k <= 5 ? 5 : 8, GS);
-            if (k <= 5) { if (cand) k_knn_keys<5, GS, true, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand);
-                          else k_knn_keys<5, GS, false, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); }
-            else { if (cand) k_knn_keys<8, GS, true, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand);
-                   else k_knn_keys<8, GS, false, 4, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); }
+            // ALOAM_KNN_U=2 / 3 (tuning knob): candidate slots per lane and batch (default 4)
+            const int us = ue ? atoi(ue) : 4;
+            std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), us == 2 || us == 3 ? "k_knn_keys<%d,%d,U%d>" : "k_knn_keys<%d,%d>",
+                          k <= 5 ? 5 : 8, GS, us);
+#define KNNKS(KK, UU) do { if (cand) k_knn_keys<KK, GS, true, UU, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); \
+                           else k_knn_keys<KK, GS, false, UU, false><<<blocks, 256, 0, C.stream>>>(gf.desc, gf.cell_start, gf.pts, gc.desc, gc.cell_start, gc.pts, q, nq, k, r2, idx, d2, cand); } while (0)
+            if (us == 2) { if (k <= 5) KNNKS(5, 2); else KNNKS(8, 2); }
+            else if (us == 3) { if (k <= 5) KNNKS(5, 3); else KNNKS(8, 3); }
+            else { if (k <= 5) KNNKS(5, 4); else KNNKS(8, 4); }
+#undef KNNKS
             return;
         }
         std::snprintf(C.knn_kernel, sizeof(C.knn_kernel), "k_knn_keys<%d,%d,%s>", k <= 5 ? 5 : 8, GS, u8 ? "U8" : "PK");
