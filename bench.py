@@ -244,7 +244,32 @@ def c4_registration(lvo, torch, dev, dist, rank, world, steps, cpu_rounds):
     ctx = lvo.Context(p, device=dev.index or 0)
     ctx.s2m_set_map(d_m.data_ptr(), d_m.data_ptr(), len(cm), len(sm))
     ctx.s2m_set_queries(d_cq.data_ptr(), d_sq.data_ptr(), len(cq), len(sq))
-    lvo.replicas.init_shard(ctx, dist)
+    exchange = "none (1 rank)"
+    if world > 1:
+        # the device exchange (one persistent Solve per rank, records over IPC-mapped peer memory) unless
+        # ALOAM_BENCH_EXCHANGE=rccl; RCCL all-gathers if it cannot be opened or a warm-up registration fails
+        # on any rank (decided collectively)
+        exchange = "rccl"
+        if os.environ.get("ALOAM_BENCH_EXCHANGE", "device") == "device":
+            ok = True
+            try:
+                lvo.replicas.init_peer_exchange(ctx, dist)
+                for _ in range(2):
+                    ctx.s2m_register(x0)
+            except (RuntimeError, lvo.ALOAMError) as e:
+                ok = False
+                print(f"[bench] rank {rank}: device exchange failed ({e}); RCCL exchange", file=sys.stderr)
+            flags = [None] * world
+            dist.all_gather_object(flags, ok)
+            if all(flags):
+                exchange = "device"
+            else:
+                try:
+                    ctx.shard_peer_close()
+                except lvo.ALOAMError:
+                    pass
+        if exchange == "rccl":
+            lvo.replicas.init_shard(ctx, dist)
     for _ in range(2):
         g = ctx.s2m_register(x0)
     elapsed, g = lvo.replicas.timed_region(lambda: [ctx.s2m_register(x0) for _ in range(steps)][-1], dist=dist,
@@ -255,8 +280,9 @@ def c4_registration(lvo, torch, dev, dist, rank, world, steps, cpu_rounds):
         "value": round(steps / elapsed, 3), "unit": "registrations/s", "n_gpus": world, "steps": steps,
         "ms_per_registration": round(elapsed / steps * 1e3, 4), "scaling": "strong",
         "parallelism": f"query slots sharded x{world} ({g['slot_end'] - g['slot_begin']} on rank {rank}), map replicated",
-        "exchange": "RCCL all-gather of 256 x 32 fp64 normal-equation records per LM pass" if world > 1 else
-                    "none (1 rank)",
+        "exchange": {"device": "device-side: one persistent Solve per rank, 256 x 32 fp64 normal-equation records "
+                               "gathered over IPC-mapped peer memory per LM pass (aloam_shard_peer_open)",
+                     "rccl": "RCCL all-gather of 256 x 32 fp64 normal-equation records per LM pass"}.get(exchange, exchange),
         "pose_err_m": float(np.linalg.norm(g["x"][4:] - x_true[4:])),
         "surf_correspondences_last_round": g["surf_num"][-1],
     }

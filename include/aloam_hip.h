@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ALOAM_ABI_VERSION 6
+#define ALOAM_ABI_VERSION 7
 
 /* error codes */
 #define ALOAM_OK             0
@@ -393,6 +393,22 @@ int aloam_s2m_register_group(aloam_ctx** ctxs, int world, double x[7], aloam_s2m
  * id a one-rank communicator is created and the exchange still goes through RCCL. */
 int aloam_shard_unique_id(unsigned char id[128]);
 int aloam_shard_init(aloam_ctx* ctx, int rank, int world, const unsigned char* id);
+/* The exchange on the device, no host and no RCCL in it (replaces the per-pass ncclAllGather of
+ * aloam_s2m_register; the reference's counterpart is ceres::Solve's in-process evaluation,
+ * laserMapping.cpp:714-721). Each rank exports a small uncached buffer (records + arrival counters);
+ * aloam_shard_peer_handle returns its IPC handle, the caller all-gathers the world's handles (e.g.
+ * torch.distributed), every rank calls aloam_shard_peer_open with them (rank r's handle at
+ * handles + r * ALOAM_PEER_HANDLE_BYTES), then a barrier, then aloam_s2m_register as usual: every Solve
+ * is one persistent launch per rank whose workgroups publish their block records, wait on the peers'
+ * monotonic arrival counters and gather the peers' records over xGMI themselves; results are
+ * bit-identical to the RCCL exchange. World <= 8, one rank per GPU (or several processes on one GPU
+ * with ALOAM_S2M_SOLVE_G x world <= the CU count), the same ALOAM_S2M_SOLVE_G on every rank. While open it
+ * takes precedence over a shard communicator. A peer that never arrives ends the Solve after ~2 s
+ * with ALOAM_E_HIP and closes the exchange (open it again on every rank). */
+#define ALOAM_PEER_HANDLE_BYTES 64
+int aloam_shard_peer_handle(aloam_ctx* ctx, unsigned char handle[ALOAM_PEER_HANDLE_BYTES]);
+int aloam_shard_peer_open(aloam_ctx* ctx, const unsigned char* handles, int world, int rank);
+int aloam_shard_peer_close(aloam_ctx* ctx);
 /* [begin, end) query slots of `rank` among n_slots (pure host function, no device needed). */
 int aloam_shard_slot_range(int n_slots, int rank, int world, int* begin, int* end);
 

@@ -73,6 +73,9 @@ def _declare(L):
     L.aloam_shard_unique_id.argtypes = [C.c_char_p]
     L.aloam_shard_init.argtypes = [vp, C.c_int, C.c_int, C.c_char_p]
     L.aloam_shard_slot_range.argtypes = [C.c_int, C.c_int, C.c_int, I, I]
+    L.aloam_shard_peer_handle.argtypes = [vp, C.c_char_p]
+    L.aloam_shard_peer_open.argtypes = [vp, C.c_char_p, C.c_int, C.c_int]
+    L.aloam_shard_peer_close.argtypes = [vp]
     L.aloam_set_cu_mask.argtypes = [vp, C.POINTER(C.c_uint), C.c_int]
     L.aloam_set_cu_mask.restype = C.c_int
     L.aloam_serial_sort_fallbacks.argtypes = [C.POINTER(C.c_ulonglong)]
@@ -95,7 +98,8 @@ def _declare(L):
     for name in ("aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing"):
         getattr(L, name).restype = C.c_int
     for name in ("aloam_s2m_set_map", "aloam_s2m_set_queries", "aloam_s2m_register", "aloam_s2m_register_group",
-                 "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range"):
+                 "aloam_shard_unique_id", "aloam_shard_init", "aloam_shard_slot_range",
+                 "aloam_shard_peer_handle", "aloam_shard_peer_open", "aloam_shard_peer_close"):
         getattr(L, name).restype = C.c_int
     for name in ("aloam_forward_mapping_input", "aloam_knn_device", "aloam_knn_build", "aloam_knn_query", "aloam_forward_features", "aloam_scan_registration", "aloam_feature_counts", "aloam_get_features", "aloam_odometry",
                  "aloam_set_features", "aloam_set_odom_state", "aloam_mapping", "aloam_set_mapping_input",
@@ -136,6 +140,7 @@ EXPORTED_SYMBOLS = [
     "aloam_pipeline_create", "aloam_pipeline_destroy", "aloam_pipeline_last_error", "aloam_pipeline_context",
     "aloam_pipeline_push", "aloam_pipeline_flush", "aloam_pipeline_set_profiling", "aloam_pipeline_timing",
     "aloam_map_high_freq_pose", "aloam_knn_kernel", "aloam_knn_build", "aloam_knn_query",
+    "aloam_shard_peer_handle", "aloam_shard_peer_open", "aloam_shard_peer_close",
 ]
 
 
@@ -390,6 +395,22 @@ class Context:
         if world > 1 and (uid is None or len(uid) != 128):
             raise ALOAMError("shard_init needs the 128-byte unique id for world > 1")
         self._check(lib().aloam_shard_init(self.h, int(rank), int(world), bytes(uid) if uid is not None else None))
+
+    def shard_peer_handle(self):
+        """64-byte IPC handle of this context's exchange buffer (aloam_shard_peer_handle)."""
+        buf = C.create_string_buffer(64)
+        self._check(lib().aloam_shard_peer_handle(self.h, buf))
+        return buf.raw
+
+    def shard_peer_open(self, handles, rank):
+        """Open the device-side exchange over the world's handles (rank order); collective, follow it with a
+        barrier before the first s2m_register (aloam_shard_peer_open)."""
+        if any(len(h) != 64 for h in handles):
+            raise ALOAMError("peer handles are 64 bytes each")
+        self._check(lib().aloam_shard_peer_open(self.h, b"".join(bytes(h) for h in handles), len(handles), int(rank)))
+
+    def shard_peer_close(self):
+        self._check(lib().aloam_shard_peer_close(self.h))
 
     def set_profiling(self, on):
         self._check(lib().aloam_set_profiling(self.h, int(on)))

@@ -1640,6 +1640,25 @@ int aloam_shard_init(aloam_ctx* ctx, int rank, int world, const unsigned char* i
     API_END
 }
 
+int aloam_shard_peer_handle(aloam_ctx* ctx, unsigned char handle[ALOAM_PEER_HANDLE_BYTES]) {
+    API_BEGIN(ctx)
+    if (!handle) throw ApiError{ALOAM_E_ARG, "null handle"};
+    shard_peer_handle(C, handle);
+    API_END
+}
+
+int aloam_shard_peer_open(aloam_ctx* ctx, const unsigned char* handles, int world, int rank) {
+    API_BEGIN(ctx)
+    shard_peer_open(C, handles, world, rank);
+    API_END
+}
+
+int aloam_shard_peer_close(aloam_ctx* ctx) {
+    API_BEGIN(ctx)
+    shard_peer_close(C);
+    API_END
+}
+
 int aloam_shard_slot_range(int n_slots, int rank, int world, int* begin, int* end) {
     return shard_slot_range(n_slots, rank, world, begin, end);
 }

@@ -81,6 +81,18 @@ struct LMState {
     unsigned ticket;
 };
 
+// ---- the sharded registration's record exchange on the device (k_s2m_solve, k_s2m.hip) ----
+constexpr int S2M_PEER_MAX = 8;    // ranks of a device-side exchange (one node)
+constexpr int S2M_BARS = 16;       // barrier / arrival counters per rank, 32 unsigned apart
+struct S2MPeers {
+    double* recs;                  // [2][nrec][32] this rank's gathered records (parity = global pass & 1)
+    unsigned* gath;                // [S2M_BARS x 32] local barrier counters, monotonic
+    unsigned* base;                // global passes run by this rank's earlier Solves (the same on every rank)
+    double* xrec[S2M_PEER_MAX];    // every rank's exported records [2][nrec][32] (uncached memory; peers over xGMI)
+    unsigned* xarr[S2M_PEER_MAX];  // every rank's arrival counters [S2M_BARS x 32] (uncached, monotonic)
+    int world, rank, rp;           // rp: record blocks per rank (slice_of)
+};
+
 struct OdomState {                 // laserOdometry.cpp:123-137
     double para[7];                // q_last_curr (x,y,z,w), t_last_curr
     double q_w[4], t_w[3];
@@ -434,5 +446,8 @@ void s2m_release(Ctx& C);
 void shard_unique_id(unsigned char* id);
 void shard_init(Ctx& C, int rank, int world, const unsigned char* id);
 int shard_slot_range(int n_slots, int rank, int world, int* begin, int* end);
+void shard_peer_handle(Ctx& C, unsigned char* out);
+void shard_peer_open(Ctx& C, const unsigned char* handles, int world, int rank);
+void shard_peer_close(Ctx& C);
 
 }  // namespace aloam

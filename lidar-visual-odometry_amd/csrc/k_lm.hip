@@ -1034,15 +1034,48 @@ __global__ void __launch_bounds__(CB) k_s2m_final(const double* __restrict__ pre
     }
 }
 
-// One Solve of the sharded registration at world 1 as ONE launch: the same records, reductions and tails as
+// One Solve of the sharded registration as ONE launch per rank: the same records, reductions and tails as
 // the max_iter + 1 pass launches and the final launch above, bit for bit (k_s2m_pass's block record code
-// and k_s2m_final's tail). G co-resident workgroups compute the nrec block records of a pass (workgroup w:
-// blocks w, w + G, ...) into a double-buffered record array, meet at a grid barrier (agent-scope counter
-// `bar`: S2M_BARS counters, zeroed before the launch), then every workgroup reduces the nrec records in block order and runs
-// the tail on its LDS copy of the state; a Solve that terminated stops in every workgroup at the same pass.
-constexpr int S2M_BARS = 16;                 // k_s2m_solve's barrier counters (32 unsigned apart)
+// and k_s2m_final's tail). G co-resident workgroups compute this rank's block records of a pass (workgroup
+// w: blocks rec0 + w, rec0 + w + G, ...) into the double-buffered record array T.recs. At world > 1 each
+// record also goes to the rank's exported array T.xrec[rank] (uncached memory other ranks map: IPC over
+// xGMI, or direct pointers in group mode), every workgroup then announces the pass on its arrival counter
+// (system scope), waits for every peer's arrivals of the same pass and copies its share of the peers'
+// blocks into T.recs: the all-gather with no host and no collective library in between. A local barrier
+// (agent-scope counters T.gath) closes the pass, then every workgroup reduces the nrec records in block
+// order and runs the tail on its LDS copy of the state; a Solve that terminated stops in every workgroup,
+// on every rank, at the same pass. All counters are monotonic: pass gp (= *T.base + pass, counted over the
+// rank's Solves) is complete when counter c reads (gp + 1) x the workgroups on it, so nothing is zeroed
+// between Solves and a straggling peer can never be mistaken for a finished one. Every rank runs the same
+// G and the same passes, so the counts agree. A wait longer than ~2 s (a peer that never launched) sets
+// *err and ends the Solve (results void).
+__device__ __forceinline__ bool s2m_wait(const unsigned* const* ctr, int nranks, int skip, unsigned G, unsigned gp, bool sys, int* err,
+                                         int code) {
+    const int lane = threadIdx.x;                     // wave 0 only; lanes poll (rank, counter) pairs
+    const unsigned long long t0 = wall_clock64();
+    while (true) {
+        bool late = false;
+        for (int i = lane; i < nranks * S2M_BARS; i += WAVE) {
+            const int r = i / S2M_BARS, c = i % S2M_BARS;
+            if (r == skip) continue;
+            const unsigned want = (G / S2M_BARS + ((unsigned)c < G % S2M_BARS ? 1u : 0u)) * (gp + 1u);
+            const unsigned v = sys ? __hip_atomic_load(&ctr[r][c * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                   : __hip_atomic_load(&ctr[r][c * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            late |= (int)(v - want) < 0;
+        }
+        if (!__ballot(late)) break;
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > 200000000ull) {     // 100 MHz constant clock: 2 s
+            if (lane == 0) atomicCAS(err, 0, code);   // the first wait that gave up
+            return false;
+        }
+    }
+    if (sys) __threadfence_system(); else __threadfence();
+    return true;
+}
+
 __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict__ f, int nslots, int per, int nrec,
-                                                  double* __restrict__ recs, unsigned* bar, int* err, double* x, LMState* st_out,
+                                                  const S2MPeers T, int* err, double* x, LMState* st_out,
                                                   aloam_lm_summary* sum, int max_iter, int* round_cnt) {
     __shared__ double rows[CB / 4 * NACC];
     __shared__ double part8[8 * NACC];
@@ -1052,15 +1085,21 @@ __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict
     __shared__ int cnt[2];
     __shared__ int done, fail;
     const unsigned G = gridDim.x;
+    const unsigned base = *T.base;                   // written by the previous Solve (stream order)
+    const int g0 = T.rank * T.rp, g1 = min(nrec, g0 + T.rp);
+    const bool xchg = T.world > 1;
     if (threadIdx.x < 7) x0s[threadIdx.x] = x[threadIdx.x];
     if (threadIdx.x == 0) { done = 0; fail = 0; }
     __syncthreads();
-    for (int pass = 0; pass <= max_iter; pass++) {
+    int pass = 0;
+    for (; pass <= max_iter; pass++) {
+        const unsigned gp = base + (unsigned)pass;
         const double* xs = pass == 0 ? x0s : ls.cand;
         const dquat q{xs[0], xs[1], xs[2], xs[3]};
         const double t[3] = {xs[4], xs[5], xs[6]};
-        double* rb = recs + (size_t)(pass & 1) * nrec * S2M_REC;
-        for (int g = blockIdx.x; g < nrec; g += G) {                   // this workgroup's blocks (k_s2m_pass)
+        const size_t half = (size_t)(gp & 1) * nrec * S2M_REC;
+        double* rb = T.recs + half;
+        for (int g = g0 + blockIdx.x; g < g1; g += G) {               // this workgroup's blocks (k_s2m_pass)
             if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
             __syncthreads();
             double acc[NACC];
@@ -1080,32 +1119,43 @@ __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict
                 if ((threadIdx.x & 63) == 0 && (se | sp)) { atomicAdd(&cnt[0], se); atomicAdd(&cnt[1], sp); }
             }
             block_reduce_acc<CB>(acc, rows, part8, tot);
-            double* rec = rb + (size_t)g * S2M_REC;
-            if (threadIdx.x < NACC) rec[threadIdx.x] = tot[threadIdx.x];
-            if (threadIdx.x == 0) { rec[NACC] = cnt[0]; rec[NACC + 1] = cnt[1]; rec[NACC + 2] = 0.0; }
+            const double v = threadIdx.x < NACC ? tot[threadIdx.x]
+                           : threadIdx.x == NACC ? (double)cnt[0] : threadIdx.x == NACC + 1 ? (double)cnt[1] : 0.0;
+            if (threadIdx.x < NACC + 3) {
+                rb[(size_t)g * S2M_REC + threadIdx.x] = v;
+                if (xchg) T.xrec[T.rank][half + (size_t)g * S2M_REC + threadIdx.x] = v;
+            }
         }
-        // grid barrier: this pass's records of every workgroup stored. Arrivals spread over S2M_BARS counters
+        __syncthreads();
+        if (xchg) {
+            // announce this workgroup's records of pass gp to the peers, wait for theirs, gather this
+            // workgroup's share of the foreign blocks (g = w, w + G, ...; owner g / rp)
+            if (threadIdx.x < WAVE) {
+                if (threadIdx.x == 0) {
+                    __threadfence_system();
+                    __hip_atomic_fetch_add(&T.xarr[T.rank][(blockIdx.x % S2M_BARS) * 32], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                if (!s2m_wait(T.xarr, T.world, T.rank, G, gp, true, err, 0x40000000 | (T.rank << 24) | ((pass & 0xff) << 16) | (int)(gp & 0xffff))) fail = 1;
+            }
+            __syncthreads();
+            if (fail) return;
+            for (int g = blockIdx.x; g < nrec; g += G) {
+                const int owner = g / T.rp;
+                if (owner != T.rank && threadIdx.x < NACC + 3)
+                    rb[(size_t)g * S2M_REC + threadIdx.x] = T.xrec[owner][half + (size_t)g * S2M_REC + threadIdx.x];
+            }
+            __syncthreads();
+        }
+        // local grid barrier: every record of this pass in T.recs. Arrivals spread over S2M_BARS counters
         // (workgroup w on counter w % S2M_BARS, one cache line each), polled by as many lanes of wave 0: one
         // counter for all 256 workgroups serialised their atomics (measured slower than the pass launches)
-        __syncthreads();
         if (threadIdx.x < WAVE) {
             if (threadIdx.x == 0) {
                 __threadfence();
-                atomicAdd(&bar[(blockIdx.x % S2M_BARS) * 32], 1u);
+                atomicAdd(&T.gath[(blockIdx.x % S2M_BARS) * 32], 1u);
             }
-            const int lane = threadIdx.x;
-            const unsigned mine = lane < S2M_BARS ? (G / S2M_BARS + ((unsigned)lane < G % S2M_BARS ? 1u : 0u)) * (unsigned)(pass + 1) : 0u;
-            int spins = 0;
-            while (true) {
-                const unsigned v = lane < S2M_BARS ? __hip_atomic_load(&bar[lane * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                if (!__ballot(v < mine)) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1 << 22)) {
-                    if (lane == 0) { atomicExch(err, 1); fail = 1; }
-                    break;
-                }
-            }
-            __threadfence();
+            const unsigned* own = T.gath;
+            if (!s2m_wait(&own, 1, -1, G, gp, false, err, 0x50000000 | (T.rank << 24) | ((pass & 0xff) << 16) | (int)(gp & 0xffff))) fail = 1;
         }
         __syncthreads();
         if (fail) return;
@@ -1128,21 +1178,34 @@ __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict
             done = ls.done;
         }
         __syncthreads();
-        if (done) break;
+        if (done) { pass++; break; }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int i = 0; i < 7; i++) x[i] = ls.x[i];
         *st_out = ls;
+        *T.base = base + (unsigned)pass;             // passes run (every rank: the same)
     }
 }
 
-void s2m_solve_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int nrec, double* recs, unsigned* bar, double* x,
-                      LMState* st_out, aloam_lm_summary* sum, int* round_cnt) {
-    // every workgroup co-resident (<= 1 per CU, like k_lm_coop), each with nrec / G blocks (one block each on
-    // a full MI355X: the blocks' evaluations are the Solve's work, 64 workgroups x 4 blocks measured slower)
+int s2m_solve_grid(Ctx& C, int world, int rp, bool group) {
+    // every workgroup co-resident (<= 1 per CU, like k_lm_coop), each with rp / G blocks (one block each on
+    // a full MI355X at world 1: the blocks' evaluations are the Solve's work, 64 workgroups x 4 blocks
+    // measured slower). Group mode shares one GPU's CUs among the ranks, and a k_s2m_solve workgroup
+    // holds a whole CU (465 VGPRs + AGPRs: one wave per SIMD): every launch's workgroups are dealt from the
+    // same first CU over the 8 XCDs and then over each XCD's 4 shader arrays, so a rank gets a multiple of
+    // 32 workgroups (the same number on every array). Measured: W x 85 (W = 3) and W x 48 / 40 (W = 5 / 6)
+    // left a rank's last workgroups unplaced (30 per XCD, but 9-10 on one 8-CU array) until the timeout;
+    // multiples of 32 ran at every W from 2 to 8.
     static const int gcap = getenv("ALOAM_S2M_SOLVE_G") ? std::max(1, atoi(getenv("ALOAM_S2M_SOLVE_G"))) : 256;
-    const int G = std::max(1, std::min(std::min(gcap, C.n_cus), nrec));
-    k_s2m_solve<<<G, CB, 0, C.stream>>>(f, nslots, per, nrec, recs, bar, C.d_bar_err, x, st_out, sum,
+    const int share = group ? std::max(32, C.n_cus / std::max(world, 1) / 32 * 32) : C.n_cus;
+    return std::max(1, std::min(std::min(gcap, share), rp));
+}
+
+void s2m_solve_launch(Ctx& C, int G, const aloam_factor* f, int nslots, int per, int nrec, const S2MPeers& T, double* x,
+                      LMState* st_out, aloam_lm_summary* sum, int* round_cnt) {
+    if (T.world < 1 || T.world > S2M_PEER_MAX || T.rank < 0 || T.rank >= T.world || T.rp < 1 || !T.recs || !T.gath || !T.base)
+        throw ApiError{ALOAM_E_STATE, "s2m solve: bad exchange table"};
+    k_s2m_solve<<<G, CB, 0, C.stream>>>(f, nslots, per, nrec, T, C.d_bar_err, x, st_out, sum,
                                         std::min(C.P.max_solver_iterations, 200), round_cnt);
     HIPCHK(hipGetLastError());
 }

@@ -9,7 +9,11 @@
 //   * world 1:   none (the tail reads the local records),
 //   * RCCL:      ncclAllGather on the context's stream (one process per GPU, xGMI),
 //   * group:     peer copies between the streams of contexts driven by one thread
-//                (aloam_s2m_register_group: several ranks on one GPU, or one process over several).
+//                (aloam_s2m_register_group: several ranks on one GPU, or one process over several),
+//   * device:    no host in the exchange at all (aloam_shard_peer_open, or group mode with
+//                ALOAM_S2M_PEER=1): each Solve is ONE persistent launch per rank (k_s2m_solve) whose
+//                workgroups export their records into uncached memory the peers map (IPC over xGMI),
+//                announce them on monotonic arrival counters and gather the peers' records themselves.
 // Because the block decomposition and the reduction order are global, every rank, in every mode and
 // world size, runs the bitwise-identical LM tail.
 #include <dlfcn.h>
@@ -29,12 +33,17 @@ void s2m_pass_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec
                      const LMState* st_in, LMState* st_out, const double* x0, int pass, aloam_lm_summary* sum, int* round_cnt,
                      double* send);
 void s2m_final_launch(Ctx& C, const double* prev, int nrec, const LMState* st_in, double* x, int last_pass, aloam_lm_summary* sum);
-void s2m_solve_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int nrec, double* recs, unsigned* bar, double* x,
+int s2m_solve_grid(Ctx& C, int world, int rp, bool group);
+void s2m_solve_launch(Ctx& C, int G, const aloam_factor* f, int nslots, int per, int nrec, const S2MPeers& T, double* x,
                       LMState* st_out, aloam_lm_summary* sum, int* round_cnt);
 
 constexpr int S2M_REC = 32;                     // doubles per record (k_lm.hip)
 constexpr int NREC = ALOAM_S2M_RECORDS;
 constexpr int RECV_CAP = 2 * NREC;              // world * ceil(NREC / world) <= 2 NREC
+constexpr size_t XR_REC_BYTES = sizeof(double) * 2 * NREC * S2M_REC;           // exported records (2 parities)
+constexpr size_t XR_BYTES = XR_REC_BYTES + sizeof(unsigned) * S2M_BARS * 32;    // + arrival counters
+constexpr size_t GATH_WORDS = S2M_BARS * 32 + 32;                               // local barrier counters + base
+static_assert(ALOAM_PEER_HANDLE_BYTES == sizeof(hipIpcMemHandle_t), "IPC handle size");
 
 struct S2MOut {
     aloam_lm_summary lm[ALOAM_MAX_ROUNDS];
@@ -54,7 +63,11 @@ struct S2M {
     double* d_x = nullptr;                      // [8] parameters (laserMapping.cpp:129)
     double* d_send = nullptr;                   // 2 x NREC records (pass parity: group-mode reuse guard)
     double* d_recv = nullptr;                   // RECV_CAP records
-    unsigned* d_bar = nullptr;                  // [ALOAM_MAX_ROUNDS][16 x 32] grid-barrier counters of the one-launch Solves
+    double* d_lrec = nullptr;                   // one-launch Solves: [2][NREC][32] gathered records
+    unsigned* d_gath = nullptr;                 // GATH_WORDS: local barrier counters, then the pass tally (base)
+    void* d_xr = nullptr;                       // device exchange: exported records + arrival counters (uncached)
+    void* peer_map[S2M_PEER_MAX] = {};          // every rank's d_xr as mapped here (IPC), own at [peer_rank]
+    int peer_world = 0, peer_rank = 0;          // > 0: the device exchange is open (aloam_shard_peer_open)
     S2MOut* d_out = nullptr;
     S2MOut* h_out = nullptr;                    // pinned
     hipEvent_t ev[2] = {nullptr, nullptr};      // group mode: records of this rank ready (per parity)
@@ -117,7 +130,8 @@ static S2M& s2m_of(Ctx& C) {
         S->d_send = (double*)dalloc(C, sizeof(double) * 2 * NREC * S2M_REC);
         S->d_recv = (double*)dalloc(C, sizeof(double) * RECV_CAP * S2M_REC);
         S->d_out = (S2MOut*)dalloc(C, sizeof(S2MOut));
-        S->d_bar = (unsigned*)dalloc(C, sizeof(unsigned) * ALOAM_MAX_ROUNDS * 512);
+        S->d_lrec = (double*)dalloc(C, sizeof(double) * 2 * NREC * S2M_REC);
+        S->d_gath = (unsigned*)dalloc(C, sizeof(unsigned) * GATH_WORDS);
         HIPCHK(hipHostMalloc((void**)&S->h_out, sizeof(S2MOut), hipHostMallocDefault));
         for (auto& e : S->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipMemsetAsync(S->d_recv, 0, sizeof(double) * RECV_CAP * S2M_REC, C.stream));
@@ -125,10 +139,20 @@ static S2M& s2m_of(Ctx& C) {
     return *C.s2m;
 }
 
+static void peer_unmap(S2M& S) {
+    for (int r = 0; r < S2M_PEER_MAX; r++) {
+        if (S.peer_map[r] && S.peer_map[r] != S.d_xr) (void)hipIpcCloseMemHandle(S.peer_map[r]);
+        S.peer_map[r] = nullptr;
+    }
+    S.peer_world = 0;
+}
+
 void s2m_release(Ctx& C) {   // device buffers belong to C.bufs; the rest is released here
     if (C.shard_comm && rccl()) (void)rccl()->comm_destroy((ncclComm_t)C.shard_comm);
     C.shard_comm = nullptr;
     if (!C.s2m) return;
+    peer_unmap(*C.s2m);
+    if (C.s2m->d_xr) (void)hipFree(C.s2m->d_xr);
     for (auto& e : C.s2m->ev) if (e) (void)hipEventDestroy(e);
     if (C.s2m->h_out) (void)hipHostFree(C.s2m->h_out);
     delete C.s2m;
@@ -208,6 +232,40 @@ static void check_ready(Ctx& C) {
 // the map gate of laserMapping.cpp:554
 static bool s2m_gate(const S2M& S) { return S.nc > 10 && S.ns > 50; }
 
+// ---- the device exchange (k_s2m_solve) ----
+static void ensure_xr(Ctx& C, S2M& S) {
+    if (S.d_xr) return;
+    HIPCHK(hipSetDevice(C.device));
+    // uncached: the peers' polls and record reads go to this GPU's HBM over xGMI, never to a stale line
+    HIPCHK(hipExtMallocWithFlags(&S.d_xr, XR_BYTES, hipDeviceMallocUncached));
+    HIPCHK(hipMemsetAsync(S.d_xr, 0, XR_BYTES, C.stream));
+    HIPCHK(hipStreamSynchronize(C.stream));
+}
+// counters and pass tally to zero (the stream is idle after this); every rank of an exchange does it
+// before any of them launches a Solve (group mode: in the call; IPC: aloam_shard_peer_open + the
+// caller's barrier)
+static void reset_exchange(Ctx& C, S2M& S) {
+    HIPCHK(hipSetDevice(C.device));
+    HIPCHK(hipStreamSynchronize(C.stream));
+    HIPCHK(hipMemsetAsync(S.d_gath, 0, sizeof(unsigned) * GATH_WORDS, C.stream));
+    if (S.d_xr) HIPCHK(hipMemsetAsync((char*)S.d_xr + XR_REC_BYTES, 0, XR_BYTES - XR_REC_BYTES, C.stream));
+    HIPCHK(hipStreamSynchronize(C.stream));
+}
+static S2MPeers table_of(S2M& S, int world, int rank, int rp, void* const* xr) {
+    S2MPeers T{};
+    T.recs = S.d_lrec;
+    T.gath = S.d_gath;
+    T.base = S.d_gath + S2M_BARS * 32;
+    T.world = world;
+    T.rank = rank;
+    T.rp = rp;
+    for (int r = 0; r < world && xr; r++) {
+        T.xrec[r] = (double*)xr[r];
+        T.xarr[r] = (unsigned*)((char*)xr[r] + XR_REC_BYTES);
+    }
+    return T;
+}
+
 static void begin(Ctx& C, const double* x) {
     S2M& S = *C.s2m;
     HIPCHK(hipMemsetAsync(S.d_out, 0, sizeof(S2MOut), C.stream));
@@ -220,9 +278,26 @@ static void finish(Ctx& C, int rank, int world, double* x, aloam_s2m_result* out
     HIPCHK(hipMemcpyAsync(xo, S.d_x, sizeof(double) * 7, hipMemcpyDeviceToHost, C.stream));
     HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, sizeof(S2MOut), hipMemcpyDeviceToHost, C.stream));
     HIPCHK(hipStreamSynchronize(C.stream));
-    if (*(volatile int*)C.h_bar_err) {          // a one-launch Solve's grid barrier timed out (results void)
+    if (const int code = *(volatile int*)C.h_bar_err) {   // a one-launch Solve's grid barrier timed out (results void)
         *(volatile int*)C.h_bar_err = 0;
-        throw ApiError{ALOAM_E_HIP, "s2m solve: grid barrier timed out"};
+        if (getenv("ALOAM_S2M_PEER_DEBUG")) {  // the counters as the Solve left them
+            unsigned g[GATH_WORDS], xa[S2M_BARS * 32] = {};
+            HIPCHK(hipMemcpy(g, S.d_gath, sizeof(g), hipMemcpyDeviceToHost));
+            if (S.d_xr) HIPCHK(hipMemcpy(xa, (char*)S.d_xr + XR_REC_BYTES, sizeof(xa), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "s2m timeout ctx %p: first wait given up %s rank %d pass %d gp %d; base %u gath", (void*)&C,
+                         (code >> 28) == 4 ? "peers" : (code >> 28) == 5 ? "local" : "?", (code >> 24) & 15, (code >> 16) & 255,
+                         code & 0xffff, g[S2M_BARS * 32]);
+            for (int c = 0; c < S2M_BARS; c++) std::fprintf(stderr, " %u", g[c * 32]);
+            std::fprintf(stderr, " | arrivals");
+            for (int c = 0; c < S2M_BARS; c++) std::fprintf(stderr, " %u", xa[c * 32]);
+            std::fprintf(stderr, "\n");
+        }
+        // the counters no longer agree between the ranks: a device exchange must be opened again
+        const bool peer = S.peer_world > 0;
+        peer_unmap(S);
+        reset_exchange(C, S);
+        throw ApiError{ALOAM_E_HIP, peer ? "s2m solve: peer exchange timed out (call aloam_shard_peer_open again on every rank)"
+                                         : "s2m solve: grid barrier timed out"};
     }
     if (copy_x) std::memcpy(x, xo, sizeof(xo));
     if (!out) return;
@@ -246,9 +321,10 @@ static void finish(Ctx& C, int rank, int world, double* x, aloam_s2m_result* out
 void s2m_register(Ctx& C, double* x, aloam_s2m_result* out) {
     check_ready(C);
     S2M& S = *C.s2m;
-    const int world = C.shard_world, rank = C.shard_rank;
-    if (world > 1 && !C.shard_comm) throw ApiError{ALOAM_E_STATE, "shard communicator not initialised"};
-    const bool rccl_exchange = C.shard_comm != nullptr;   // world 1 with a communicator: exercises the RCCL path
+    const bool peer = S.peer_world > 0;                   // the device exchange (aloam_shard_peer_open)
+    const int world = peer ? S.peer_world : C.shard_world, rank = peer ? S.peer_rank : C.shard_rank;
+    if (world > 1 && !peer && !C.shard_comm) throw ApiError{ALOAM_E_STATE, "shard communicator not initialised"};
+    const bool rccl_exchange = !peer && C.shard_comm != nullptr;   // world 1 with a communicator: exercises the RCCL path
     const int Q = S.nqc + S.nqs;
     const Slice sl = slice_of(Q, rank, world);
     begin(C, x);
@@ -257,16 +333,17 @@ void s2m_register(Ctx& C, double* x, aloam_s2m_result* out) {
     // vs 2.04 ms per registration, profiles/r05_s2m_persist.txt): a grid barrier per pass costs ~3 us more
     // than the boundary between two queued launches
     static const bool persist = getenv("ALOAM_S2M_PERSIST") && atoi(getenv("ALOAM_S2M_PERSIST")) == 1;
-    const bool one_launch = persist && world == 1 && !rccl_exchange;
+    const bool one_launch = peer || (persist && world == 1 && !rccl_exchange);
     if (s2m_gate(S)) {
         const int rounds = std::min(C.P.map_rounds, ALOAM_MAX_ROUNDS);
         const int max_iter = std::min(C.P.max_solver_iterations, 200);
-        if (one_launch) HIPCHK(hipMemsetAsync(S.d_bar, 0, sizeof(unsigned) * ALOAM_MAX_ROUNDS * 512, C.stream));
+        const S2MPeers T = table_of(S, world, rank, sl.rp, peer ? S.peer_map : nullptr);
+        const int G = one_launch ? s2m_solve_grid(C, world, sl.rp, false) : 0;
         for (int it = 0; it < rounds; it++) {
             s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
                              S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
             if (one_launch) {
-                s2m_solve_launch(C, S.d_f, Q, sl.per, NREC, S.d_send, S.d_bar + 512 * it, S.d_x, S.d_st, &S.d_out->lm[it], S.d_out->cnt[it]);
+                s2m_solve_launch(C, G, S.d_f, Q, sl.per, NREC, T, S.d_x, S.d_st, &S.d_out->lm[it], S.d_out->cnt[it]);
                 continue;
             }
             const double* prev = nullptr;   // the exchanged records of the previous pass
@@ -302,7 +379,47 @@ void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
     }
     for (int r = 0; r < world; r++) { HIPCHK(hipSetDevice(cs[r]->device)); begin(*cs[r], x); }
     const int rp = slice_of(Q, 0, world).rp;
-    if (s2m_gate(S0)) {
+    // ALOAM_S2M_PEER=1: the device exchange between the contexts (direct pointers; one persistent Solve per
+    // rank, G = CUs / world each so that every rank's workgroups are co-resident on a shared GPU). The ranks'
+    // streams must map to distinct hardware queues (GPU_MAX_HW_QUEUES >= 2 x world + 1): a Solve queued
+    // behind a peer's would leave that peer waiting until the exchange times out.
+    static const bool dev_x = getenv("ALOAM_S2M_PEER") && atoi(getenv("ALOAM_S2M_PEER")) == 1;
+    if (dev_x && world <= S2M_PEER_MAX && s2m_gate(S0)) {
+        void* xr[S2M_PEER_MAX] = {};
+        bool one_gpu = true;
+        for (int r = 0; r < world; r++) {
+            Ctx& C = *cs[r];
+            ensure_xr(C, *C.s2m);
+            xr[r] = C.s2m->d_xr;
+            one_gpu &= C.device == cs[0]->device;
+            for (int p = 0; p < world; p++)
+                if (cs[p]->device != C.device) {
+                    const hipError_t e = hipDeviceEnablePeerAccess(cs[p]->device, 0);
+                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+                    (void)hipGetLastError();
+                }
+        }
+        for (int r = 0; r < world; r++) reset_exchange(*cs[r], *cs[r]->s2m);
+        int G = s2m_solve_grid(*cs[0], world, rp, one_gpu);
+        const int rounds = std::min(cs[0]->P.map_rounds, ALOAM_MAX_ROUNDS);
+        for (int it = 0; it < rounds; it++) {
+            for (int r = 0; r < world; r++) {
+                Ctx& C = *cs[r];
+                S2M& S = *C.s2m;
+                const Slice sl = slice_of(Q, r, world);
+                HIPCHK(hipSetDevice(C.device));
+                s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
+                                 S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
+            }
+            for (int r = 0; r < world; r++) {
+                Ctx& C = *cs[r];
+                S2M& S = *C.s2m;
+                HIPCHK(hipSetDevice(C.device));
+                s2m_solve_launch(C, G, S.d_f, Q, slice_of(Q, r, world).per, NREC, table_of(S, world, r, rp, xr), S.d_x, S.d_st,
+                                 &S.d_out->lm[it], S.d_out->cnt[it]);
+            }
+        }
+    } else if (s2m_gate(S0)) {
         const int rounds = std::min(cs[0]->P.map_rounds, ALOAM_MAX_ROUNDS);
         const int max_iter = std::min(cs[0]->P.max_solver_iterations, 200);
         for (int it = 0; it < rounds; it++) {
@@ -347,6 +464,11 @@ void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
             }
         }
     }
+    if (getenv("ALOAM_S2M_PEER_DEBUG"))
+        for (int r = 0; r < world; r++) {
+            HIPCHK(hipStreamSynchronize(cs[r]->stream));
+            std::fprintf(stderr, "rank %d err %08x\n", r, *(volatile int*)cs[r]->h_bar_err);
+        }
     for (int r = 0; r < world; r++) {
         HIPCHK(hipSetDevice(cs[r]->device));
         finish(*cs[r], r, world, x, out ? out + r : nullptr, r == 0);
@@ -379,6 +501,43 @@ void shard_init(Ctx& C, int rank, int world, const unsigned char* id) {
     HIPCHK(hipSetDevice(C.device));
     rcclchk(R->comm_init_rank(&comm, world, u, rank), "ncclCommInitRank");
     C.shard_comm = comm;
+}
+
+void shard_peer_handle(Ctx& C, unsigned char* out) {
+    S2M& S = s2m_of(C);
+    ensure_xr(C, S);
+    hipIpcMemHandle_t h;
+    HIPCHK(hipIpcGetMemHandle(&h, S.d_xr));
+    std::memcpy(out, &h, sizeof(h));
+}
+
+void shard_peer_open(Ctx& C, const unsigned char* handles, int world, int rank) {
+    if (world < 1 || world > S2M_PEER_MAX || rank < 0 || rank >= world || !handles) throw ApiError{ALOAM_E_ARG, "bad rank / world / handles"};
+    S2M& S = s2m_of(C);
+    ensure_xr(C, S);
+    peer_unmap(S);
+    HIPCHK(hipSetDevice(C.device));
+    for (int r = 0; r < world; r++) {
+        if (r == rank) { S.peer_map[r] = S.d_xr; continue; }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)r * sizeof(h), sizeof(h));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            peer_unmap(S);
+            throw ApiError{ALOAM_E_HIP, std::string("hipIpcOpenMemHandle (rank ") + std::to_string(r) + "): " + hipGetErrorString(e)};
+        }
+        S.peer_map[r] = p;
+    }
+    reset_exchange(C, S);
+    S.peer_world = world;
+    S.peer_rank = rank;
+}
+
+void shard_peer_close(Ctx& C) {
+    if (!C.s2m) return;
+    HIPCHK(hipStreamSynchronize(C.stream));
+    peer_unmap(*C.s2m);
 }
 
 int shard_slot_range(int n_slots, int rank, int world, int* begin, int* end) {

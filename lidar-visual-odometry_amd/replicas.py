@@ -68,3 +68,40 @@ def init_shard(ctx, dist=None, uid_fn=None):
     dist.broadcast_object_list(box, src=0)
     ctx.shard_init(rank, world, box[0])
     return rank, world
+
+
+def init_peer_exchange(ctx, dist=None):
+    """Open the device-side record exchange (aloam_shard_peer_open) across the torch.distributed world:
+    every rank publishes its 64-byte IPC handle (ctx.shard_peer_handle()), all-gathers the world's, opens
+    them, then every rank learns every other's outcome (an all-gather that is also the barrier no Solve
+    may start before: every rank has zeroed its counters). Collective; if any rank failed, every rank
+    closes the exchange and RuntimeError is raised on all of them (fall back to init_shard / RCCL)."""
+    if dist is None or not dist.is_initialized():
+        ctx.shard_peer_open([ctx.shard_peer_handle()], 0)
+        return 0, 1
+    rank, world = dist.get_rank(), dist.get_world_size()
+    err = None
+    try:
+        h = ctx.shard_peer_handle()
+    except Exception as e:  # noqa: BLE001 - reported collectively below
+        h, err = None, f"rank {rank}: {e}"
+    handles = [None] * world
+    dist.all_gather_object(handles, h)
+    if err is None:
+        if any(x is None for x in handles):
+            err = f"rank {rank}: a peer has no handle"
+        else:
+            try:
+                ctx.shard_peer_open(handles, rank)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {rank}: {e}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    bad = [e for e in errs if e]
+    if bad:
+        try:
+            ctx.shard_peer_close()
+        except Exception:  # noqa: BLE001
+            pass
+        raise RuntimeError("device exchange unavailable: " + bad[0])
+    return rank, world

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi_version():
     L = lvo.lib()
-    assert L.aloam_abi_version() == 6
+    assert L.aloam_abi_version() == 7
 
 
 def test_struct_layouts_match_header():

@@ -274,3 +274,143 @@ def test_s2m_one_launch_solve_bit_identical():
                          timeout=110, cwd=here)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert out.stdout.strip().splitlines()[-1].startswith("ok")
+
+_PEER_GROUP_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from lvo_amd_loader import lvo
+import test_s2m as T
+wl = T.small_workload()
+x0 = wl[4]
+cm, sm, cq, sq, _, _ = wl
+p = lvo.abi.default_params(128)
+p.max_scan_points, p.max_map_points = max(len(cq) + len(sq), 1024), 1024
+def ctx():
+    c = lvo.Context(p)
+    c.s2m_set_map(cm, sm)
+    c.s2m_set_queries(cq, sq)
+    return c
+g = ctx().s2m_register(x0)                        # world 1, pass launches, no exchange
+for world in (2, 3, 5, 8):
+    ctxs = [ctx() for _ in range(world)]
+    for call in range(2):                         # the counters stay consistent over calls
+        res = lvo.s2m_register_group(ctxs, x0)
+        for r in range(world):
+            assert np.array_equal(g["x"].view(np.uint64), res[r]["x"].view(np.uint64)), (world, r, g["x"], res[r]["x"])
+            assert g["lm"] == res[r]["lm"] and g["surf_num"] == res[r]["surf_num"] and g["corner_num"] == res[r]["corner_num"]
+    del ctxs
+# world 1 through the exchange API (own handle only): the one-launch Solve without a gather
+c = ctx()
+c.shard_peer_open([c.shard_peer_handle()], 0)
+for call in range(2):
+    r1 = c.s2m_register(x0)
+    assert np.array_equal(g["x"].view(np.uint64), r1["x"].view(np.uint64))
+    assert g["lm"] == r1["lm"]
+c.shard_peer_close()
+print("ok", list(g["x"]))
+"""
+
+
+def test_s2m_device_exchange_group_bit_identical():
+    """ALOAM_S2M_PEER=1 (read once per process, so in a child): the group registration runs one persistent
+    Solve per rank whose workgroups exchange the block records themselves (exported uncached records,
+    monotonic arrival counters, k_s2m_solve) — W = 2, 3, 5, 8 ranks sharing one GPU, two calls each: every
+    rank's pose, summaries and counts are bit-identical to the single-context pass launches. The ranks'
+    streams need distinct hardware queues (GPU_MAX_HW_QUEUES=16)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ALOAM_S2M_PEER="1", GPU_MAX_HW_QUEUES="16")
+    out = subprocess.run([sys.executable, "-c", _PEER_GROUP_SCRIPT, here], env=env, capture_output=True, text=True,
+                         timeout=150, cwd=here)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert out.stdout.strip().splitlines()[-1].startswith("ok")
+
+
+_PEER_IPC_SCRIPT = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import torch.distributed as dist
+from lvo_amd_loader import lvo
+import test_s2m as T
+replicas = lvo.replicas
+dist.init_process_group("gloo", init_method="env://")
+rank, world = dist.get_rank(), dist.get_world_size()
+wl = T.small_workload()
+x0 = wl[4]
+cm, sm, cq, sq, _, _ = wl
+p = lvo.abi.default_params(128)
+p.max_scan_points, p.max_map_points = max(len(cq) + len(sq), 1024), 1024
+c = lvo.Context(p)
+c.s2m_set_map(cm, sm)
+c.s2m_set_queries(cq, sq)
+replicas.init_peer_exchange(c, dist)
+out = {"rank": rank, "x": [], "lm": None}
+for call in range(2):
+    r = c.s2m_register(x0)
+    out["x"].append(r["x"].view(np.uint64).tolist())
+    out["lm"] = r["lm"]
+    out["slots"] = [r["slot_begin"], r["slot_end"], r["world"]]
+dist.barrier()
+# a peer that never arrives: rank 0 registers alone, its Solve gives up after ~2 s and closes the exchange
+if rank == 0:
+    try:
+        c.s2m_register(x0)
+        out["timeout"] = "no error"
+    except lvo.ALOAMError as e:
+        out["timeout"] = str(e)
+    out["after"] = c.s2m_register(x0)["x"].view(np.uint64).tolist()   # exchange closed: world-1 path
+    ref = lvo.Context(p)
+    ref.s2m_set_map(cm, sm)
+    ref.s2m_set_queries(cq, sq)
+    g = ref.s2m_register(x0)
+    out["ref_x"] = g["x"].view(np.uint64).tolist()
+    out["ref_lm"] = g["lm"]
+dist.barrier()
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_s2m_peer_exchange_two_processes():
+    """The device exchange across processes (aloam_shard_peer_handle / _open via replicas.init_peer_exchange
+    over a gloo group): 2 ranks, each its own process and context on the one GPU (64 workgroups each),
+    records exchanged through IPC-mapped uncached memory. Both ranks' poses are bit-identical to a
+    no-exchange registration, their slot ranges are the library's decomposition, and a peer that never
+    launches ends the Solve with an error (not a hang) and closes the exchange."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   ALOAM_S2M_SOLVE_G="64")
+        procs.append(subprocess.Popen([sys.executable, "-c", _PEER_IPC_SCRIPT, here], env=env, cwd=here,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            so, se = pr.communicate(timeout=150)
+            assert pr.returncode == 0, so[-2000:] + se[-3000:]
+            outs.append(json.loads([l for l in so.splitlines() if l.startswith("RESULT ")][-1][7:]))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    r0 = outs[0]
+    for o in outs:
+        for xs in o["x"]:
+            assert xs == r0["ref_x"], (o["rank"], xs, r0["ref_x"])
+        assert o["lm"] == r0["ref_lm"]
+    q = len(small_workload()[2]) + len(small_workload()[3])
+    assert [tuple(o["slots"]) for o in outs] == [lvo.shard_slot_range(q, r, 2) + (2,) for r in range(2)]
+    assert "timed out" in r0["timeout"], r0["timeout"]
+    assert r0["after"] == r0["ref_x"]

@@ -93,3 +93,59 @@ def test_init_shard_single_process_needs_no_id():
     c = _FakeCtx()
     assert lvo.replicas.init_shard(c, None) == (0, 1)
     assert c.args == (0, 1, None)
+
+
+class _FakePeerCtx:
+    """Stands in for lvo.Context's device-exchange calls: a rank-stamped 64-byte handle; `fail` makes
+    shard_peer_open raise like a refused IPC mapping."""
+    def __init__(self, rank, fail=False):
+        self.rank, self.fail = rank, fail
+        self.opened, self.closed = None, False
+
+    def shard_peer_handle(self):
+        return bytes([self.rank + 1]) * 64
+
+    def shard_peer_open(self, handles, rank):
+        if self.fail:
+            raise lvo.ALOAMError("hipIpcOpenMemHandle: invalid argument")
+        self.opened = (list(handles), rank)
+
+    def shard_peer_close(self):
+        self.closed = True
+
+
+def _peer_worker(rank, world, port, fail_rank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lvo_amd_loader import lvo as L
+    c = _FakePeerCtx(rank, fail=rank == fail_rank)
+    try:
+        L.replicas.init_peer_exchange(c, dist)
+        err = None
+    except RuntimeError as e:
+        err = str(e)
+    q.put((rank, c.opened, c.closed, err))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_init_peer_exchange_over_gloo(fail_rank):
+    """replicas.init_peer_exchange: every rank opens the world's handles in rank order; one rank's failed
+    open makes EVERY rank close the exchange and raise (the bench then falls back to RCCL together)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_peer_worker, args=(r, world, port, fail_rank, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    handles = [bytes([r + 1]) * 64 for r in range(world)]
+    if fail_rank < 0:
+        assert [r[1] for r in res] == [(handles, r) for r in range(world)]
+        assert all(r[3] is None and not r[2] for r in res)
+    else:
+        assert all(r[3] and "rank 1" in r[3] and r[2] for r in res)
