@@ -582,6 +582,15 @@ __device__ __forceinline__ void lm_tail_fast(LMState* st, const double* tot, int
     }
 }
 
+#ifdef ALOAM_LM_TAIL_NOINLINE   // A/B build: the tail with a register allocation of its own
+__device__ __noinline__ void lm_tail_call(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+    lm_tail_fast(st, tot, pass, xp, out, max_iter);
+}
+#else
+__device__ __forceinline__ void lm_tail_call(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+    lm_tail_fast(st, tot, pass, xp, out, max_iter);
+}
+#endif
 // The same tail on a register copy of the state (one LDS read/write burst instead of dependent LDS
 // round trips inside the step computation).
 __device__ __forceinline__ void lm_tail_reg(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
@@ -866,7 +875,7 @@ __global__ void __launch_bounds__(CB) k_lm_coop(const aloam_factor* __restrict__
         reduce_rows(rows, G, part8, tot);
         LM_TS(pass, 2);
         if (threadIdx.x == 0) {
-            lm_tail_fast(&ls, tot, pass, xl, blockIdx.x == 0 ? out : nullptr, max_iter);
+            lm_tail_call(&ls, tot, pass, xl, blockIdx.x == 0 ? out : nullptr, max_iter);
             done = ls.done;
         }
         __syncthreads();

@@ -381,6 +381,62 @@ def test_knn_build_once_query_many(gpu_ctx_factory):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fine", ["0.3", "0"])
+def test_knn_device_edge_cases_vs_oracle(gpu_ctx_factory, monkeypatch, fine):
+    """aloam_knn_build / _query at the edges the reference's kd-tree meets (laserMapping.cpp:558-559 build,
+    :582/:648 nearestKSearch + the 1 m gate): an empty map (every slot -1), no queries, a one-point map,
+    heavy duplicates (40 copies of each of 50 points: ties by index, the kd-tree restatement's order),
+    queries far outside the map, a map 5 km wide (the cell grows until the grid fits its cap) and k = 8 at
+    r = 2 m; both the two-phase and the single-phase search. Indices equal the oracle's, distances bit for
+    bit where found."""
+    import torch
+    monkeypatch.setenv("ALOAM_KNN_FINE", fine)
+    ctx = gpu_ctx_factory(64)
+    rng = np.random.default_rng(11)
+
+    def gpu(m, q, k, r):
+        dm = torch.from_numpy(np.ascontiguousarray(m, np.float32).reshape(-1, 4)).cuda()
+        dq = torch.from_numpy(np.ascontiguousarray(q, np.float32).reshape(-1, 4)).cuda()
+        idx = torch.full((max(len(q), 1), k), -7, dtype=torch.int32, device="cuda")
+        d2 = torch.full((max(len(q), 1), k), -7.0, dtype=torch.float32, device="cuda")
+        ctx.knn_build(dm.data_ptr() if len(m) else 0, len(m), r)
+        ctx.knn_query(dq.data_ptr() if len(q) else 0, len(q), k, idx.data_ptr(), d2.data_ptr())
+        return idx.cpu().numpy()[:len(q)], d2.cpu().numpy()[:len(q)]
+
+    def check(m, q, k, r, what):
+        gi, gd = gpu(m, q, k, r)
+        oi, od = ob.knn(m, q, k, r) if len(m) else (np.full((len(q), k), -1, np.int32), None)
+        assert np.array_equal(gi, oi), what
+        if od is not None:
+            ok = oi >= 0
+            assert np.array_equal(gd[ok].view(np.uint32), od[ok].view(np.uint32)), what
+        return gi
+
+    def cloud(xyz):
+        a = np.zeros((len(xyz), 4), np.float32)
+        a[:, :3] = xyz
+        return a
+
+    q = cloud(rng.uniform(-3, 3, (500, 3)))
+    assert (check(np.zeros((0, 4), np.float32), q, 5, 1.0, "empty map") == -1).all()
+    gpu(cloud(rng.uniform(-3, 3, (100, 3))), np.zeros((0, 4), np.float32), 5, 1.0)     # no queries: a no-op
+    one = check(cloud(np.array([[0.2, -0.1, 0.3]])), q, 5, 1.0, "one-point map")
+    assert (one[:, 1:] == -1).all() and (one[:, 0] >= 0).any()
+    base = rng.uniform(-2, 2, (50, 3))
+    dup = cloud(np.repeat(base, 40, axis=0)[rng.permutation(2000)])
+    di = check(dup, cloud(base + rng.normal(0, 0.05, base.shape)), 8, 1.0, "duplicates")
+    assert (di[:, 7] >= 0).all()
+    far = q.copy()
+    far[:, 0] += 1e4
+    assert (check(cloud(rng.uniform(-3, 3, (3000, 3))), far, 5, 1.0, "far queries") == -1).all()
+    wide = np.concatenate([rng.uniform(-3, 3, (20000, 3)), rng.uniform(-3, 3, (20000, 3)) + [5000.0, 0.0, 0.0]])
+    qw = np.concatenate([rng.uniform(-3.5, 3.5, (1500, 3)), rng.uniform(-3.5, 3.5, (1500, 3)) + [5000.0, 0.0, 0.0]])
+    wi = check(cloud(wide), cloud(qw), 5, 1.0, "5 km map")
+    assert (wi[:, 4] >= 0).mean() > 0.5
+    check(cloud(rng.uniform(-10, 10, (30000, 3))), cloud(rng.uniform(-11, 11, (2000, 3))), 8, 2.0, "k 8, r 2")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("step,k,radius,frac", [(0.107, 5, 1.0, "0.3"), (0.15, 8, 1.0, "0.2"), (0.5, 5, 1.0, "0.3"),
                                                 (0.107, 3, 0.5, "0.45")])
 def test_knn_device_two_phase_bit_identical(gpu_ctx_factory, monkeypatch, step, k, radius, frac):
