@@ -63,6 +63,7 @@ struct Grid {
     int* rHo = nullptr;
     int* rblk = nullptr;
     unsigned* rbb = nullptr;      // per-tile bbox partials (7 words per tile)
+    int* rcf = nullptr;           // per chunk of the cell-start array: its first run head (k_gr_starts)
     int rcap = 0;
 };
 

@@ -9,6 +9,8 @@
 //
 // Build = counting sort by cell: bbox (ordered-int atomics) -> per-cell counts -> exclusive scan ->
 // scatter (atomic decrement, which leaves the count array zeroed for the next build).
+#include <climits>
+
 #include "aloam_device.hpp"
 #include "aloam_internal.hpp"
 
@@ -153,7 +155,8 @@ void grid_alloc(Ctx& C, Grid& g, int cap, float min_cell, int nlayers, bool w_in
 
 void grid_free(Ctx& C, Grid& g) {
     for (void* p : {(void*)g.desc, (void*)g.cell_count, (void*)g.cell_start, (void*)g.blk, (void*)g.pts, (void*)g.idx, (void*)g.pcell,
-                    (void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk})
+                    (void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk,
+                    (void*)g.rbb, (void*)g.rcf})
         if (p) dfree(C, p);
     g = Grid{};
 }
@@ -315,9 +318,12 @@ void grid_build_multi(Ctx& C, const GridBuild* b, int nj) {
 // exclusive scan of the (digit, tile) counts, and a stable scatter in which each wave ranks its 64 keys of
 // a chunk by 9 ballots (peers with the same digit) and advances its own per-digit run in LDS. No per-point
 // global atomic; inside a cell the points end in original index order, so the built grid is deterministic.
-// Then the sorted copy (gather), each occupied cell's count from its run, the cell scan above, and the
-// counts cleared again. Excluded points (cube gating) take key ncells and sort past the last cell.
+// Then the sorted copy (gather) and the cell starts straight from the sorted keys (k_gr_starts: no per-cell
+// counts, no scan). Excluded points (cube gating) take key ncells and sort past the last cell.
 constexpr int GR_T = 256, GR_PER = 16, GR_TILE = GR_T * GR_PER, GR_BITS = 9, GR_NB = 1 << GR_BITS;
+constexpr int GS_T = 256, GS_PER = 8, GS_CH = GS_T * GS_PER;         // k_gr_starts: cells per chunk
+constexpr int GS_BLOCKS = 1024;                                       // k_gr_starts workgroups per grid (chunks grid-strided)
+constexpr int GS_NCH = GRID_MAX_CELLS_BIG / GS_CH + 2;                // chunks of the largest grid (+ the end cell)
 constexpr int GR_WAVES = GR_T / WAVE, GR_WCH = GR_TILE / GR_WAVES / WAVE;   // chunks of 64 per wave and tile
 static_assert(GR_NB == 2 * GR_T, "k_gr_scatter: two digits per thread in the tile prefix");
 struct GrJob {
@@ -325,6 +331,7 @@ struct GrJob {
     const float4* pts; const int* d_n; const int* cube_of; const unsigned char* cube_valid;
     float min_cell; int nlayers; int w_index; int flat; int max_cells;
     unsigned* k0; unsigned* k1; int* v0; int* v1; int* H; int* Ho; int* Hblk; unsigned* bbp;
+    int* cf;          // first run head per chunk of GS_CH cells (INT_MAX: none), for k_gr_starts
 };
 struct GrJobs { GrJob j[GRID_MULTI_MAX]; };
 __device__ __forceinline__ int gr_tiles(int n) { return (n + GR_TILE - 1) / GR_TILE; }
@@ -431,6 +438,7 @@ __global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
     }
     __syncthreads();
     const GridDesc gd = gds;
+    for (int i = blockIdx.x * GR_T + threadIdx.x; i < GS_NCH; i += gridDim.x * GR_T) g.cf[i] = INT_MAX;   // k_gr_finish fills
     const int n = *g.d_n, nt = gr_tiles(n);
     if ((int)blockIdx.x >= nt) return;
     const int i0 = blockIdx.x * GR_TILE + threadIdx.x;
@@ -587,7 +595,7 @@ __global__ void __launch_bounds__(GR_T) k_gr_scatter(GrJobs J, int pass) {
         dv[pos] = stv[t];
     }
 }
-// sorted copy; each occupied cell's run END + 1 into its count slot (k_gr_counts subtracts the run start)
+// the sorted copy (and the included count published for the searches)
 __global__ void __launch_bounds__(GR_T) k_gr_finish(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
     GridDesc* d = g.desc;
@@ -599,15 +607,15 @@ __global__ void __launch_bounds__(GR_T) k_gr_finish(GrJobs J) {
 #pragma unroll
     for (int h = 0; h < GR_PER; h += 8) {
         int val[8];
-        unsigned key[8], nxt[8];
+        unsigned key[8], prv[8];
         float4 pt[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const int p = p0 + (h + u) * GR_T;
             const bool ok = p < ninc;
-            key[u] = ok ? sk[p] : 0u;
-            nxt[u] = p + 1 < ninc ? sk[p + 1] : 0xffffffffu;
             val[u] = ok ? sv[p] : 0;
+            key[u] = ok ? sk[p] : 0u;
+            prv[u] = ok && p > 0 ? sk[p - 1] : 0xffffffffu;
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) pt[u] = g.pts[val[u]];
@@ -617,34 +625,119 @@ __global__ void __launch_bounds__(GR_T) k_gr_finish(GrJobs J) {
             if (p >= ninc) continue;
             g.spts[p] = g.w_index ? make_float4(pt[u].x, pt[u].y, pt[u].z, __int_as_float(val[u])) : pt[u];
             g.sidx[p] = val[u];
-            if (nxt[u] != key[u]) g.cell_count[key[u]] = p + 1;
+            // a run head: its cell's start + 1 (0: empty, the counts are zero between builds); the first run
+            // head of a chunk of cells (its key's chunk differs from the previous key's) also into cf
+            if (prv[u] != key[u]) g.cell_count[key[u]] = p + 1;
+            if (prv[u] == 0xffffffffu || (int)(key[u] / GS_CH) != (int)(prv[u] / GS_CH)) g.cf[key[u] / GS_CH] = p;
         }
     }
 }
-// run starts: count = (end + 1) - start; clear = 0 (counts back to zero after the cell scan, bbox re-armed)
-template <bool CLEAR>
-__global__ void __launch_bounds__(GR_T) k_gr_runs(GrJobs J) {
+// The cell starts from the run heads, with no scan over the dense cell array: cell_start[c] =
+// lower_bound(keys, c) for c in [0, ncells] (excluded points carry key ncells, so cell_start[ncells] = the
+// included count). k_gr_finish (position-parallel) writes every run head's start + 1 into its cell's count
+// slot (zero between builds) and each chunk's first head into cf; k_gr_cfscan turns cf into every chunk's
+// lower_bound (a suffix minimum); k_gr_starts fills the chunks: a chunk without points is one constant
+// (nothing read), the others read their head slots (clearing them) and take a suffix minimum (an empty cell
+// starts where the next occupied one does, the chunk's last ones at the next chunk's lower_bound). The
+// dense array is read only where points are, not scanned twice and cleared as in the counting build.
+// every chunk's lower_bound: the first recorded head at or after it (ninc if none), by a suffix minimum of
+// the chunk heads in place (one workgroup; <= GS_NCH chunks, GS_NCH / GS_T + 1 per thread)
+constexpr int GS_CPT = GS_NCH / 1024 + 1;
+__global__ void __launch_bounds__(1024) k_gr_cfscan(GrJobs J) {
+    const GrJob& g = J.j[blockIdx.y];
+    __shared__ int wmin[1024 / WAVE];
+    const int nch = g.desc->ncells / GS_CH + 2, ninc = g.desc->n;   // chunk nch - 1: past the end (ninc)
+    const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+    int v[GS_CPT];
+    int bm = INT_MAX;
+#pragma unroll
+    for (int i = 0; i < GS_CPT; i++) {
+        const int jj = t * GS_CPT + i;
+        v[i] = jj < nch - 1 ? g.cf[jj] : (jj == nch - 1 ? ninc : INT_MAX);
+        bm = min(bm, v[i]);
+    }
+    int x = bm;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const int y = __shfl_down(x, off);
+        if (lane + off < WAVE) x = min(x, y);
+    }
+    int after = __shfl_down(x, 1);
+    if (lane == WAVE - 1) after = INT_MAX;
+    if (lane == 0) wmin[w] = x;
+    __syncthreads();
+    int run = after;
+    for (int ww = w + 1; ww < 1024 / WAVE; ww++) run = min(run, wmin[ww]);
+#pragma unroll
+    for (int i = GS_CPT - 1; i >= 0; i--) {
+        run = min(run, v[i]);
+        const int jj = t * GS_CPT + i;
+        if (jj < nch) g.cf[jj] = run;
+    }
+}
+__global__ void __launch_bounds__(GS_T) k_gr_starts(GrJobs J) {
     const GrJob& g = J.j[blockIdx.y];
     GridDesc* d = g.desc;
-    const int npass = d->npass, ninc = d->n;
-    const unsigned* sk = (npass & 1) ? g.k1 : g.k0;
-    const int p0 = blockIdx.x * GR_TILE + threadIdx.x;
-    unsigned key[GR_PER], prv[GR_PER];
+    __shared__ int wmin[GS_T / WAVE];
+    const int nc = d->ncells;
+    const int nch = nc / GS_CH + 1;                       // chunks of cells 0 .. nc
+    const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+    for (int j = blockIdx.x; j < nch; j += gridDim.x) {
+        const int c0 = j * GS_CH, c1 = min(c0 + GS_CH, nc + 1);
+        const int p0 = g.cf[j], p1 = g.cf[j + 1];         // lower_bound(c0), lower_bound(c0 + GS_CH) (k_gr_cfscan)
+        const int cb = c0 + t * GS_PER;
+        const bool whole = cb + GS_PER <= c1;
+        int v[GS_PER];
+        if (p0 == p1) {                                   // no point in the chunk: every cell starts at p0
 #pragma unroll
-    for (int k = 0; k < GR_PER; k++) {
-        const int p = p0 + k * GR_T;
-        key[k] = p < ninc ? sk[p] : 0u;
-        prv[k] = p > 0 && p < ninc ? sk[p - 1] : 0xffffffffu;
-    }
+            for (int i = 0; i < GS_PER; i++) v[i] = p0;
+        } else {                                          // the heads' starts + 1 (k_gr_finish), read and cleared
+            if (whole) {
+                int4* q = (int4*)(g.cell_count + cb);
 #pragma unroll
-    for (int k = 0; k < GR_PER; k++) {
-        const int p = p0 + k * GR_T;
-        if (p < ninc && prv[k] != key[k]) {
-            if (CLEAR) g.cell_count[key[k]] = 0;
-            else g.cell_count[key[k]] -= p;
+                for (int k = 0; k < GS_PER / 4; k++) {
+                    const int4 a = q[k];
+                    v[4 * k] = a.x; v[4 * k + 1] = a.y; v[4 * k + 2] = a.z; v[4 * k + 3] = a.w;
+                    q[k] = make_int4(0, 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < GS_PER; i++) {
+                    v[i] = cb + i < c1 ? g.cell_count[cb + i] : 0;
+                    if (cb + i < c1) g.cell_count[cb + i] = 0;
+                }
+            }
+            int bm = INT_MAX;
+#pragma unroll
+            for (int i = 0; i < GS_PER; i++) { v[i] = v[i] ? v[i] - 1 : INT_MAX; bm = min(bm, v[i]); }
+            // min over the threads after t (in the wave, then the later waves), then p1
+            int x = bm;
+#pragma unroll
+            for (int off = 1; off < WAVE; off <<= 1) {
+                const int y = __shfl_down(x, off);
+                if (lane + off < WAVE) x = min(x, y);
+            }
+            int after = __shfl_down(x, 1);
+            if (lane == WAVE - 1) after = INT_MAX;
+            if (lane == 0) wmin[w] = x;
+            __syncthreads();
+            int carry = p1;
+            for (int ww = w + 1; ww < GS_T / WAVE; ww++) carry = min(carry, wmin[ww]);
+            int run = min(carry, after);
+#pragma unroll
+            for (int i = GS_PER - 1; i >= 0; i--) { run = min(run, v[i]); v[i] = run; }
+            __syncthreads();                              // wmin is reused by the next chunk
+        }
+        if (whole) {
+            int4* q = (int4*)(g.cell_start + cb);
+#pragma unroll
+            for (int k = 0; k < GS_PER / 4; k++) q[k] = make_int4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < GS_PER; i++) if (cb + i < c1) g.cell_start[cb + i] = v[i];
         }
     }
-    if (CLEAR && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && t == 0) {                      // bbox re-armed for the counting build, count cleared
         d->n_acc = 0;
         for (int a = 0; a < 3; a++) { d->bb[a] = 0xffffffffu; d->bb[3 + a] = 0u; }
     }
@@ -653,14 +746,13 @@ __global__ void __launch_bounds__(GR_T) k_gr_runs(GrJobs J) {
 static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
     hipStream_t st = C.stream;
     GrJobs J{};
-    GridJobs GJ{};
     int cap = 1, maxc = 0;
     for (int k = 0; k < nj; k++) {
         Grid& g = *b[k].g;
         const int need = std::max(std::max(b[k].cap_n, g.cap), 1);
         if (g.rcap < need) {
             for (void* p : {(void*)g.rk[0], (void*)g.rk[1], (void*)g.rv[0], (void*)g.rv[1], (void*)g.rH, (void*)g.rHo, (void*)g.rblk,
-                            (void*)g.rbb})
+                            (void*)g.rbb, (void*)g.rcf})
                 if (p) dfree(C, p);
             const int tcap = (need + GR_TILE - 1) / GR_TILE;
             g.rk[0] = (unsigned*)dalloc(C, sizeof(unsigned) * need);
@@ -671,13 +763,12 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
             g.rHo = (int*)dalloc(C, sizeof(int) * ((size_t)GR_NB * tcap + 1));   // + the scan's total
             g.rblk = (int*)dalloc(C, sizeof(int) * SCAN_T * SCAN_CPT);
             g.rbb = (unsigned*)dalloc(C, sizeof(unsigned) * 8 * (size_t)tcap);
+            g.rcf = (int*)dalloc(C, sizeof(int) * GS_NCH);
             g.rcap = need;
         }
         J.j[k] = GrJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, b[k].pts, b[k].d_n, b[k].cube_of, b[k].cube_valid,
                        g.min_cell, g.nlayers, g.w_index ? 1 : 0, g.flat ? 1 : 0, g.max_cells,
-                       g.rk[0], g.rk[1], g.rv[0], g.rv[1], g.rH, g.rHo, g.rblk, g.rbb};
-        GJ.j[k] = GridJob{g.desc, g.cell_count, g.cell_start, g.blk, g.pts, g.idx, g.pcell, b[k].pts, b[k].d_n, b[k].cube_of,
-                          b[k].cube_valid, g.min_cell, g.nlayers, g.w_index ? 1 : 0, g.flat ? 1 : 0, g.max_cells};
+                       g.rk[0], g.rk[1], g.rv[0], g.rv[1], g.rH, g.rHo, g.rblk, g.rbb, g.rcf};
         cap = std::max(cap, b[k].cap_n);
         maxc = std::max(maxc, g.max_cells);
     }
@@ -696,10 +787,8 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
         k_gr_scatter<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
     }
     k_gr_finish<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
-    k_gr_runs<false><<<dim3(tiles, nj), GR_T, 0, st>>>(J);
-    k_gm_scan1<<<dim3(maxc / SCAN_CHUNK, nj), SCAN_T, 0, st>>>(GJ);
-    k_gm_scan3<<<dim3(maxc / SCAN_CHUNK, nj), SCAN_T, 0, st>>>(GJ);
-    k_gr_runs<true><<<dim3(tiles, nj), GR_T, 0, st>>>(J);
+    k_gr_cfscan<<<dim3(1, nj), 1024, 0, st>>>(J);
+    k_gr_starts<<<dim3(GS_BLOCKS, nj), GS_T, 0, st>>>(J);
     HIPCHK(hipGetLastError());
 }
 
