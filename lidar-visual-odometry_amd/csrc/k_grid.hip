@@ -348,7 +348,11 @@ __device__ __forceinline__ unsigned long long gr_peers(int d, bool valid) {
     return m;
 }
 // one LDS atomic per distinct digit of the wave (a tile's keys crowd into few digits in the high passes)
-__device__ __forceinline__ void gr_count(int* hist, int d, bool valid) {
+__device__ __forceinline__ void gr_count(int* hist, int d, bool valid, bool plain = false) {
+    if (plain) {                                   // A/B: one LDS atomic per key
+        if (valid) atomicAdd(&hist[d], 1);
+        return;
+    }
     const unsigned long long m = gr_peers(d, valid);
     if (valid && __popcll(m & lanemask_lt64()) == 0) atomicAdd(&hist[d], __popcll(m));
 }
@@ -472,7 +476,7 @@ __global__ void __launch_bounds__(GR_T) k_gr_keys(GrJobs J) {
     for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
 }
 // digit histogram of pass `pass` (data in k[pass & 1]), 16 keys per thread loaded at once
-__global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass) {
+__global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass, int plain) {
     const GrJob& g = J.j[blockIdx.y];
     if (pass >= g.desc->npass) return;
     __shared__ int hist[GR_NB];
@@ -490,7 +494,7 @@ __global__ void __launch_bounds__(GR_T) k_gr_hist(GrJobs J, int pass) {
     }
 #pragma unroll
     for (int k = 0; k < GR_PER; k++)
-        gr_count(hist, (int)((kk[k] >> sh) & (GR_NB - 1)), blockIdx.x * GR_TILE + k * GR_T + (int)threadIdx.x < n);
+        gr_count(hist, (int)((kk[k] >> sh) & (GR_NB - 1)), blockIdx.x * GR_TILE + k * GR_T + (int)threadIdx.x < n, plain & (1 << pass));
     __syncthreads();
     for (int d = threadIdx.x; d < GR_NB; d += GR_T) g.H[d * nt + blockIdx.x] = hist[d];
 }
@@ -778,10 +782,14 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
     for (int k = 0; k < nj; k++)
         if ((tiles + 0) > (b[k].g->rcap + GR_TILE - 1) / GR_TILE) throw ApiError{ALOAM_E_ARG, "grid_build_radix: tile scratch"};
     const int nsbH = (GR_NB * tiles + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    // A/B knob (read per build): bit p = pass p's histogram with one LDS atomic per key instead of the
+    // ballot-aggregated counts (k_gr_hist, passes 1 and 2)
+    const char* pe = getenv("ALOAM_GR_PLAIN");
+    const int gr_plain = pe ? atoi(pe) : 0;
     k_gr_bbox<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     k_gr_keys<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     for (int pass = 0; pass < 3; pass++) {
-        if (pass > 0) k_gr_hist<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
+        if (pass > 0) k_gr_hist<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass, gr_plain);
         k_gr_hscan1<<<dim3(nsbH, nj), SCAN_T, 0, st>>>(J, pass);
         k_gr_hscan3<<<dim3(nsbH, nj), SCAN_T, 0, st>>>(J, pass);
         k_gr_scatter<<<dim3(tiles, nj), GR_T, 0, st>>>(J, pass);
