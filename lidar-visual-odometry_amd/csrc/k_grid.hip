@@ -782,10 +782,12 @@ static void grid_build_radix(Ctx& C, const GridBuild* b, int nj) {
     for (int k = 0; k < nj; k++)
         if ((tiles + 0) > (b[k].g->rcap + GR_TILE - 1) / GR_TILE) throw ApiError{ALOAM_E_ARG, "grid_build_radix: tile scratch"};
     const int nsbH = (GR_NB * tiles + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    // A/B knob (read per build): bit p = pass p's histogram with one LDS atomic per key instead of the
-    // ballot-aggregated counts (k_gr_hist, passes 1 and 2)
+    // knob (read per build): bit p = pass p's histogram with one LDS atomic per key instead of the
+    // ballot-aggregated counts (k_gr_hist, passes 1 and 2). Default 2: pass 1 plain (its digits are spread:
+    // 20 -> 16 us), pass 2 aggregated (its high digits crowd a tile; plain measured the same),
+    // micro/gr_hist_ab.sh
     const char* pe = getenv("ALOAM_GR_PLAIN");
-    const int gr_plain = pe ? atoi(pe) : 0;
+    const int gr_plain = pe ? atoi(pe) : 2;
     k_gr_bbox<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     k_gr_keys<<<dim3(tiles, nj), GR_T, 0, st>>>(J);
     for (int pass = 0; pass < 3; pass++) {
