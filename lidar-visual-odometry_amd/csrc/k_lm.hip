@@ -957,6 +957,22 @@ __device__ __forceinline__ void s2m_reduce_records(const double* __restrict__ re
     block_reduce_acc<CB>(acc, rows, part8, tot);
 }
 
+// the same for records handed over inside one launch (k_s2m_solve): every load an agent-scope (sc1) 8-byte load,
+// the hand-off form of MI355X_MICROARCH.md's sc1 table (sc1 stores, each storing wave drained before the arrival)
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void s2m_reduce_records_sc1(const double* __restrict__ recs, int nrec, double* rows, double* part8, double* tot) {
+    double acc[NACC];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NACC; i++) acc[i] = t < nrec ? ld_sc1(recs + (size_t)t * S2M_REC + i) : 0.0;
+    block_reduce_acc<CB>(acc, rows, part8, tot);
+}
+
 __global__ void __launch_bounds__(CB) k_s2m_pass(const aloam_factor* __restrict__ f, int nslots, int per, int rec0, int nrec,
                                                  const double* __restrict__ prev, const LMState* __restrict__ st_in,
                                                  LMState* __restrict__ st_out, const double* __restrict__ x0, int pass,
@@ -1079,7 +1095,7 @@ __device__ __forceinline__ bool s2m_wait(const unsigned* const* ctr, int nranks,
             return false;
         }
     }
-    if (sys) __threadfence_system(); else __threadfence();
+    if (sys) __threadfence_system();   // the local hand-off needs none: its stores and loads are sc1
     return true;
 }
 
@@ -1131,7 +1147,7 @@ __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict
             const double v = threadIdx.x < NACC ? tot[threadIdx.x]
                            : threadIdx.x == NACC ? (double)cnt[0] : threadIdx.x == NACC + 1 ? (double)cnt[1] : 0.0;
             if (threadIdx.x < NACC + 3) {
-                rb[(size_t)g * S2M_REC + threadIdx.x] = v;
+                st_sc1(rb + (size_t)g * S2M_REC + threadIdx.x, v);
                 if (xchg) T.xrec[T.rank][half + (size_t)g * S2M_REC + threadIdx.x] = v;
             }
         }
@@ -1151,7 +1167,7 @@ __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict
             for (int g = blockIdx.x; g < nrec; g += G) {
                 const int owner = g / T.rp;
                 if (owner != T.rank && threadIdx.x < NACC + 3)
-                    rb[(size_t)g * S2M_REC + threadIdx.x] = T.xrec[owner][half + (size_t)g * S2M_REC + threadIdx.x];
+                    st_sc1(rb + (size_t)g * S2M_REC + threadIdx.x, T.xrec[owner][half + (size_t)g * S2M_REC + threadIdx.x]);
             }
             __syncthreads();
         }
@@ -1160,18 +1176,22 @@ __global__ void __launch_bounds__(CB) k_s2m_solve(const aloam_factor* __restrict
         // counter for all 256 workgroups serialised their atomics (measured slower than the pass launches)
         if (threadIdx.x < WAVE) {
             if (threadIdx.x == 0) {
-                __threadfence();
-                atomicAdd(&T.gath[(blockIdx.x % S2M_BARS) * 32], 1u);
+                // wave 0 made every record store of this workgroup (sc1): drained, then the arrival
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_fetch_add(&T.gath[(blockIdx.x % S2M_BARS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             const unsigned* own = T.gath;
             if (!s2m_wait(&own, 1, -1, G, gp, false, err, 0x50000000 | (T.rank << 24) | ((pass & 0xff) << 16) | (int)(gp & 0xffff))) fail = 1;
         }
         __syncthreads();
         if (fail) return;
-        s2m_reduce_records(rb, nrec, rows, part8, tot);
+        s2m_reduce_records_sc1(rb, nrec, rows, part8, tot);
         if (pass == 0 && blockIdx.x == 0 && round_cnt) {              // this round's correspondences (pass-0 records)
             int a = 0, b = 0;
-            for (int r = threadIdx.x; r < nrec; r += CB) { a += (int)rb[(size_t)r * S2M_REC + NACC]; b += (int)rb[(size_t)r * S2M_REC + NACC + 1]; }
+            for (int r = threadIdx.x; r < nrec; r += CB) {
+                a += (int)ld_sc1(rb + (size_t)r * S2M_REC + NACC);
+                b += (int)ld_sc1(rb + (size_t)r * S2M_REC + NACC + 1);
+            }
             a = wave_sum_i(a);
             b = wave_sum_i(b);
             if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
