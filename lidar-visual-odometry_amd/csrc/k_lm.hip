@@ -402,9 +402,11 @@ __device__ __forceinline__ void lm_tail(LMState* st, const double* tot, int pass
 // A step that lm_post finds invalid (mcc < 0, StepIsInvalid) is then handled by the next tail exactly
 // as the immediate check would have (radius / decrease_factor, new step, iteration consumed); only its
 // speculative evaluation pass is wasted. Same decisions and state sequence as lm_tail up to rounding.
-__device__ __forceinline__ void chol_solve6_packed(const double* Ml, const double* rhs, double* y, bool* okp) {
-    // Ml: lower triangle packed by rows (i, j <= i) at i(i+1)/2 + j
-    double L[21], inv[6];
+__device__ __forceinline__ void chol_solve6_packed(double* Ml, const double* rhs, double* y, bool* okp) {
+    // Ml: lower triangle packed by rows (i, j <= i) at i(i+1)/2 + j; factored in place (L over M: each
+    // entry is read once, before its own L value is written, so the values and their order are unchanged)
+    double* L = Ml;
+    double inv[6];
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 6; j++) {
@@ -525,11 +527,18 @@ __device__ __forceinline__ void lm_post(LMState* st) {
     st->pending = 0;
 }
 __device__ __forceinline__ void lm_tail_fast(LMState* st, const double* tot, int pass, double* xp, aloam_lm_summary* out, int max_iter) {
+#ifdef ALOAM_LM_TAIL_REGS
     double A[21], g[6];
 #pragma unroll
     for (int i = 0; i < 21; i++) A[i] = tot[i];
 #pragma unroll
     for (int i = 0; i < 6; i++) g[i] = tot[21 + i];
+#else
+    // the normal equations read where they are (LDS) rather than held in 54 registers across the tail: the
+    // same values, fewer spills (k_lm_coop runs at the 256-VGPR limit)
+    const double* A = tot;
+    const double* g = tot + 21;
+#endif
     const double new_cost = tot[27];
     if (pass == 0) {
         #pragma unroll
