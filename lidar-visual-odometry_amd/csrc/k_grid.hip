@@ -652,12 +652,13 @@ __global__ void __launch_bounds__(1024) k_gr_cfscan(GrJobs J) {
     __shared__ int wmin[1024 / WAVE];
     const int nch = g.desc->ncells / GS_CH + 2, ninc = g.desc->n;   // chunk nch - 1: past the end (ninc)
     const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+    const int cpt = (nch + 1023) / 1024;                  // this grid's chunks per thread (<= GS_CPT)
     int v[GS_CPT];
     int bm = INT_MAX;
 #pragma unroll
     for (int i = 0; i < GS_CPT; i++) {
-        const int jj = t * GS_CPT + i;
-        v[i] = jj < nch - 1 ? g.cf[jj] : (jj == nch - 1 ? ninc : INT_MAX);
+        const int jj = t * cpt + i;
+        v[i] = i >= cpt ? INT_MAX : jj < nch - 1 ? g.cf[jj] : (jj == nch - 1 ? ninc : INT_MAX);
         bm = min(bm, v[i]);
     }
     int x = bm;
@@ -675,8 +676,8 @@ __global__ void __launch_bounds__(1024) k_gr_cfscan(GrJobs J) {
 #pragma unroll
     for (int i = GS_CPT - 1; i >= 0; i--) {
         run = min(run, v[i]);
-        const int jj = t * GS_CPT + i;
-        if (jj < nch) g.cf[jj] = run;
+        const int jj = t * cpt + i;
+        if (i < cpt && jj < nch) g.cf[jj] = run;
     }
 }
 __global__ void __launch_bounds__(GS_T) k_gr_starts(GrJobs J) {
