@@ -414,3 +414,45 @@ def test_s2m_peer_exchange_two_processes():
     assert [tuple(o["slots"]) for o in outs] == [lvo.shard_slot_range(q, r, 2) + (2,) for r in range(2)]
     assert "timed out" in r0["timeout"], r0["timeout"]
     assert r0["after"] == r0["ref_x"]
+
+
+_PEER_C4_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import torch
+from lvo_amd_loader import lvo
+cm, sm, cq, sq, x0, x_true = lvo.synth.c4_registration()
+dev = torch.device("cuda", 0)
+dm, dcq, dsq = (torch.from_numpy(a).to(dev) for a in (cm, cq, sq))
+def ctx():
+    p = lvo.abi.default_params(128)
+    p.max_scan_points, p.max_map_points = 1024, 1024
+    c = lvo.Context(p)
+    c.s2m_set_map(dm.data_ptr(), dm.data_ptr(), len(cm), len(sm))
+    c.s2m_set_queries(dcq.data_ptr(), dsq.data_ptr(), len(cq), len(sq))
+    return c
+g = ctx().s2m_register(x0)
+assert np.linalg.norm(g["x"][4:] - x_true[4:]) < 0.02
+for world in (2, 4):
+    res = lvo.s2m_register_group([ctx() for _ in range(world)], x0)
+    for r in res:
+        assert np.array_equal(r["x"].view(np.uint64), g["x"].view(np.uint64)), (world, r["x"], g["x"])
+        assert r["lm"] == g["lm"] and r["surf_num"] == g["surf_num"] and r["corner_num"] == g["corner_num"]
+print("ok")
+"""
+
+
+def test_s2m_device_exchange_c4_full_size():
+    """BASELINE configs[3] at full size (the 128-line sweep against the ~2.1M-point map) through the device
+    exchange (ALOAM_S2M_PEER=1, W = 2 and 4 contexts on one GPU): every rank's pose, LM summaries and counts
+    are bit-identical to the single-context registration, which recovers the true pose."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ALOAM_S2M_PEER="1", GPU_MAX_HW_QUEUES="16")
+    out = subprocess.run([sys.executable, "-c", _PEER_C4_SCRIPT, here], env=env, capture_output=True, text=True,
+                         timeout=170, cwd=here)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert out.stdout.strip().splitlines()[-1] == "ok"
