@@ -149,3 +149,10 @@ def test_init_peer_exchange_over_gloo(fail_rank):
         assert all(r[3] is None and not r[2] for r in res)
     else:
         assert all(r[3] and "rank 1" in r[3] and r[2] for r in res)
+
+
+def test_init_peer_exchange_single_process_opens_own_handle():
+    """Without a process group the device exchange is world 1: the context's own handle, rank 0."""
+    c = _FakePeerCtx(0)
+    assert lvo.replicas.init_peer_exchange(c, None) == (0, 1)
+    assert c.opened == ([bytes([1]) * 64], 0)
