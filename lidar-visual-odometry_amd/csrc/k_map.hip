@@ -538,10 +538,13 @@ __global__ void __launch_bounds__(256) k_s2m_assoc(const float4* __restrict__ cs
 // neighbour positions (+ found | fine-copy flag) in global memory, then k_s2m_fit fits one slot per lane
 // — the same fit_factor on the same neighbours, so the same factor records as the fused kernel.
 constexpr int S2M_NBR = 8;          // ints per parked slot: 5 positions, flags, pad
+// The 5-NN of the split path as 64-bit (d2, original index) keys (group_knn27_keys, the C4 search's loop: row bounds
+// in registers, branch-free top-5 insertion), fine 3x3x3 block first, the coarse block for the unsettled with phase
+// 1's 5th key as the bound. Same neighbours in the same (d2, index) order as knn5_fine_coarse, parked as ORIGINAL
+// map indices (the grids carry them in w): k_s2m_fit reads the map arrays themselves.
 __global__ void __launch_bounds__(256) k_s2m_knn(const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc,
                                                  int s0, int s1, const double* __restrict__ x, KindGrids fc, KindGrids fs,
                                                  KindGrids cc, KindGrids cs, int use_fine, int* __restrict__ nbr) {
-    __shared__ int tabs[256 / AG][20];
     double par[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) par[i] = x[i];
@@ -554,36 +557,61 @@ __global__ void __launch_bounds__(256) k_s2m_knn(const float4* __restrict__ csta
         const int li = corner ? qi : qi - nc;
         const float4 po = live ? (corner ? cstack[li] : sstack[li]) : make_float4(0, 0, 0, 0);
         const float4 sel = associate_to_map(par, po);
-        int pos[5];
-        const float4* sp;
-        const int found = knn5_fine_coarse(fc, fs, cc, cs, use_fine != 0, corner, sel, live, pos, &sp, tabs[threadIdx.x / AG]);
+        unsigned long long key[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) key[k] = ~0ull;
+        int found = 0;
+        bool need = live;
+        if (use_fine) {                                   // kernel-uniform
+            const KindGrids& f = corner ? fc : fs;
+            const GridDesc gd = *f.gd;
+            found = group_knn27_keys<5, AG, 4, false>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, f.cs, f.sp, sel.x, sel.y,
+                                                      sel.z, 1.0f, live, key, nullptr, gd.n);
+            const float lim = 0.99f * gd.cell;
+            const float d4 = key[4] == ~0ull ? INFINITY : __uint_as_float((unsigned)(key[4] >> 32));
+            need = live && !(found == 5 && d4 < lim * lim);
+        }
+        if (__any(need)) {                                // wave-uniform: every lane takes part in the group search
+            const KindGrids& c = corner ? cc : cs;
+            const GridDesc gd = *c.gd;
+            unsigned long long k2[5];
+            const int f2 = group_knn27_keys<5, AG, 4, false>(gd.ox, gd.oy, gd.oz, gd.inv_cell, gd.dx, gd.dy, gd.dz, c.cs, c.sp, sel.x,
+                                                             sel.y, sel.z, 1.0f, need, k2, nullptr, gd.n, key[4]);
+            if (need) {
+#pragma unroll
+                for (int k = 0; k < 5; k++) key[k] = k2[k];
+                found = f2;
+            }
+        }
         if (live && (lane_id() & (AG - 1)) == 0) {
             int* o = nbr + (size_t)(qi - s0) * S2M_NBR;
-            *(int4*)o = make_int4(pos[0], pos[1], pos[2], pos[3]);
-            *(int4*)(o + 4) = make_int4(pos[4], found | ((use_fine && sp == (corner ? fc.sp : fs.sp)) ? 256 : 0), 0, 0);
+            int ix[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) ix[k] = key[k] == ~0ull ? -1 : (int)(unsigned)key[k];
+            *(int4*)o = make_int4(ix[0], ix[1], ix[2], ix[3]);
+            *(int4*)(o + 4) = make_int4(ix[4], found, 0, 0);
         }
     }
 }
+// one slot per lane: the fit on the parked neighbours, read from the map arrays by original index
 __global__ void __launch_bounds__(256) k_s2m_fit(const float4* __restrict__ cstack, const float4* __restrict__ sstack, int nc,
-                                                 int s0, int s1, KindGrids fc, KindGrids fs, KindGrids cc, KindGrids cs,
+                                                 int s0, int s1, const float4* __restrict__ cmap, const float4* __restrict__ smap,
                                                  const int* __restrict__ nbr, aloam_factor* __restrict__ out) {
     for (int qi = s0 + blockIdx.x * blockDim.x + threadIdx.x; qi < s1; qi += gridDim.x * blockDim.x) {
         const int* o = nbr + (size_t)(qi - s0) * S2M_NBR;
         const int4 a = *(const int4*)o, b = *(const int4*)(o + 4);
         const int pos[5] = {a.x, a.y, a.z, a.w, b.x};
-        const int fl = b.y;
         const bool corner = qi < nc;
         const float4 po = corner ? cstack[qi] : sstack[qi - nc];
-        const float4* sp = (fl & 256) ? (corner ? fc.sp : fs.sp) : (corner ? cc.sp : cs.sp);
         aloam_factor f;
         f.type = -1; f.pad = 0;
-        if ((fl & 255) == 5) fit_factor(corner, po, sp, pos, f);
+        if (b.y == 5) fit_factor(corner, po, corner ? cmap : smap, pos, f);
         out[qi] = f;
     }
 }
 
 void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
-                      const Grid* gcf, const Grid* gsf, aloam_factor* out) {
+                      const Grid* gcf, const Grid* gsf, const float4* cmap, const float4* smap, aloam_factor* out) {
     if (s1 <= s0) return;
     // regime threshold (tests force either path). Default 1: the split 5-NN / fit kernels at any slot count —
     // a rank's share at world 4 / 8 (65k / 33k slots) runs 4.65 / 13.55 ms per group registration on one GPU
@@ -607,7 +635,7 @@ void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0
         const int waves = (n + WAVE / AG - 1) / (WAVE / AG);
         k_s2m_knn<<<std::max(1, std::min(16384, (waves + 3) / 4)), 256, 0, C.stream>>>(cq, sq, nc, s0, s1, d_x, fc, fs, cc, cs,
                                                                                       fine, C.d_s2m_nbr);
-        k_s2m_fit<<<std::max(1, std::min(4096, (n + 255) / 256)), 256, 0, C.stream>>>(cq, sq, nc, s0, s1, fc, fs, cc, cs,
+        k_s2m_fit<<<std::max(1, std::min(4096, (n + 255) / 256)), 256, 0, C.stream>>>(cq, sq, nc, s0, s1, cmap, smap,
                                                                                       C.d_s2m_nbr, out);
     } else if (s1 - s0 >= batch_min) {   // throughput regime: 8 NB points per wave pass, fits on 8 NB lanes
         const char* nbe = getenv("ALOAM_S2M_NB");                    // tuning knob: 2, 4, 8

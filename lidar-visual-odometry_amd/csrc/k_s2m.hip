@@ -28,7 +28,7 @@
 namespace aloam {
 
 void s2m_assoc_launch(Ctx& C, const float4* cq, const float4* sq, int nc, int s0, int s1, const double* d_x, Grid& gc, Grid& gs,
-                      const Grid* gcf, const Grid* gsf, aloam_factor* out);
+                      const Grid* gcf, const Grid* gsf, const float4* cmap, const float4* smap, aloam_factor* out);
 void s2m_pass_launch(Ctx& C, const aloam_factor* f, int nslots, int per, int rec0, int nrec_local, int nrec, const double* prev,
                      const LMState* st_in, LMState* st_out, const double* x0, int pass, aloam_lm_summary* sum, int* round_cnt,
                      double* send);
@@ -341,7 +341,7 @@ void s2m_register(Ctx& C, double* x, aloam_s2m_result* out) {
         const int G = one_launch ? s2m_solve_grid(C, world, sl.rp, false) : 0;
         for (int it = 0; it < rounds; it++) {
             s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
-                             S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
+                             S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_mc, S.shared ? S.d_mc : S.d_ms, S.d_f);
             if (one_launch) {
                 s2m_solve_launch(C, G, S.d_f, Q, sl.per, NREC, T, S.d_x, S.d_st, &S.d_out->lm[it], S.d_out->cnt[it]);
                 continue;
@@ -409,7 +409,7 @@ void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
                 const Slice sl = slice_of(Q, r, world);
                 HIPCHK(hipSetDevice(C.device));
                 s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
-                                 S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
+                                 S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_mc, S.shared ? S.d_mc : S.d_ms, S.d_f);
             }
             for (int r = 0; r < world; r++) {
                 Ctx& C = *cs[r];
@@ -429,7 +429,7 @@ void s2m_register_group(Ctx** cs, int world, double* x, aloam_s2m_result* out) {
                 const Slice sl = slice_of(Q, r, world);
                 HIPCHK(hipSetDevice(C.device));
                 s2m_assoc_launch(C, S.d_qc, S.d_qs, S.nqc, sl.s0, sl.s1, S.d_x, S.gc, S.shared ? S.gc : S.gs, S.fine ? &S.gcf : nullptr,
-                             S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_f);
+                             S.fine ? (S.shared ? &S.gcf : &S.gsf) : nullptr, S.d_mc, S.shared ? S.d_mc : S.d_ms, S.d_f);
             }
             for (int pass = 0; pass <= max_iter; pass++) {
                 const int parity = pass & 1;
