@@ -992,6 +992,12 @@ __global__ void __launch_bounds__(CB) k_s2m_pass(const aloam_factor* __restrict_
     __shared__ LMState ls;
     __shared__ double xl[7];
     __shared__ int cnt[2];
+    double* rec = send + (size_t)blockIdx.x * S2M_REC;
+    if (pass > 1 && st_in->done) {               // the Solve ended before the previous pass: nothing to reduce or
+        if (threadIdx.x < S2M_REC) rec[threadIdx.x] = 0.0;   // evaluate; the state carried to the next buffer
+        if (blockIdx.x == 0 && threadIdx.x == 0) *st_out = *st_in;
+        return;
+    }
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
     if (pass > 0) {
         if (threadIdx.x == 0) ls = *st_in;
@@ -1018,7 +1024,6 @@ __global__ void __launch_bounds__(CB) k_s2m_pass(const aloam_factor* __restrict_
         __syncthreads();
         if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
     }
-    double* rec = send + (size_t)blockIdx.x * S2M_REC;
     const int g = rec0 + blockIdx.x;
     if ((pass > 0 && ls.done) || g >= nrec) {                    // uniform: the same state everywhere
         if (threadIdx.x < S2M_REC) rec[threadIdx.x] = 0.0;
@@ -1056,6 +1061,10 @@ __global__ void __launch_bounds__(CB) k_s2m_final(const double* __restrict__ pre
     __shared__ double tot[NACC];
     __shared__ LMState ls;
     __shared__ double xl[7];
+    if (last_pass > 0 && st_in->done) {          // ended earlier: the parameters are the state's
+        if (threadIdx.x < 7) x[threadIdx.x] = st_in->x[threadIdx.x];
+        return;
+    }
     if (threadIdx.x == 0) ls = *st_in;
     s2m_reduce_records(prev, nrec, rows, part8, tot);
     if (threadIdx.x == 0) {
